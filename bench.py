@@ -1,0 +1,170 @@
+"""Benchmark: Mray/s + ms/frame at 1920x1080, 64 spp (BASELINE.json metric) on the
+C3 `dragon1m` scene (1,000,000-triangle BVH, mirror + dielectric spheres, Whitted depth 6).
+
+One step = one full frame.  With N ranks (torch.distributed.run, one GPU each) every rank
+renders the rows y % N == rank into a zero-initialised full-frame accumulator and the
+frames are summed onto rank 0 with one RCCL reduce (exact: disjoint pixel support).
+value = rays traced by all ranks / max-over-ranks frame time.
+
+Prints ONE JSON line (rank 0).  Extra objects:
+  roofline     dominant kernel k_trace (closest hit), algorithmic bytes per launch from the
+               SURVEY §8(d) model B = 64 + 32*N_node + 36*N_tri per ray (N_* measured by a
+               stats frame outside the timed region), divided by its HIP-event launch time.
+  cpu_baseline the CPU restatement (oracle/) on a bounded row sample of the same frame.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raytracer-795_amd"))
+
+METRIC = "Mray/s + ms/frame at 1920×1080, 64 spp; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(scene, rows: int, threads: int) -> dict:
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    cam = scene.cameras[0]
+    o = pyoracle.Oracle(scene)
+    y0 = cam.ny // 2 - rows // 2
+    t0 = time.perf_counter()
+    o.render(0, nthreads=threads, row_begin=y0, row_end=y0 + rows)
+    dt = time.perf_counter() - t0
+    c = o.ray_counts()
+    nrays = c["primary"] + c["secondary"] + c["shadow"]
+    o.close()
+    return {"value": nrays / dt / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"rows {y0}..{y0 + rows - 1} of the same 1920x1080x{cam.num_samples}spp frame "
+                      f"({rows * cam.nx} px, {nrays} rays, {dt:.1f} s, literal visit-both-children BVH)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--cpu-rows", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    import rtg
+    from rtg import scenegen
+
+    t0 = time.perf_counter()
+    scene = scenegen.dragon1m(args.width, args.height, spp=args.spp)
+    log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
+    t0 = time.perf_counter()
+    r = rtg.Renderer(scene, device=local)
+    log(f"[rank {rank}] rtg_scene_create (BVH build + upload) {time.perf_counter() - t0:.1f}s")
+    cam = scene.cameras[0]
+    frame = torch.zeros((cam.ny, cam.nx, 3), dtype=torch.float32, device=f"cuda:{local}")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(**kw):
+        r.render_device(0, frame.data_ptr(), stream, row_offset=rank, row_stride=world, **kw)
+        st = r.stats()
+        if dist is not None:
+            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+        return st
+
+    # traversal statistics for the roofline model (outside the timed region)
+    st_stats = step(collect_stats=1)
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rays = 0
+    trace_ms = 0.0
+    trace_launches = 0
+    trace_rays = 0
+    for i in range(args.steps):
+        st = step(collect_timing=1)
+        rays += st["total_rays"]
+        trace_ms += st["trace_ms"]
+        trace_launches += st["trace_launches"]
+        trace_rays += st["primary_rays"] + st["secondary_rays"]
+        log(f"[rank {rank}] step {i}: {st['render_ms']:.1f} ms device, rays {st['total_rays']}")
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=frame.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        rt = torch.tensor([rays], dtype=torch.float64, device=frame.device)
+        dist.all_reduce(rt, op=dist.ReduceOp.SUM)
+        rays = int(rt.item())
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = rays / elapsed / 1e6
+    # roofline of the dominant kernel (closest-hit trace)
+    traced = st_stats["primary_rays"] + st_stats["secondary_rays"]
+    n_node = st_stats["node_visits"] / max(traced, 1)
+    n_tri = st_stats["tri_tests"] / max(traced, 1)
+    bytes_per_ray = 64 + 32 * n_node + 36 * n_tri
+    avg_launch_ms = trace_ms / max(trace_launches, 1)
+    bytes_per_launch = bytes_per_ray * trace_rays / max(trace_launches, 1)
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "k_trace<false,false> (closest hit, primary+secondary)",
+            "avg_launch_ms": round(avg_launch_ms, 3), "launches": trace_launches,
+            "bytes_per_ray": round(bytes_per_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),
+            "trace_share_of_frame": round(trace_ms / max(args.steps * ms_per_step, 1e-9), 3)}
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            log("[rank 0] cpu baseline ...")
+            cpu = cpu_baseline(scene, args.cpu_rows, args.cpu_threads)
+        line = {"metric": METRIC, "value": round(value, 2), "unit": "Mray/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic (scenegen.dragon1m, seed 20261015)",
+                "config": {"workload": "C3 dragon1m: 1,000,004-triangle BVH + mirror & dielectric spheres, "
+                                       "point light, Whitted depth 6",
+                           "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
+                           "parallelism": f"row-interleaved pixel shards x{world} + RCCL reduce"},
+                "rays_per_frame": rays // max(args.steps, 1),
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,288 @@
+/*
+ * rtg.h — C ABI of the MI355X-native render loop for the CENG795 XML ray tracer
+ * (badiba/raytracer-795).  Plain C, plain pointers and sizes, no C++/torch types.
+ *
+ * Drop-in seam:
+ *   reference  void Scene::renderScene(void)                       src/Scene.h:89, src/Scene.cpp:425-494
+ *   reference  ReturnVal BVHMethods::FindIntersection(ray,objs,inst) src/Helper.h:25, src/Helper.cpp:72-134
+ *
+ *   rtg_scene_create()  replaces the precompute half of renderScene()
+ *                        (Perlin table, ComputeObjectTransformations, smooth normals,
+ *                        per-object BVH construction: src/Scene.cpp:427-458)
+ *   rtg_render()        replaces the per-camera pixel loop of renderScene()
+ *                        (8 std::threads of ThreadedRendering -> Single/MultiSample ->
+ *                        Shading: src/Scene.cpp:461-488, 400-423, 496-542) and writes
+ *                        the float RGB framebuffer the reference keeps in Image::_data
+ *                        (src/Image.cpp:176-184) — [y][x][c], 0..255 scale, unclamped.
+ *   rtg_trace_closest() replaces BVHMethods::FindIntersection for a batch of rays
+ *                        (closest-hit with the reference's object/instance rules).
+ *
+ * The scene descriptor is exactly what the reference Parser leaves in the global
+ * Scene after `new Scene(xml)` (src/Scene.cpp:586-634, src/Parser.h): raw vertices,
+ * texture coordinates, objects with their transformation-reference lists, instances,
+ * materials, textures (decoded texels), lights in the reference's light order, scalars.
+ * All indices keep the reference's conventions: vertex / material / texture indices
+ * are 1-based positions (materials[matIndex-1], src/Scene.cpp:506; vertices[idx-1],
+ * src/Shape.cpp:232), transformation ids are 1-based positions into the per-kind lists
+ * (src/Helper.cpp:212).
+ *
+ * Every function returns RTG_OK (0) or a negative rtg_status; rtg_last_error() returns
+ * a thread-local message.  Nothing throws or aborts.  The library copies all inputs to
+ * device memory at create time and keeps no pointer into caller memory after return.
+ */
+#ifndef RTG_H_
+#define RTG_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTG_ABI_VERSION 1
+
+typedef enum rtg_status {
+    RTG_OK = 0,
+    RTG_ERR_INVALID = -1,   /* malformed descriptor / argument */
+    RTG_ERR_NO_DEVICE = -2, /* no usable gfx950 device */
+    RTG_ERR_OOM = -3,       /* device or host allocation failed */
+    RTG_ERR_HIP = -4,       /* HIP runtime error (message in rtg_last_error) */
+    RTG_ERR_UNSUPPORTED = -5
+} rtg_status;
+
+/* ---- enums mirror src/defs.h:8-11, src/Material.h:8-9, src/Light.h:12, src/Transformation.h:8 ---- */
+typedef enum rtg_object_type { RTG_OBJ_SPHERE = 0, RTG_OBJ_TRIANGLE = 1, RTG_OBJ_MESH = 2 } rtg_object_type;
+typedef enum rtg_xform_type {
+    RTG_XF_TRANSLATION = 1, RTG_XF_SCALING = 2, RTG_XF_ROTATION = 3, RTG_XF_COMPOSITE = 4
+} rtg_xform_type;
+typedef enum rtg_material_type {
+    RTG_MAT_NORMAL = 0, RTG_MAT_MIRROR = 1, RTG_MAT_CONDUCTOR = 2, RTG_MAT_DIELECTRIC = 3
+} rtg_material_type;
+/* BRDFType order of src/Material.h:9 */
+typedef enum rtg_brdf_type {
+    RTG_BRDF_NONE = 0, RTG_BRDF_OBP = 1, RTG_BRDF_MBP = 2, RTG_BRDF_MBPN = 3, RTG_BRDF_OP = 4,
+    RTG_BRDF_MP = 5, RTG_BRDF_MPN = 6, RTG_BRDF_TS = 7, RTG_BRDF_TSF = 8
+} rtg_brdf_type;
+/* DecalMode order of src/defs.h:8 */
+typedef enum rtg_decal_mode {
+    RTG_DECAL_REPLACE_KD = 0, RTG_DECAL_BLEND_KD = 1, RTG_DECAL_BUMP_NORMAL = 2,
+    RTG_DECAL_REPLACE_NORMAL = 3, RTG_DECAL_REPLACE_ALL = 4, RTG_DECAL_REPLACE_BACKGROUND = 5,
+    RTG_DECAL_NONE = 6
+} rtg_decal_mode;
+typedef enum rtg_interp { RTG_INTERP_NN = 0, RTG_INTERP_BILINEAR = 1 } rtg_interp;
+typedef enum rtg_texture_kind { RTG_TEX_IMAGE = 0, RTG_TEX_PERLIN = 1 } rtg_texture_kind;
+typedef enum rtg_noise_conv { RTG_NC_ABSVAL = 0, RTG_NC_LINEAR = 1, RTG_NC_NONE = 2 } rtg_noise_conv;
+/* lights are given in the order the reference pushes them (src/Parser.h:1223-1314):
+   all Point, then Directional, Spot, Area, SphericalDirectional (environment). */
+typedef enum rtg_light_type {
+    RTG_LIGHT_POINT = 0, RTG_LIGHT_AREA = 1, RTG_LIGHT_DIRECTIONAL = 2, RTG_LIGHT_SPOT = 3,
+    RTG_LIGHT_ENVIRONMENT = 4
+} rtg_light_type;
+
+/* One entry of an object's <Transformations> list, e.g. "t1 s2 r1" (src/Parser.h:763-791).
+   index is the 1-based position in the list of that kind. */
+typedef struct rtg_xform_ref { int32_t type; int32_t index; } rtg_xform_ref;
+
+typedef struct rtg_object_desc {
+    int32_t type;            /* rtg_object_type */
+    int32_t id;              /* XML id (MeshInstance baseMeshId lookup, src/Parser.h:1181-1186) */
+    int32_t material;        /* 1-based material position */
+    int32_t num_textures;    /* 0..2 (src/Parser.h:830-853) */
+    int32_t textures[2];     /* 1-based texture positions */
+    int32_t texture_offset;  /* Mesh: xml textureOffset - vertexOffset (src/Parser.h:1147); others 0 */
+    int32_t smooth;          /* Mesh shadingMode="smooth" (src/Parser.h:958-974); ignored otherwise */
+    int32_t xform_first;     /* range in rtg_scene_desc.xform_refs */
+    int32_t xform_count;
+    float blur[3];           /* MotionBlur translation (src/Parser.h:856-861), 0 if absent */
+    /* sphere */
+    int32_t center;          /* 1-based vertex index */
+    float radius;
+    /* triangle */
+    int32_t v[3];            /* 1-based vertex indices */
+    /* mesh */
+    int32_t face_first;      /* range in rtg_scene_desc.faces (triples of 1-based vertex indices,
+                                vertexOffset already added: src/Parser.h:1112-1139) */
+    int32_t face_count;
+} rtg_object_desc;
+
+typedef struct rtg_instance_desc {
+    int32_t base_object;     /* 0-based index into objects (a Mesh) */
+    int32_t id;
+    int32_t material;        /* 1-based; overrides the base mesh material (src/Helper.cpp:122) */
+    int32_t reset_transform; /* src/Helper.cpp:270-272 */
+    int32_t xform_first;
+    int32_t xform_count;
+    float blur[3];
+} rtg_instance_desc;
+
+typedef struct rtg_material_desc {   /* src/Material.h:11-34, src/Parser.h:304-472 */
+    int32_t type;            /* rtg_material_type */
+    int32_t brdf;            /* rtg_brdf_type */
+    int32_t phong_exp;
+    int32_t is_rough;
+    float roughness;
+    float ambient[3];
+    float diffuse[3];
+    float specular[3];
+    float mirror[3];
+    float refraction_index;
+    float absorption_index;
+    float absorption_coeff[3];
+} rtg_material_desc;
+
+typedef struct rtg_texture_desc {    /* src/Texture.h:13-51 */
+    int32_t kind;            /* rtg_texture_kind */
+    int32_t decal;           /* rtg_decal_mode */
+    int32_t interp;          /* rtg_interp */
+    int32_t noise_conv;      /* rtg_noise_conv (Perlin) */
+    int32_t normalizer;
+    float noise_scale;
+    float bump_factor;
+    int32_t width;           /* image textures: texels is width*height*3 floats, */
+    int32_t height;          /* row j=0 first, [j][i][c] — the values GetColorAtPixel returns */
+    const float* texels;     /* (raw 0..255 for PNG/JPG, linear floats for EXR). */
+} rtg_texture_desc;
+
+typedef struct rtg_light_desc {      /* src/Light.h:35-139 */
+    int32_t type;            /* rtg_light_type */
+    float position[3];       /* point/spot/area */
+    float direction[3];      /* directional/spot direction; area normal (normalized by the library) */
+    float intensity[3];      /* point/spot intensity; directional/area radiance */
+    float coverage_deg;      /* spot CoverageAngle */
+    float falloff_deg;       /* spot FalloffAngle */
+    float size;              /* area Size */
+    int32_t texture;         /* environment: 0-based index into rtg_scene_desc.textures
+                                (a bilinear, normalizer-1 image texture) */
+} rtg_light_desc;
+
+typedef struct rtg_scene_desc {
+    int32_t abi_version;     /* RTG_ABI_VERSION */
+    int32_t max_recursion_depth;   /* src/Parser.h:23 default 1 */
+    float shadow_ray_eps;          /* default 0.002 */
+    float intersection_test_eps;   /* default 0.001 */
+    float background[3];
+    float ambient_light[3];
+    int32_t background_texture;    /* 0-based texture index with decal replace_background, -1 none
+                                      (last such texture, src/Scene.cpp:625-631) */
+    int32_t environment_light;     /* 0-based light index, -1 none (src/Parser.h:1302-1313) */
+
+    const float* vertices;   int32_t num_vertices;    /* xyz triples */
+    const float* texcoords;  int32_t num_texcoords;   /* uv pairs */
+    const int32_t* faces;    int32_t num_faces;       /* mesh face triples (1-based vertex idx) */
+    const float* translations; int32_t num_translations;  /* xyz */
+    const float* scalings;   int32_t num_scalings;        /* xyz */
+    const float* rotations;  int32_t num_rotations;       /* angle_deg, x, y, z */
+    const float* composites; int32_t num_composites;      /* 16 floats, glm column-major m[col][row] */
+    const rtg_xform_ref* xform_refs; int32_t num_xform_refs;
+    const rtg_object_desc* objects;  int32_t num_objects;  /* order: spheres, triangles, meshes */
+    const rtg_instance_desc* instances; int32_t num_instances;
+    const rtg_material_desc* materials; int32_t num_materials;
+    const rtg_texture_desc* textures;   int32_t num_textures;
+    const rtg_light_desc* lights;       int32_t num_lights;
+} rtg_scene_desc;
+
+typedef struct rtg_camera_desc {     /* src/Camera.h:351-399; FovY/GazePoint already resolved */
+    float position[3];
+    float gaze[3];
+    float up[3];
+    float left, right, bottom, top;  /* near plane */
+    float near_distance;
+    int32_t nx, ny;
+    int32_t num_samples;
+    int32_t is_dof;                  /* FocusDistance present */
+    float focus_distance;
+    float aperture_size;
+    int32_t left_handed;
+} rtg_camera_desc;
+
+typedef struct rtg_render_opts {
+    uint64_t seed;           /* Philox key for all stochastic draws (reference: random_device) */
+    int32_t row_offset;      /* render only rows y with y % row_stride == row_offset; other */
+    int32_t row_stride;      /* rows are written as 0 (multi-GPU pixel sharding). 0/1 = all */
+    int32_t traversal;       /* 0 = ordered + pruned (default), 1 = exhaustive (literal line test) */
+    int32_t max_batch_rays;  /* 0 = auto */
+    int32_t collect_stats;   /* 1 = count BVH node visits / triangle tests (slower) */
+    int32_t collect_timing;  /* 1 = HIP-event time every closest-hit / shadow launch */
+} rtg_render_opts;
+
+typedef struct rtg_render_stats {
+    uint64_t primary_rays;
+    uint64_t secondary_rays;
+    uint64_t shadow_rays;
+    uint64_t total_rays;
+    double render_ms;        /* device time of the last rtg_render* call */
+    int32_t passes;
+    int32_t max_level;
+    uint64_t node_visits;    /* collect_stats: 32-byte BVH child records read by closest-hit rays */
+    uint64_t tri_tests;      /* collect_stats: triangle tests by closest-hit (primary+secondary) rays */
+    uint64_t shadow_node_visits;   /* same for shadow queries */
+    uint64_t shadow_tri_tests;
+    double trace_ms;         /* collect_timing: summed device time of closest-hit launches */
+    double shadow_ms;        /* collect_timing: summed device time of shadow launches */
+    int32_t trace_launches;
+    int32_t shadow_launches;
+} rtg_render_stats;
+
+typedef struct rtg_ray {             /* src/Ray.h:10-12 */
+    float origin[3];
+    float direction[3];
+    float time;
+} rtg_ray;
+
+typedef struct rtg_hit {             /* what FindIntersection leaves in ReturnVal for a hit */
+    int32_t full;            /* 1 = hit */
+    int32_t object;          /* top-level index: [0,num_objects) objects, then instances */
+    int32_t prim;            /* primitive index in the object's original (parse) order */
+    int32_t material;        /* 1-based material (instance override applied) */
+    float t;                 /* gett() distance along the world ray (src/Helper.cpp:95) */
+    float point[3];          /* world hit point = ray.getPoint(t) */
+    float normal[3];         /* world normal after TransformNormal (src/Helper.cpp:129-131) */
+} rtg_hit;
+
+typedef struct rtg_scene rtg_scene;
+
+int32_t rtg_abi_version(void);
+const char* rtg_last_error(void);
+int32_t rtg_device_count(void);
+
+#define RTG_DEVICE_HOST_ONLY (-1)
+/* Build device-resident scene on HIP device `device`.  RTG_DEVICE_HOST_ONLY builds only
+   the host-side structures (matrices, normals, BVH) for introspection; such a scene
+   cannot render or trace (RTG_ERR_NO_DEVICE). */
+int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene** out);
+int32_t rtg_scene_destroy(rtg_scene* scene);
+
+/* Render one camera; rgb_out is caller-owned host memory of ny*nx*3 floats ([y][x][c]). */
+int32_t rtg_render(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_opts* opts,
+                   float* rgb_out);
+/* Same, output left in device memory (caller-owned, ny*nx*3 floats on the scene's device),
+   enqueued on `stream` (hipStream_t, NULL = default stream). Synchronous on return. */
+int32_t rtg_render_device(rtg_scene* scene, const rtg_camera_desc* cam,
+                          const rtg_render_opts* opts, float* rgb_out_device, void* stream);
+int32_t rtg_last_render_stats(const rtg_scene* scene, rtg_render_stats* out);
+
+/* Batch closest-hit query (BVHMethods::FindIntersection) over host arrays. */
+int32_t rtg_trace_closest(rtg_scene* scene, const rtg_ray* rays, int32_t n, rtg_hit* hits,
+                          int32_t traversal);
+
+/* Introspection for BVH parity tests: per object (0-based, objects only).
+   perm[k] = original primitive index at BVH position k (length num_prims).
+   nodes: num_nodes * 4 int32 {left, right, start, end} in the reference's pre-order
+   (node, left subtree, right subtree); left/right are node numbers or -1 (null),
+   start/end is the primitive range the node covers; leaves have left=right=-1.
+   boxes: num_nodes * 6 floats (min xyz, max xyz; leaves hold the leaf's own range box,
+   which the reference never tests).  Pass NULL buffers to query the sizes. */
+int32_t rtg_scene_object_bvh(const rtg_scene* scene, int32_t object, int32_t* num_prims,
+                             int32_t* num_nodes, int32_t* perm, int32_t* nodes, float* boxes);
+/* Composed matrices per top-level object (objects then instances): inverse and
+   inverse-transpose, glm column-major, 16 floats each. */
+int32_t rtg_scene_object_matrices(const rtg_scene* scene, int32_t top_object, float* inverse16,
+                                  float* inverse_transpose16);
+/* Smooth vertex normals after renderScene's precompute (src/Scene.cpp:433-449): 3*num_vertices. */
+int32_t rtg_scene_vertex_normals(const rtg_scene* scene, float* normals);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTG_H_ */

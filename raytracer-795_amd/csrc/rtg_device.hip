@@ -1,0 +1,1248 @@
+// rtg_device.hip — gfx950 kernels of the wavefront render loop.
+//
+// The reference's recursive per-pixel loop (src/Scene.cpp:279-350, 400-423, 496-542) is
+// flattened into levels: raygen -> [trace -> shade -> shadow] per ray-tree level ->
+// bottom-up resolve -> in-order sample accumulation.  Every floating-point expression
+// follows the reference's evaluation order (compiled with -ffp-contract=off and correctly
+// rounded f32 div/sqrt), so hit indices are bit-identical to the oracle and colours agree
+// to the transcendental convention documented in oracle/rtg_oracle.c.
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#include "rtg_internal.h"
+
+namespace rtg {
+
+#define DEV __device__ __forceinline__
+constexpr double PI_D = 3.14159265358979323846;
+
+// ------------------------------------------------------------------ vectors (Eigen order)
+struct f3 { float x, y, z; };
+DEV f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+DEV f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+DEV f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+DEV f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
+DEV f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+DEV f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+DEV f3 cw(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+DEV float dot(f3 a, f3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+DEV float sqn(f3 a) { return a.x * a.x + (a.y * a.y + a.z * a.z); }
+DEV float norm(f3 a) { return sqrtf(sqn(a)); }
+DEV f3 normalized(f3 a) {
+    float z = sqn(a);
+    if (z > 0.0f) return a / sqrtf(z);
+    return a;
+}
+DEV f3 cross(f3 a, f3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+DEV bool isnan3(f3 a) { return a.x != a.x || a.y != a.y || a.z != a.z; }
+DEV f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+DEV float fmax0(float x) { return (0.0f < x) ? x : 0.0f; }
+DEV float stdmin(float a, float b) { return (b < a) ? b : a; }
+DEV float vget(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+// transcendental convention: (float) of the double-precision function
+DEV float f_acos(float x) { return (float)acos((double)x); }
+DEV float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+DEV float f_cos(float x) { return (float)cos((double)x); }
+DEV float f_sin(float x) { return (float)sin((double)x); }
+DEV float f_exp(float x) { return (float)exp((double)x); }
+DEV float f_powi(float x, int n) { return (float)pow((double)x, (double)n); }
+
+// glm mat4 (column-major) * (v, w): (c0*x + c1*y) + (c2*z + c3*w)
+DEV f3 xform(const float* m, f3 v, float w) {
+    float r[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float add0 = m[0 * 4 + i] * v.x + m[1 * 4 + i] * v.y;
+        float add1 = m[2 * 4 + i] * v.z + m[3 * 4 + i] * w;
+        r[i] = add0 + add1;
+    }
+    return mk(r[0], r[1], r[2]);
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+enum { RNG_CAMERA = 1, RNG_ROUGH = 2, RNG_AREA = 3, RNG_ENV = 4 };
+DEV void rng4(uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, uint32_t purpose, uint32_t light,
+              uint32_t iter, float out[4]) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ (uint32_t)(path >> 32);
+    uint32_t c0 = pixel, c1 = sample, c2 = (uint32_t)path;
+    uint32_t c3 = (purpose << 28) | ((light & 0xFFFu) << 16) | (iter & 0xFFFFu);
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    uint32_t c[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float f = (float)c[i] / 4294967296.0f;
+        out[i] = (f >= 1.0f) ? 0x1.fffffep-1f : f;
+    }
+}
+
+// ------------------------------------------------------------------ BVH helpers (src/BVH.cpp)
+DEV float min3(float a, float b, float c) {
+    if (a <= b && a <= c) return a;
+    else if (b <= a && b <= c) return b;
+    return c;
+}
+DEV float max3(float a, float b, float c) {
+    if (a >= b && a >= c) return a;
+    else if (b >= a && b >= c) return b;
+    return c;
+}
+// BVH::RayBBoxIntersection, src/BVH.cpp:212-266 (exact divisions: it decides reachability)
+DEV bool box_test(f3 o, f3 d, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
+    float txe, txl, tye, tyl, tze, tzl;
+    if (d.x > 0) { txe = (mnx - o.x) / d.x; txl = (mxx - o.x) / d.x; }
+    else { txe = (mxx - o.x) / d.x; txl = (mnx - o.x) / d.x; }
+    if (d.y > 0) { tye = (mny - o.y) / d.y; tyl = (mxy - o.y) / d.y; }
+    else { tye = (mxy - o.y) / d.y; tyl = (mny - o.y) / d.y; }
+    if (d.z > 0) { tze = (mnz - o.z) / d.z; tzl = (mxz - o.z) / d.z; }
+    else { tze = (mxz - o.z) / d.z; tzl = (mnz - o.z) / d.z; }
+    float sl = min3(txl, tyl, tzl);
+    float le = max3(txe, tye, tze);
+    return !(sl < le);
+}
+// Conservative lower bound of |p - o| over points p within `pad` of the box (pruning only).
+DEV float box_lb(f3 o, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float pad, float oabs) {
+    float dx = fmaxf(fmaxf(mnx - o.x, o.x - mxx), 0.0f);
+    float dy = fmaxf(fmaxf(mny - o.y, o.y - mxy), 0.0f);
+    float dz = fmaxf(fmaxf(mnz - o.z, o.z - mxz), 0.0f);
+    float l = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+    return l * (1.0f - 1e-5f) - pad - 1e-6f * (oabs + l);
+}
+// Eigen 3x3 determinant (row-0 expansion) of the matrix with columns c0, c1, c2
+DEV float det3(f3 c0, f3 c1, f3 c2) {
+    float h0 = c0.x * (c1.y * c2.z - c1.z * c2.y);
+    float h1 = c1.x * (c0.y * c2.z - c0.z * c2.y);
+    float h2 = c2.x * (c0.y * c1.z - c0.z * c1.y);
+    return (h0 - h1) + h2;
+}
+
+struct Cand {           // Triangle::bvhIntersect acceptance + point (src/Shape.cpp:413-461)
+    bool ok;
+    float beta, gamma, t;
+    f3 p;
+};
+DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps) {
+    f3 a = mk(g.p0.x, g.p0.y, g.p0.z);
+    f3 amb = mk(g.p0.w, g.p1.x, g.p1.y);
+    f3 amc = mk(g.p1.z, g.p1.w, g.p2.x);
+    f3 amo = a - o;
+    Cand c;
+    float det = det3(amb, amc, d);
+    c.beta = det3(amo, amc, d) / det;
+    c.gamma = det3(amb, amo, d) / det;
+    c.t = det3(amb, amc, amo) / det;
+    c.ok = (c.t >= -eps && (c.beta + c.gamma <= 1) && c.beta >= -eps && c.gamma >= -eps);
+    c.p = o + d * c.t;
+    return c;
+}
+// Sphere::bvhIntersect root selection (src/Shape.cpp:463-507)
+DEV bool sphere_test(f3 o, f3 d, f3 c, float R, float eps, f3& ip) {
+    f3 oc = o - c;
+    float dd = dot(d, oc);
+    float disc = dd * dd - dot(d, d) * (dot(oc, oc) - R * R);
+    if (disc < eps) return false;
+    float sq = sqrtf(disc);
+    float t1 = (-dd + sq) / dot(d, d);
+    float t2 = (-dd - sq) / dot(d, d);
+    if (t1 >= 0 && t2 < 0) ip = o + d * t1;
+    else if (t2 >= 0 && t1 < 0) ip = o + d * t2;
+    else if (t1 < 0 && t2 < 0) return false;
+    else ip = (t1 < t2) ? (o + d * t1) : (o + d * t2);
+    return true;
+}
+// Ray::gett (src/Ray.cpp:21-36)
+DEV float gett(f3 o, f3 d, f3 p) {
+    float t = (p.x - o.x) / d.x;
+    if (t == t) return t;
+    t = (p.y - o.y) / d.y;
+    if (t == t) return t;
+    t = (p.z - o.z) / d.z;
+    return t;
+}
+// Transforming::TransformRay (src/Helper.cpp:164-187)
+DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d2) {
+    f3 b = mk(T.blur[0] * time, T.blur[1] * time, T.blur[2] * time);
+    f3 oo = o;
+    oo.x -= b.x; oo.y -= b.y; oo.z -= b.z;
+    o2 = xform(T.inv, oo, 1.0f);
+    d2 = xform(T.inv, d, 0.0f);
+}
+
+struct Stats { unsigned nodes, tris; };
+
+// ------------------------------------------------------------------ closest hit
+// BVHMethods::FindIntersection (src/Helper.cpp:72-134) with the per-object nearest
+// candidate of BVH::FindIntersectionWithBVH (src/BVH.cpp:137-210).  The reference visits
+// both children of every node whose box the infinite line crosses; its result is the
+// candidate of minimal Euclidean distance, ties -> rightmost leaf, then lowest index in
+// the leaf.  This ordered traversal computes the same total order and prunes subtrees
+// whose distance lower bound exceeds the current best (EXHAUSTIVE disables pruning).
+// `tmax`: hits with gett() >= tmax are irrelevant to the caller (shadow queries).
+template <bool EXHAUSTIVE, bool STATS>
+DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride,
+                       Stats& st) {
+    HitRec out;
+    out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
+    if (isnan3(o) || isnan3(d)) return out;
+    float nearest = tmax;
+    const float eps = sv.int_eps;
+    for (int i = 0; i < sv.num_tops; i++) {
+        const TopObject& T = sv.tops[i];
+        const Geometry& g = sv.geoms[T.geom];
+        f3 o2, d2;
+        transform_ray(T, o, d, time, o2, d2);
+        bool found = false;
+        int bprim = -1;
+        f3 bp = mk(0, 0, 0);
+        if (g.type == RTG_OBJ_SPHERE) {
+            if (g.nprims > 0) {
+                f3 ip;
+                if (sphere_test(o2, d2, ld3(g.center), g.radius, eps, ip)) {
+                    float dist = norm(ip - o2);
+                    if (dist < FLT_MAX) { found = true; bprim = g.prim_base; bp = ip; }
+                }
+            }
+        } else {
+            // distance bound from the best hit so far (see DESIGN.md "pruning")
+            float boundD = FLT_MAX;
+            if (!EXHAUSTIVE && nearest < FLT_MAX) {
+                float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
+                float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
+                float dl = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+                if (da != 0.0f) {
+                    float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * (1.0f + 1e-5f);
+                    boundD = tm * dl * (1.0f + 2e-5f) + 1e-30f;
+                    if (!(boundD == boundD)) boundD = FLT_MAX;
+                }
+            }
+            float oabs = fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fabsf(o2.z));
+            const float pad = g.prune_pad;
+            float best_d = FLT_MAX;
+            int best_leaf = -1;
+            auto leaf = [&](int start, int count) {
+                for (int k = start; k < start + count; k++) {
+                    const TriGeom tg = sv.tris[k];
+                    if (STATS) st.tris++;
+                    Cand c = tri_test(tg, o2, d2, eps);
+                    if (c.ok) {
+                        float dist = norm(c.p - o2);
+                        if (dist < FLT_MAX &&
+                            (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
+                            best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                        }
+                    }
+                }
+            };
+            if (g.node_base < 0) {
+                if (g.root_leaf_count > 0) leaf(g.root_leaf_start, g.root_leaf_count);
+            } else if (box_test(o2, d2, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0], g.root_max[1],
+                                g.root_max[2])) {
+                int sp = 0;
+                int cur = g.node_base;
+                while (true) {
+                    if (STATS) st.nodes += 2;   // one 64-B node = two 32-B child records
+                    const Node nd = sv.nodes[cur];
+                    const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
+                    float bound = EXHAUSTIVE ? FLT_MAX : fminf(best_d, boundD);
+                    bool lok = false, rok = false;
+                    float llb = 0.0f, rlb = 0.0f;
+                    if (lcnt >= 0) {
+                        if (!EXHAUSTIVE) llb = box_lb(o2, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, pad, oabs);
+                        lok = EXHAUSTIVE || !(llb > bound);
+                        if (lok && lcnt == 0) lok = box_test(o2, d2, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y);
+                    }
+                    if (rcnt >= 0) {
+                        if (!EXHAUSTIVE) rlb = box_lb(o2, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, pad, oabs);
+                        rok = EXHAUSTIVE || !(rlb > bound);
+                        if (rok && rcnt == 0) rok = box_test(o2, d2, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w);
+                    }
+                    // leaf children are resolved immediately, nearer first
+                    bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
+                    if (lleaf && rleaf && rlb < llb) {
+                        leaf(rref, rcnt);
+                        if (EXHAUSTIVE || !(llb > fminf(best_d, boundD))) leaf(lref, lcnt);
+                        lok = rok = false;
+                    } else {
+                        if (lleaf) { leaf(lref, lcnt); lok = false; }
+                        if (rleaf) {
+                            if (EXHAUSTIVE || !(rlb > fminf(best_d, boundD))) leaf(rref, rcnt);
+                            rok = false;
+                        }
+                    }
+                    if (!EXHAUSTIVE && (lok || rok)) {
+                        bound = fminf(best_d, boundD);
+                        lok = lok && !(llb > bound);
+                        rok = rok && !(rlb > bound);
+                    }
+                    if (lok && rok) {
+                        int nearc = lref, farc = rref;
+                        if (rlb < llb) { nearc = rref; farc = lref; }
+                        stack[sp * sstride] = farc;
+                        sp++;
+                        cur = nearc;
+                    } else if (lok) {
+                        cur = lref;
+                    } else if (rok) {
+                        cur = rref;
+                    } else {
+                        if (sp == 0) break;
+                        sp--;
+                        cur = stack[sp * sstride];
+                    }
+                }
+            }
+        }
+        if (found) {
+            float t = gett(o2, d2, bp);
+            if (t < nearest && t > 0) {
+                nearest = t;
+                out.obj = i; out.prim = bprim; out.t = t;
+            }
+        }
+    }
+    return out;
+}
+
+// ------------------------------------------------------------------ textures / Perlin
+DEV f3 tex_pixel(const SceneView& sv, const TextureDev& t, int i, int j) {   // src/Texture.cpp:41-74
+    if (i < 0) i = 0; else if (i >= t.w) i = t.w - 1;
+    if (j < 0) j = 0; else if (j >= t.h) j = t.h - 1;
+    const float* p = sv.texels + t.texel_offset + ((long long)j * t.w + i) * 3;
+    return mk(p[0], p[1], p[2]);
+}
+DEV f3 tex_color(const SceneView& sv, const TextureDev& t, float u, float v) {   // :111-131
+    u = u - floorf(u);
+    v = v - floorf(v);
+    float i = u * (float)t.w;
+    float j = v * (float)t.h;
+    if (t.interp == RTG_INTERP_NN) return tex_pixel(sv, t, (int)i, (int)j);
+    int li = (int)floorf(i), lj = (int)floorf(j);
+    float a = i - (float)li, b = j - (float)lj;
+    f3 c00 = tex_pixel(sv, t, li, lj), c01 = tex_pixel(sv, t, li, lj + 1);
+    f3 c10 = tex_pixel(sv, t, li + 1, lj), c11 = tex_pixel(sv, t, li + 1, lj + 1);
+    float w00 = (1 - a) * (1 - b), w01 = (1 - a) * b, w10 = a * (1 - b), w11 = a * b;
+    return ((c00 * w00 + c01 * w01) + c10 * w10) + c11 * w11;
+}
+DEV void tex_change(const SceneView& sv, const TextureDev& t, float u, float v, float& du, float& dv) {  // :76-109
+    u = u - floorf(u);
+    v = v - floorf(v);
+    int i = (int)(u * (float)t.w);
+    int j = (int)(v * (float)t.h);
+    if (i < 0) i = 0; else if (i >= t.w - 1) i = t.w - 2;
+    if (j < 0) j = 0; else if (j >= t.h - 1) j = t.h - 2;
+    f3 a = tex_pixel(sv, t, i + 1, j), b = tex_pixel(sv, t, i, j), c = tex_pixel(sv, t, i, j + 1);
+    float dede = ((a.x + a.y) + a.z) / 3.0f;
+    float nene = ((b.x + b.y) + b.z) / 3.0f;
+    f3 dd = c - b;
+    du = dede - nene;
+    dv = ((dd.x + dd.y) + dd.z) / 3.0f;
+}
+
+__constant__ float c_perlin_table[16][3] = {
+    {1, 1, 0}, {-1, 1, 0}, {1, -1, 0}, {-1, -1, 0}, {1, 0, 1}, {-1, 0, 1}, {1, 0, -1}, {-1, 0, -1},
+    {0, 1, 1}, {0, -1, 1}, {0, 1, -1}, {0, -1, -1}, {1, 1, 0}, {-1, 1, 0}, {0, -1, 1}, {0, -1, -1}};
+__constant__ int c_perlin_shuffled[16] = {12, 7, 15, 6, 11, 0, 4, 9, 13, 3, 14, 8, 2, 5, 1, 10};
+DEV int perlin_P(int i) { int idx = i % 16; if (idx < 0) idx += 16; return c_perlin_shuffled[idx]; }
+DEV float perlin_weight(float x) {                      // src/Perlin.cpp:27-30 (double pow)
+    double xd = (double)fabsf(x);
+    return (float)((((-6) * pow(xd, 5.0)) + (15 * pow(xd, 4.0))) - (10 * pow(xd, 3.0)) + 1);
+}
+DEV float perlin_compute(f3 p, float scale, int nc) {   // src/Perlin.cpp:52-84
+    f3 pt = p * scale;
+    int ii = (int)floorf(pt.x), jj = (int)floorf(pt.y), kk = (int)floorf(pt.z);
+    float value = 0;
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++)
+            for (int k = 0; k < 2; k++) {
+                int lx = ii + i, ly = jj + j, lz = kk + k;
+                int idx = perlin_P(lx + perlin_P(ly + perlin_P(lz)));
+                f3 g = mk(c_perlin_table[idx][0], c_perlin_table[idx][1], c_perlin_table[idx][2]);
+                f3 l = pt - mk((float)lx, (float)ly, (float)lz);
+                float w = (perlin_weight(l.x) * perlin_weight(l.y)) * perlin_weight(l.z);
+                value += dot(g, l) * w;
+            }
+    if (nc == RTG_NC_LINEAR) value = (value + 1) * 0.5f;
+    else if (nc == RTG_NC_ABSVAL) value = fabsf(value);
+    return value;
+}
+DEV f3 perlin_gradient(f3 p, float scale, int nc) {     // src/Perlin.cpp:36-50
+    const float eps = 0.001f;
+    f3 xe = p, ye = p, ze = p;
+    xe.x += eps; ye.y += eps; ze.z += eps;
+    float o = perlin_compute(p, scale, nc);
+    return mk((perlin_compute(xe, scale, nc) - o) / eps, (perlin_compute(ye, scale, nc) - o) / eps,
+              (perlin_compute(ze, scale, nc) - o) / eps);
+}
+DEV f3 ortho_u(f3 v) {                                  // src/Helper.cpp:322-343
+    float a0 = fabsf(v.x), a1 = fabsf(v.y), a2 = fabsf(v.z);
+    f3 nl = v;
+    if (a0 <= a1 && a0 <= a2) nl.x = 1.0f;
+    else if (a1 <= a0 && a1 <= a2) nl.y = 1.0f;
+    else nl.z = 1.0f;
+    return normalized(cross(v, nl));
+}
+
+// ------------------------------------------------------------------ full hit record
+struct Ret {            // ReturnVal (src/defs.h:13-22)
+    f3 point, normal;
+    int matIndex, dm;
+    f3 tc;
+    float tn;
+};
+
+DEV f3 tbn_apply(f3 T, f3 B, f3 N, f3 r) {   // Matrix3f(T,B,N cols) * r, rows summed x0+(x1+x2)
+    return mk(T.x * r.x + (B.x * r.y + N.x * r.z), T.y * r.x + (B.y * r.y + N.y * r.z),
+              T.z * r.x + (B.z * r.y + N.z * r.z));
+}
+DEV void perlin_decal(const TextureDev& t, Ret& ret) {
+    if (t.decal == RTG_DECAL_REPLACE_KD) {
+        ret.dm = t.decal;
+        float p = perlin_compute(ret.point, t.noise_scale, t.nc);
+        ret.tc = mk(p, p, p);
+        ret.tn = 1;
+    } else if (t.decal == RTG_DECAL_BUMP_NORMAL) {
+        f3 g = perlin_gradient(ret.point, t.noise_scale, t.nc);
+        f3 gpar = ret.normal * dot(g, ret.normal);
+        f3 nn = ret.normal - (g - gpar) * t.bump;
+        ret.normal = (dot(ret.normal, nn) > 0) ? nn : -nn;
+        ret.normal = normalized(ret.normal);
+    }
+}
+// Sphere::TextureComputation, src/Shape.cpp:516-619
+DEV void sphere_texture(const SceneView& sv, const Geometry& g, Ret& ret) {
+    ret.dm = RTG_DECAL_NONE;
+    f3 c = ld3(g.center);
+    float R = g.radius;
+    for (int i = 0; i < g.num_textures; i++) {
+        const TextureDev t = sv.textures[g.textures[i] - 1];
+        if (t.kind == RTG_TEX_IMAGE) {
+            f3 lc = ret.point - c;
+            float theta = f_acos(lc.y / R);
+            float phi = f_atan2(lc.z, lc.x);
+            float tu = (float)((-(double)phi + PI_D) / (2 * PI_D));
+            float tv = (float)((double)theta / PI_D);
+            if (t.decal == RTG_DECAL_REPLACE_KD || t.decal == RTG_DECAL_BLEND_KD || t.decal == RTG_DECAL_REPLACE_ALL) {
+                ret.dm = t.decal;
+                ret.tc = tex_color(sv, t, tu, tv);
+                ret.tn = (float)t.normalizer;
+            } else if (t.decal == RTG_DECAL_REPLACE_NORMAL || t.decal == RTG_DECAL_BUMP_NORMAL) {
+                float pi = (float)PI_D;
+                f3 dpdu = mk((lc.z * 2) * pi, 0, (lc.x * (-2)) * pi);
+                f3 dpdv = mk((lc.y * f_cos(phi)) * pi, (((-1) * R) * f_sin(theta)) * pi, (lc.y * f_sin(phi)) * pi);
+                if (t.decal == RTG_DECAL_REPLACE_NORMAL) {
+                    f3 rn = tex_color(sv, t, tu, tv) / 255.0f;
+                    rn = normalized(rn - mk(0.5f, 0.5f, 0.5f));
+                    ret.normal = tbn_apply(normalized(dpdu), normalized(dpdv), ret.normal, rn);
+                } else {
+                    float du, dv;
+                    tex_change(sv, t, tu, tv, du, dv);
+                    du = du * t.bump; dv = dv * t.bump;
+                    f3 dpu = dpdu + ret.normal * du;
+                    f3 dpv = dpdv + ret.normal * dv;
+                    f3 nn = normalized(cross(dpv, dpu));
+                    ret.normal = (dot(ret.normal, nn) > 0) ? nn : -nn;
+                }
+            }
+        } else {
+            perlin_decal(t, ret);
+        }
+    }
+}
+DEV void texcoord(const SceneView& sv, int idx, float& u, float& v) {
+    if (idx < 0 || idx >= sv.num_texcoords) { u = 0; v = 0; return; }
+    u = sv.texcoords[2 * idx]; v = sv.texcoords[2 * idx + 1];
+}
+// Triangle::TextureComputation, src/Shape.cpp:621-732
+DEV void triangle_texture(const SceneView& sv, const Geometry& g, int4 vi, f3 e1, f3 e2, float beta, float gamma,
+                          Ret& ret) {
+    ret.dm = RTG_DECAL_NONE;
+    if (g.num_textures == 0) return;
+    float alpha = (1 - beta) - gamma;
+    float u0, v0, u1, v1, u2, v2;
+    texcoord(sv, vi.x - 1 + g.texture_offset, u0, v0);
+    texcoord(sv, vi.y - 1 + g.texture_offset, u1, v1);
+    texcoord(sv, vi.z - 1 + g.texture_offset, u2, v2);
+    float uu = (u0 * alpha + u1 * beta) + u2 * gamma;
+    float vv = (v0 * alpha + v1 * beta) + v2 * gamma;
+    for (int i = 0; i < g.num_textures; i++) {
+        const TextureDev t = sv.textures[g.textures[i] - 1];
+        if (t.kind == RTG_TEX_IMAGE) {
+            if (t.decal == RTG_DECAL_REPLACE_KD || t.decal == RTG_DECAL_BLEND_KD || t.decal == RTG_DECAL_REPLACE_ALL) {
+                ret.dm = t.decal;
+                ret.tc = tex_color(sv, t, uu, vv);
+                ret.tn = (float)t.normalizer;
+            } else if (t.decal == RTG_DECAL_REPLACE_NORMAL || t.decal == RTG_DECAL_BUMP_NORMAL) {
+                float a00 = u1 - u0, a01 = v1 - v0, a10 = u2 - u0, a11 = v2 - v0;
+                float invdet = 1.0f / (a00 * a11 - a10 * a01);
+                float i00 = a11 * invdet, i10 = -a10 * invdet, i01 = -a01 * invdet, i11 = a00 * invdet;
+                f3 T = mk(i00 * e1.x + i01 * e2.x, i00 * e1.y + i01 * e2.y, i00 * e1.z + i01 * e2.z);
+                f3 B = mk(i10 * e1.x + i11 * e2.x, i10 * e1.y + i11 * e2.y, i10 * e1.z + i11 * e2.z);
+                if (t.decal == RTG_DECAL_REPLACE_NORMAL) {
+                    f3 rn = tex_color(sv, t, uu, vv) / 255.0f;
+                    rn = normalized(rn - mk(0.5f, 0.5f, 0.5f));
+                    ret.normal = tbn_apply(T, B, ret.normal, rn);
+                } else {
+                    float du, dv;
+                    tex_change(sv, t, uu, vv, du, dv);
+                    du = du * t.bump; dv = dv * t.bump;
+                    f3 dpu = T + ret.normal * du;
+                    f3 dpv = B + ret.normal * dv;
+                    f3 nn = normalized(cross(dpv, dpu));
+                    ret.normal = (dot(ret.normal, nn) > 0) ? nn : -nn;
+                }
+            }
+        } else {
+            perlin_decal(t, ret);
+        }
+    }
+}
+
+// Re-derive the full ReturnVal of a hit found by closest_hit: the winning primitive's
+// object-space intersection (identical arithmetic), texturing, then the top-level
+// world point and TransformNormal (src/Helper.cpp:93-131).
+DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h) {
+    const TopObject& T = sv.tops[h.obj];
+    const Geometry& g = sv.geoms[T.geom];
+    f3 o2, d2;
+    transform_ray(T, o, d, time, o2, d2);
+    Ret ret;
+    ret.matIndex = T.material;
+    ret.tc = mk(0, 0, 0);
+    ret.tn = 0;
+    if (g.type == RTG_OBJ_SPHERE) {
+        f3 ip = mk(0, 0, 0);
+        sphere_test(o2, d2, ld3(g.center), g.radius, sv.int_eps, ip);
+        ret.point = ip;
+        f3 pc = ip - ld3(g.center);
+        ret.normal = pc / norm(pc);
+        sphere_texture(sv, g, ret);
+    } else {
+        const TriGeom tg = sv.tris[h.prim];
+        Cand c = tri_test(tg, o2, d2, sv.int_eps);
+        int4 vi = sv.prim_idx[h.prim];
+        f3 a = mk(tg.p0.x, tg.p0.y, tg.p0.z);
+        f3 b = ld3(sv.vertices + 3 * (vi.y - 1)), cc = ld3(sv.vertices + 3 * (vi.z - 1));
+        f3 normal;
+        if (vi.w) {
+            float alpha = (1 - c.beta) - c.gamma;
+            f3 n1 = ld3(sv.vnormals + 3 * (vi.x - 1)), n2 = ld3(sv.vnormals + 3 * (vi.y - 1)),
+               n3 = ld3(sv.vnormals + 3 * (vi.z - 1));
+            normal = (n1 * alpha + n2 * c.beta) + n3 * c.gamma;
+        } else {
+            normal = cross(cc - b, a - b);
+        }
+        ret.normal = normal / norm(normal);
+        ret.point = c.p;
+        triangle_texture(sv, g, vi, b - a, cc - a, c.beta, c.gamma, ret);
+    }
+    float t = gett(o2, d2, ret.point);
+    ret.point = o + d * t;
+    ret.normal = normalized(xform(T.invT, ret.normal, 1.0f));
+    return ret;
+}
+
+// ------------------------------------------------------------------ lights (src/Light.cpp)
+DEV float conductor_fresnel(float n_t, float k_t, f3 ray, f3 normal) {   // Light.cpp:156-166, Scene.cpp:266-277
+    float cos_t = -dot(ray, normal);
+    float twoNtCost = (2 * n_t) * cos_t;
+    float cosSquared = (float)pow((double)cos_t, 2.0);
+    float ntk = (float)(pow((double)n_t, 2.0) + pow((double)k_t, 2.0));
+    float rs = ((ntk - twoNtCost) + cosSquared) / ((ntk + twoNtCost) + cosSquared);
+    float rp = ((ntk * cosSquared - twoNtCost) + 1) / ((ntk * cosSquared + twoNtCost) + 1);
+    return 0.5f * (rs + rp);
+}
+DEV float geometry_ts(f3 wi, f3 wo, f3 wh, f3 n) {      // Light.cpp:187-198
+    float left = (2.0f * dot(n, wh)) * dot(n, wo);
+    left = left / dot(wo, wh);
+    float right = (2.0f * dot(n, wh)) * dot(n, wi);
+    right = right / dot(wi, wh);
+    float x = stdmin(left, right);
+    return stdmin(1.0f, x);
+}
+DEV float distribution_ts(float cosAlpha, int p) {       // Light.cpp:150-154
+    float x = (float)((double)((float)p + 2.0f) / (double)(2.0f * PI_D));
+    x = (float)((double)x * pow((double)cosAlpha, (double)p));
+    return x;
+}
+DEV f3 term_brdf(f3 wi, f3 wo, f3 n, const MaterialDev& m) {   // Light.cpp:200-293
+    f3 kd = ld3(m.diffuse), ks = ld3(m.specular);
+    int p = m.phong_exp;
+    switch (m.brdf) {
+    case RTG_BRDF_MP:
+    case RTG_BRDF_OP:
+    case RTG_BRDF_MPN: {
+        float n_wi = dot(n, wi);
+        f3 wr = -wi + (n * 2) * n_wi;
+        wr = wr / norm(wr);
+        float cosAngle = fmax0(dot(wr, wo));
+        if (m.brdf == RTG_BRDF_MP) return kd + ks * f_powi(cosAngle, p);
+        if (m.brdf == RTG_BRDF_OP) {
+            float cti = fmax0(dot(wi, n));
+            if (cti < 0.001f) return mk(0, 0, 0);
+            return kd + (ks * f_powi(cosAngle, p)) / cti;
+        }
+        return kd / (float)PI_D + (ks * (float)((p + 2) / (2 * PI_D))) * f_powi(cosAngle, p);
+    }
+    case RTG_BRDF_MBP:
+    case RTG_BRDF_OBP:
+    case RTG_BRDF_MBPN: {
+        f3 h = normalized(wo + wi);
+        float cosAngle = fmax0(dot(n, h));
+        if (m.brdf == RTG_BRDF_MBP) return kd + ks * f_powi(cosAngle, p);
+        if (m.brdf == RTG_BRDF_OBP) {
+            float cti = fmax0(dot(wi, n));
+            if (cti < 0.001f) return mk(0, 0, 0);
+            return kd + (ks * f_powi(cosAngle, p)) / cti;
+        }
+        return kd / (float)PI_D + (ks * (float)((p + 8) / (8 * PI_D))) * f_powi(cosAngle, p);
+    }
+    case RTG_BRDF_TS:
+    case RTG_BRDF_TSF: {
+        f3 wh = normalized(wo + wi);
+        float f = 0;
+        f3 dp = kd / (float)PI_D;
+        if (m.brdf == RTG_BRDF_TSF) {
+            f = conductor_fresnel(m.refraction_index, m.absorption_index, -wo, n);
+            dp = dp * (1 - f);
+        }
+        float cosAlpha = dot(wh, n), cosTheta = dot(wi, n), cosPhi = dot(wo, n);
+        float gg = geometry_ts(wi, wo, wh, n);
+        float dd = distribution_ts(cosAlpha, p);
+        f3 sp = (ks * gg) * dd;
+        sp = sp / ((4.0f * cosPhi) * cosTheta);
+        if (m.brdf == RTG_BRDF_TSF) sp = sp * f;
+        return dp + sp;
+    }
+    default:
+        return mk(0, 0, 0);
+    }
+}
+DEV f3 brdf(f3 wi, f3 wo, f3 n, f3 radiance, const MaterialDev& m) {   // Light.cpp:295-300
+    f3 t = term_brdf(wi, wo, n, m);
+    float cosAngle = fmax0(dot(wi, n));
+    return cw(radiance, t) * cosAngle;
+}
+DEV f3 diffuse_term(f3 LC, const Ret& ret, const MaterialDev& m, float alpha) {
+    if (ret.dm == RTG_DECAL_REPLACE_KD) return cw(LC, (ret.tc / ret.tn) * alpha);
+    if (ret.dm == RTG_DECAL_BLEND_KD) return cw(LC, ((ld3(m.diffuse) + ret.tc / ret.tn) * 0.5f) * alpha);
+    return cw(LC, ld3(m.diffuse) * alpha);
+}
+DEV f3 specular_term(f3 LC, f3 wo, f3 wi, const Ret& ret, const MaterialDev& m) {
+    f3 s = wo + wi;
+    f3 h = s / norm(s);
+    float alpha = fmax0(dot(ret.normal, h));
+    return cw(LC, ld3(m.specular) * f_powi(alpha, m.phong_exp));
+}
+DEV f3 phong_or_brdf(f3 LC, f3 wo, f3 wi, const Ret& ret, const MaterialDev& m) {
+    if (m.brdf != RTG_BRDF_NONE) return brdf(wi, wo, ret.normal, LC, m);
+    float alpha = fmax0(dot(ret.normal, wi));
+    return diffuse_term(LC, ret, m, alpha) + specular_term(LC, wo, wi, ret, m);
+}
+DEV f3 env_radiance(const SceneView& sv, const LightDev& L, f3 dir) {   // Light.cpp:701-713
+    float theta = f_acos(dir.y);
+    float phi = f_atan2(dir.z, dir.x);
+    float tu = (float)((-(double)phi + PI_D) / (2 * PI_D));
+    float tv = (float)((double)theta / PI_D);
+    f3 rad = tex_color(sv, sv.textures[L.tex], tu, tv);
+    return (rad * 2) * (float)PI_D;
+}
+
+// Unshadowed contribution of light li plus the shadow query it needs.
+DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
+                      uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
+    const LightDev& L = sv.lights[li];
+    f3 wo = -primeDir;
+    f3 origin = ret.point + ret.normal * sv.shadow_eps;
+    f3 c = mk(0, 0, 0);
+    f3 dir = mk(0, 0, 0), lp = mk(0, 0, 0);
+    float mode = 0.0f, tmax = FLT_MAX;
+    switch (L.type) {
+    case RTG_LIGHT_POINT: {                                     // PointLight::BasicShading :376-388
+        f3 pos = ld3(L.pos);
+        f3 dv = pos - ret.point;
+        dir = dv / norm(dv);
+        lp = pos;
+        mode = 1.0f;
+        float dist = norm(ret.point - pos);
+        f3 LC = ld3(L.inten) / (dist * dist);
+        c = phong_or_brdf(LC, wo, normalized(pos - ret.point), ret, m);
+        break;
+    }
+    case RTG_LIGHT_DIRECTIONAL: {                               // :447-459
+        dir = -ld3(L.dir);
+        mode = 2.0f;
+        c = phong_or_brdf(ld3(L.inten), wo, dir, ret, m);
+        break;
+    }
+    case RTG_LIGHT_SPOT: {                                      // :547-574
+        f3 pos = ld3(L.pos);
+        f3 dv = pos - ret.point;
+        dir = dv / norm(dv);
+        lp = pos;
+        f3 dtp = normalized(ret.point - pos);
+        float angle = f_acos(dot(dtp, ld3(L.dir)));
+        if (angle < L.fall || angle < L.coverage) {
+            mode = 1.0f;
+            float dist = norm(ret.point - pos);
+            f3 LC = ld3(L.inten) / (dist * dist);
+            c = phong_or_brdf(LC, wo, normalized(pos - ret.point), ret, m);
+            if (!(angle < L.fall)) {
+                float fo = (float)pow((cos((double)angle) - (double)L.cos_cov) / (double)(L.cos_fall - L.cos_cov), 4.0);
+                c = c * fo;
+            }
+        }
+        break;
+    }
+    case RTG_LIGHT_AREA: {                                      // :660-683
+        float xi[4];
+        rng4(seed, pixel, sample, path, RNG_AREA, (uint32_t)li, 0, xi);
+        float uChi = xi[0] - 0.5f, vChi = xi[1] - 0.5f;
+        f3 smp = (ld3(L.pos) + (ld3(L.u) * L.size) * uChi) + (ld3(L.v) * L.size) * vChi;
+        f3 dv = smp - ret.point;
+        dir = dv / norm(dv);
+        lp = smp;
+        mode = 1.0f;
+        f3 pms = ret.point - smp;
+        float cosTheta = fabsf(dot(normalized(pms), ld3(L.normal)));
+        float dSq = norm(pms);
+        dSq = dSq * dSq;
+        f3 LC = ld3(L.inten) * ((L.size * L.size) * (cosTheta / dSq));
+        c = phong_or_brdf(LC, wo, normalized(smp - ret.point), ret, m);
+        break;
+    }
+    case RTG_LIGHT_ENVIRONMENT: {                               // :766-798
+        f3 n = ret.normal;
+        f3 u = ortho_u(n);
+        f3 w = cross(n, u);
+        f3 direction = n;
+        for (uint32_t it = 0; it <= 1000000u; it++) {
+            float xi[4];
+            rng4(seed, pixel, sample, path, RNG_ENV, (uint32_t)li, it, xi);
+            float x = xi[0] * 2 - 1.0f, y = xi[1] * 2 - 1.0f, z = xi[2] * 2 - 1.0f;
+            f3 smp = ((ret.point + u * x) + n * y) + w * z;
+            f3 dd = smp - ret.point;
+            if (dot(dd, n) > 0 && norm(dd) <= 1) { direction = normalized(dd); break; }
+        }
+        dir = direction;
+        mode = 2.0f;
+        c = phong_or_brdf(env_radiance(sv, L, direction), wo, direction, ret, m);
+        break;
+    }
+    }
+    if (mode == 1.0f) {
+        // hits with gett() beyond |p-L| + eps can never satisfy the blocking test
+        float dl = norm(ret.point - lp);
+        float oabs = fmaxf(fmaxf(fabsf(origin.x), fabsf(origin.y)), fabsf(origin.z));
+        tmax = (dl + sv.shadow_eps) * (1.0f + 1e-4f) + 1e-5f * oabs + 1e-30f;
+        if (!(tmax == tmax)) tmax = FLT_MAX;
+    }
+    sr.o = make_float4(origin.x, origin.y, origin.z, time);
+    sr.d = make_float4(dir.x, dir.y, dir.z, tmax);
+    sr.c = make_float4(c.x, c.y, c.z, mode);
+    sr.L = make_float4(lp.x, lp.y, lp.z, 0.0f);
+}
+
+// ------------------------------------------------------------------ camera / background
+DEV void slot_pixel(const CameraDev& cam, int slot, int s0, int row_offset, int row_stride, int npix, uint32_t& pixel,
+                    uint32_t& sample, int& x, int& y) {
+    int sl = slot / npix, pl = slot - sl * npix;
+    int k = pl / cam.nx;
+    x = pl - k * cam.nx;
+    y = row_offset + k * row_stride;
+    pixel = (uint32_t)(y * cam.nx + x);
+    sample = (uint32_t)(s0 + sl);
+}
+DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f3 dir) {   // Scene.cpp:544-566
+    if (sv.env_light != -1) {
+        const LightDev& L = sv.lights[sv.env_light];
+        if (L.type != RTG_LIGHT_ENVIRONMENT) return ld3(sv.background);
+        float theta = f_acos(dir.y);
+        float phi = f_atan2(dir.z, dir.x);
+        float tu = (float)((-(double)phi + PI_D) / (2 * PI_D));
+        float tv = (float)((double)theta / PI_D);
+        return tex_color(sv, sv.textures[L.tex], tu, tv);
+    }
+    if (sv.bg_texture == -1) return ld3(sv.background);
+    float u = ((float)col) / (float)cam.nx;
+    float v = ((float)row) / (float)cam.ny;
+    return tex_color(sv, sv.textures[sv.bg_texture], u, v);
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, int s0, int row_offset, int row_stride, int npix,
+                                                uint64_t seed, RayRec* __restrict__ rays, RayMeta* __restrict__ meta,
+                                                int n, int max_depth) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t pixel, sample;
+    int x, y;
+    slot_pixel(cam, i, s0, row_offset, row_stride, npix, pixel, sample, x, y);
+    f3 pos = ld3(cam.pos), gaze = ld3(cam.gaze), right = ld3(cam.right), up = ld3(cam.up);
+    f3 o = pos, d;
+    float time = 0.0f;
+    if (cam.total > 1) {
+        // PixelLBCorner (Camera.cpp:84-92) + getSampleRay (:94-113) + AddDepthOfField (:119-139)
+        float u = cam.l + (float)x * cam.pw;
+        float v = cam.t - (float)(y + 1) * cam.ph;
+        f3 m = pos + gaze * cam.dist;
+        m = m + right * u;
+        m = m + up * v;
+        float xi[4];
+        rng4(seed, pixel, sample, 1, RNG_CAMERA, 0, 0, xi);
+        int si = (int)sample;
+        int ii = si % cam.sample_count, jj = si / cam.sample_count;
+        m = m + right * (((float)ii + xi[0]) * cam.sw);
+        m = m + up * (((float)jj + xi[1]) * cam.sh);
+        f3 dv = m - pos;
+        d = dv / norm(dv);
+        if (cam.dof) {
+            float xa = xi[2] - 0.5f, xb = xi[3] - 0.5f;
+            f3 q = pos;
+            q = q + right * (cam.aperture * xa);
+            q = q + up * (cam.aperture * xb);
+            f3 dir = normalized(m - pos);
+            float tfd = cam.focus / dot(dir, gaze);
+            f3 p = pos + d * tfd;
+            o = q;
+            d = normalized(p - q);
+        } else {
+            time = xi[2];
+        }
+    } else {
+        // getPrimaryRay (Camera.cpp:63-72)
+        float u = cam.l + ((cam.r - cam.l) * ((float)x + 0.5f)) * cam.nxDA;
+        float v = cam.t - ((cam.t - cam.b) * ((float)y + 0.5f)) * cam.nyDA;
+        f3 m = pos + gaze * cam.dist;
+        m = m + right * u;
+        m = m + up * v;
+        f3 dv = m - pos;
+        d = dv / norm(dv);
+    }
+    RayRec r;
+    r.o_t = make_float4(o.x, o.y, o.z, time);
+    r.d = make_float4(d.x, d.y, d.z, FLT_MAX);
+    rays[i] = r;
+    RayMeta mt;
+    mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = max_depth;
+    meta[i] = mt;
+}
+
+template <bool EXHAUSTIVE, bool STATS>
+__global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayRec* __restrict__ rays,
+                                                       HitRec* __restrict__ hits, int n, Counters* ctr) {
+    __shared__ int s_stack[kStackDepth * kTraceBlock];
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    Stats st = {0, 0};
+    if (i < n) {
+        RayRec r = rays[i];
+        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, mk(r.o_t.x, r.o_t.y, r.o_t.z), mk(r.d.x, r.d.y, r.d.z), r.o_t.w,
+                                                  r.d.w, s_stack + threadIdx.x, kTraceBlock, st);
+        hits[i] = h;
+    }
+    if (STATS) {
+        unsigned long long nv = st.nodes, nt = st.tris;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_down(nv, off);
+            nt += __shfl_down(nt, off);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&ctr->node_visits, nv);
+            atomicAdd(&ctr->tri_tests, nt);
+        }
+    }
+}
+
+// Wave-aggregated append of 0..2 records per lane (ballot + mbcnt prefix, one atomic per wave).
+DEV int wave_append(int cnt, unsigned* counter) {
+    unsigned long long m1 = __ballot(cnt >= 1);
+    unsigned long long m2 = __ballot(cnt >= 2);
+    unsigned long long lt = __lanemask_lt();
+    int off = __popcll(m1 & lt) + __popcll(m2 & lt);
+    int total = __popcll(m1) + __popcll(m2);
+    int base = 0;
+    int lane = __lane_id();
+    int leader = __ffsll((long long)__ballot(1)) - 1;
+    if (lane == leader && total > 0) base = (int)atomicAdd(counter, (unsigned)total);
+    base = __shfl(base, leader);
+    return base + off;
+}
+
+DEV RayRec make_ray(f3 o, f3 d, float time) {
+    RayRec r;
+    r.o_t = make_float4(o.x, o.y, o.z, time);
+    r.d = make_float4(d.x, d.y, d.z, FLT_MAX);
+    return r;
+}
+
+// Scene::MirrorReflectance (src/Scene.cpp:163-186): reflected ray of node `path`
+DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialDev& m, uint64_t seed,
+                    uint32_t pixel, uint32_t sample, uint64_t path, f3& ro, f3& rd) {
+    f3 wo = -dir;
+    float n_wo = dot(ret.normal, wo);
+    f3 wr = -wo + (ret.normal * 2) * n_wo;
+    wr = wr / norm(wr);
+    if (m.is_rough) {
+        f3 u = ortho_u(wr);
+        f3 v = cross(wr, u);
+        float xi[4];
+        rng4(seed, pixel, sample, path, RNG_ROUGH, 0, 0, xi);
+        float uChi = xi[0] - 0.5f, vChi = xi[1] - 0.5f;
+        wr = normalized(wr + (u * uChi + v * vChi) * m.roughness);
+    }
+    ro = ret.point + ret.normal * sv.shadow_eps;
+    rd = wr;
+}
+
+__global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraDev cam, int level, int s0,
+                                               int row_offset, int row_stride, int npix, uint64_t seed,
+                                               const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
+                                               const HitRec* __restrict__ hits, NodeRec* __restrict__ nodes,
+                                               ShadowRec* __restrict__ shadows, RayRec* __restrict__ next_rays,
+                                               RayMeta* __restrict__ next_meta, unsigned* next_count, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int nchild = 0;
+    RayRec c0r, c1r;
+    RayMeta c0m, c1m;
+    bool has0 = false, has1 = false;
+    NodeRec nd;
+    if (i < n) {
+        RayRec r = rays[i];
+        RayMeta mt = meta[i];
+        HitRec h = hits[i];
+        f3 o = mk(r.o_t.x, r.o_t.y, r.o_t.z), d = mk(r.d.x, r.d.y, r.d.z);
+        float time = r.o_t.w;
+        uint32_t pixel, sample;
+        int x, y;
+        slot_pixel(cam, mt.slot, s0, row_offset, row_stride, npix, pixel, sample, x, y);
+        uint64_t path = ((uint64_t)mt.path_hi << 32) | mt.path_lo;
+        nd.px = nd.py = nd.pz = 0.0f;
+        nd.cr = nd.cg = nd.cb = 0.0f;
+        nd.kind = NK_FINAL;
+        nd.F = 0.0f;
+        nd.child0 = nd.child1 = -1;
+        nd.material = 0;
+        nd.slot = mt.slot;
+        bool basic = false;
+        if (h.obj < 0) {
+            if (level == 0) {
+                // SingleSample passes (row=x, col=y) (Scene.cpp:496-511); MultiSample (row=y, col=x)
+                f3 bg = (cam.total > 1) ? background(sv, cam, y, x, d) : background(sv, cam, x, y, d);
+                nd.cr = bg.x; nd.cg = bg.y; nd.cb = bg.z;
+            }
+        } else {
+            Ret ret = hit_record(sv, o, d, time, h);
+            nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
+            nd.material = ret.matIndex;
+            if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading :361-372
+                nd.cr = ret.tc.x; nd.cg = ret.tc.y; nd.cb = ret.tc.z;
+            } else {
+                const MaterialDev m = sv.materials[ret.matIndex - 1];
+                int depth = mt.depth;
+                uint64_t p0 = 2 * path, p1 = 2 * path + 1;
+                if (m.type == RTG_MAT_NORMAL || depth <= 0) {            // RecursiveShading :286-289
+                    basic = true;
+                } else if (m.type == RTG_MAT_MIRROR) {                   // :290-296
+                    basic = true;
+                    nd.kind = NK_MIRROR;
+                    f3 ro, rd;
+                    mirror_ray(sv, d, ret, m, seed, pixel, sample, path, ro, rd);
+                    if (!(isnan3(ro) || isnan3(rd))) {
+                        has1 = true; c1r = make_ray(ro, rd, time);
+                        c1m.slot = mt.slot; c1m.path_lo = (unsigned)p1; c1m.path_hi = (unsigned)(p1 >> 32); c1m.depth = depth - 1;
+                    }
+                } else if (m.type == RTG_MAT_DIELECTRIC) {               // :297-340, DielectricRefraction :188-249
+                    float dp = dot(d, ret.normal);
+                    float nt = m.refraction_index;
+                    float snell, n_t, n_i;
+                    f3 normal;
+                    bool entering;
+                    if (dp < 0) { snell = 1.0f / nt; normal = ret.normal; n_t = nt; n_i = 1; entering = true; }
+                    else { snell = nt; normal = -ret.normal; n_t = 1; n_i = nt; entering = false; }
+                    float cosTheta = -dot(d, normal);
+                    f3 leftPart = (d + normal * cosTheta) * snell;
+                    float srp = (float)(1 - pow((double)snell, 2.0) * (1 - pow((double)cosTheta, 2.0)));
+                    bool isTir = srp < 0;
+                    srp = sqrtf(srp);
+                    f3 tdir = normalized(leftPart - normal * srp);
+                    f3 torg = ret.point - normal * sv.shadow_eps;
+                    float cos_t = -dot(tdir, normal);
+                    float cos_i = -dot(d, normal);
+                    float rPar = (n_t * cos_i - n_i * cos_t) / (n_t * cos_i + n_i * cos_t);
+                    float rPer = (n_i * cos_i - n_t * cos_t) / (n_i * cos_i + n_t * cos_t);
+                    nd.F = (float)(0.5f * (pow((double)rPar, 2.0) + pow((double)rPer, 2.0)));
+                    nd.kind = entering ? NK_DIEL_ENTER : (isTir ? NK_DIEL_TIR : NK_DIEL_EXIT);
+                    basic = entering;
+                    if (!(isnan3(torg) || isnan3(tdir))) {
+                        // the refracted ray is traced in every case (its hit point feeds Beer's law)
+                        has0 = true; c0r = make_ray(torg, tdir, time);
+                        c0m.slot = mt.slot; c0m.path_lo = (unsigned)p0; c0m.path_hi = (unsigned)(p0 >> 32); c0m.depth = depth - 1;
+                    }
+                    f3 ro, rd;
+                    mirror_ray(sv, d, ret, m, seed, pixel, sample, path, ro, rd);
+                    if (!(isnan3(ro) || isnan3(rd))) {
+                        has1 = true; c1r = make_ray(ro, rd, time);
+                        c1m.slot = mt.slot; c1m.path_lo = (unsigned)p1; c1m.path_hi = (unsigned)(p1 >> 32); c1m.depth = depth - 1;
+                    }
+                } else {                                                 // conductor :341-349
+                    basic = true;
+                    nd.kind = NK_CONDUCTOR;
+                    nd.F = conductor_fresnel(m.refraction_index, m.absorption_index, d, ret.normal);
+                    f3 ro, rd;
+                    mirror_ray(sv, d, ret, m, seed, pixel, sample, path, ro, rd);
+                    if (!(isnan3(ro) || isnan3(rd))) {
+                        has1 = true; c1r = make_ray(ro, rd, time);
+                        c1m.slot = mt.slot; c1m.path_lo = (unsigned)p1; c1m.path_hi = (unsigned)(p1 >> 32); c1m.depth = depth - 1;
+                    }
+                }
+                if (basic) {
+                    // Scene::ambient :153-161 (0 + La*ka), lights added by k_shadow in order
+                    f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
+                    nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
+                    for (int li = 0; li < sv.num_lights; li++)
+                        light_sample(sv, li, d, time, ret, m, seed, pixel, sample, path,
+                                     shadows[(size_t)i * sv.num_lights + li]);
+                }
+            }
+        }
+        if (basic) nd.kind |= 0x100;
+        nchild = (has0 ? 1 : 0) + (has1 ? 1 : 0);
+    }
+    // ballot/prefix-sum compaction of the next level's rays
+    int idx = wave_append(nchild, next_count);
+    if (i < n) {
+        if (has0) { next_rays[idx] = c0r; next_meta[idx] = c0m; nd.child0 = idx; idx++; }
+        if (has1) { next_rays[idx] = c1r; next_meta[idx] = c1m; nd.child1 = idx; }
+        nodes[i] = nd;
+    }
+}
+
+// Shadow queries + in-order light sum of Scene::BasicShading (src/Scene.cpp:374-398).
+template <bool EXHAUSTIVE, bool STATS>
+__global__ void __launch_bounds__(kTraceBlock) k_shadow(const SceneView sv, const ShadowRec* __restrict__ shadows,
+                                                        NodeRec* __restrict__ nodes, int n, unsigned* traced,
+                                                        Counters* ctr) {
+    __shared__ int s_stack[kStackDepth * kTraceBlock];
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned cnt = 0;
+    Stats st = {0, 0};
+    if (i < n) {
+        NodeRec nd = nodes[i];
+        if (nd.kind & 0x100) {
+            f3 col = mk(nd.cr, nd.cg, nd.cb);
+            f3 p = mk(nd.px, nd.py, nd.pz);
+            for (int li = 0; li < sv.num_lights; li++) {
+                const ShadowRec sr = shadows[(size_t)i * sv.num_lights + li];
+                f3 add = mk(0, 0, 0);
+                if (sr.c.w != 0.0f) {
+                    f3 o = mk(sr.o.x, sr.o.y, sr.o.z), d = mk(sr.d.x, sr.d.y, sr.d.z);
+                    if (!(isnan3(o) || isnan3(d))) cnt++;
+                    HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
+                                                              s_stack + threadIdx.x, kTraceBlock, st);
+                    bool blocked;
+                    if (sr.c.w == 1.0f) {
+                        blocked = false;
+                        if (h.obj >= 0) {
+                            f3 hp = o + d * h.t;
+                            blocked = norm(p - mk(sr.L.x, sr.L.y, sr.L.z)) > norm(p - hp);
+                        }
+                    } else {
+                        blocked = h.obj >= 0;
+                    }
+                    if (!blocked) add = mk(sr.c.x, sr.c.y, sr.c.z);
+                }
+                col = col + add;
+            }
+            nd.cr = col.x; nd.cg = col.y; nd.cb = col.z;
+            nodes[i].cr = nd.cr; nodes[i].cg = nd.cg; nodes[i].cb = nd.cb;
+        }
+    }
+    // per-wave reduction of the traced-ray count
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(traced, cnt);
+    if (STATS) {
+        unsigned long long nv = st.nodes, nt = st.tris;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_down(nv, off);
+            nt += __shfl_down(nt, off);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&ctr->shadow_node_visits, nv);
+            atomicAdd(&ctr->shadow_tri_tests, nt);
+        }
+    }
+}
+
+DEV f3 nan_check(f3 c) { return isnan3(c) ? mk(0, 0, 0) : c; }   // Scene::NanCheck :352-359
+
+// Bottom-up combination of RecursiveShading (src/Scene.cpp:279-350) for one level.
+__global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __restrict__ nodes,
+                                                 const NodeRec* __restrict__ child, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    NodeRec nd = nodes[i];
+    int kind = nd.kind & 0xFF;
+    if (kind == NK_FINAL) return;
+    f3 basic = mk(nd.cr, nd.cg, nd.cb);
+    f3 c0 = mk(0, 0, 0), c1 = mk(0, 0, 0), q0 = mk(0, 0, 0);
+    if (nd.child0 >= 0) { const NodeRec& a = child[nd.child0]; c0 = mk(a.cr, a.cg, a.cb); q0 = mk(a.px, a.py, a.pz); }
+    if (nd.child1 >= 0) { const NodeRec& b = child[nd.child1]; c1 = mk(b.cr, b.cg, b.cb); }
+    const MaterialDev& m = sv.materials[nd.material - 1];
+    f3 p = mk(nd.px, nd.py, nd.pz);
+    f3 res;
+    if (kind == NK_MIRROR) {
+        res = basic + cw(ld3(m.mirror), c1);
+    } else if (kind == NK_CONDUCTOR) {
+        f3 rc = c1 * nd.F;
+        rc = cw(ld3(m.mirror), rc);
+        res = basic + rc;
+    } else {
+        float F = nd.F;
+        float bd = norm(q0 - p);                                     // BeerLaw distance :241
+        f3 beer = mk(f_exp(-m.absorption[0] * bd), f_exp(-m.absorption[1] * bd), f_exp(-m.absorption[2] * bd));
+        if (kind == NK_DIEL_ENTER) {
+            f3 inside = c0 * (1 - F);
+            inside = cw(beer, inside);
+            f3 refl = c1 * F;
+            res = (basic + nan_check(inside)) + nan_check(refl);
+        } else if (kind == NK_DIEL_TIR) {
+            res = nan_check(cw(beer, c1));
+        } else {
+            f3 outside = c0 * (1 - F);
+            f3 refl = c1 * F;
+            refl = cw(beer, refl);
+            res = nan_check(outside) + nan_check(refl);
+        }
+    }
+    nodes[i].cr = res.x; nodes[i].cg = res.y; nodes[i].cb = res.z;
+}
+
+// Scene::MultiSample sum order: color += sample_i in sample order (src/Scene.cpp:519-540).
+__global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ level0, float* __restrict__ acc,
+                                                    int npix, int ns, int mode) {
+    int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    f3 a;
+    int s = 0;
+    if (mode == 2) {            // SingleSample: the colour itself
+        const NodeRec& r = level0[p];
+        a = mk(r.cr, r.cg, r.cb);
+        s = 1;
+    } else if (mode == 1) {     // MultiSample: Vector3f color = {0,0,0}; color += ...
+        a = mk(0.0f, 0.0f, 0.0f);
+    } else {
+        a = mk(acc[3 * p], acc[3 * p + 1], acc[3 * p + 2]);
+    }
+    for (; s < ns; s++) {
+        const NodeRec& r = level0[(size_t)s * npix + p];
+        a = a + mk(r.cr, r.cg, r.cb);
+    }
+    acc[3 * p] = a.x; acc[3 * p + 1] = a.y; acc[3 * p + 2] = a.z;
+}
+
+__global__ void __launch_bounds__(256) k_finalize(const float* __restrict__ acc, float* __restrict__ out, int nx,
+                                                  int ny, int row_offset, int row_stride, int total) {
+    int pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= nx * ny) return;
+    int y = pix / nx, x = pix - y * nx;
+    float r = 0.0f, g = 0.0f, b = 0.0f;
+    if (y % row_stride == row_offset) {
+        int pl = (y / row_stride) * nx + x;
+        r = acc[3 * pl]; g = acc[3 * pl + 1]; b = acc[3 * pl + 2];
+        if (total > 1) { r = r / (float)total; g = g / (float)total; b = b / (float)total; }
+    }
+    out[3 * pix] = r; out[3 * pix + 1] = g; out[3 * pix + 2] = b;
+}
+
+__global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const RayRec* __restrict__ rays,
+                                                     const HitRec* __restrict__ hits, rtg_hit* __restrict__ out,
+                                                     const int* __restrict__ orig_prim, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    RayRec r = rays[i];
+    HitRec h = hits[i];
+    rtg_hit o;
+    o.full = h.obj >= 0;
+    o.object = h.obj;
+    o.prim = -1; o.material = 0; o.t = 0.0f;
+    o.point[0] = o.point[1] = o.point[2] = 0.0f;
+    o.normal[0] = o.normal[1] = o.normal[2] = 0.0f;
+    if (h.obj >= 0) {
+        Ret ret = hit_record(sv, mk(r.o_t.x, r.o_t.y, r.o_t.z), mk(r.d.x, r.d.y, r.d.z), r.o_t.w, h);
+        o.prim = orig_prim[h.prim];
+        o.material = ret.matIndex;
+        o.t = h.t;
+        o.point[0] = ret.point.x; o.point[1] = ret.point.y; o.point[2] = ret.point.z;
+        o.normal[0] = ret.normal.x; o.normal[1] = ret.normal.y; o.normal[2] = ret.normal.z;
+    }
+    out[i] = o;
+}
+
+// ------------------------------------------------------------------ launchers
+static inline int nblk(int n, int b) { return (n + b - 1) / b; }
+
+void launch_raygen(const SceneView& sv, const CameraDev& cam, int s0, int ns, int row_offset, int row_stride,
+                   int rows_owned, uint64_t seed, RayRec* rays, RayMeta* meta, int n, hipStream_t st) {
+    (void)ns;
+    if (n <= 0) return;
+    int npix = rows_owned * cam.nx;
+    hipLaunchKernelGGL(k_raygen, dim3(nblk(n, 256)), dim3(256), 0, st, cam, s0, row_offset, row_stride, npix, seed,
+                       rays, meta, n, sv.max_depth);
+}
+void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
+                  hipStream_t st) {
+    if (n <= 0) return;
+    dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
+    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false>), g, b, 0, st, sv, rays, hits, n, ctr);
+    else if (ctr) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, st, sv, rays, hits, n, ctr);
+    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, st, sv, rays, hits, n, ctr);
+}
+void launch_shade(const SceneView& sv, const CameraDev& cam, int level, int s0, int row_offset, int row_stride,
+                  uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
+                  ShadowRec* shadows, RayRec* next_rays, RayMeta* next_meta, unsigned* next_count, int n,
+                  hipStream_t st) {
+    if (n <= 0) return;
+    int rows_owned = (cam.ny - row_offset + row_stride - 1) / row_stride;
+    int npix = rows_owned * cam.nx;
+    hipLaunchKernelGGL(k_shade, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, s0, row_offset, row_stride,
+                       npix, seed, rays, meta, hits, nodes, shadows, next_rays, next_meta, next_count, n);
+}
+void launch_shadow(const SceneView& sv, const ShadowRec* shadows, NodeRec* nodes, int n, int exhaustive,
+                   Counters* ctr, unsigned* traced, hipStream_t st) {
+    if (n <= 0 || sv.num_lights == 0) return;
+    dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, nodes, n, traced, ctr);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, nodes, n, traced, ctr);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, nodes, n, traced, ctr);
+}
+void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, nodes, child_nodes, n);
+}
+void launch_accumulate(const NodeRec* level0, float* acc, int npix, int ns, int mode, hipStream_t st) {
+    if (npix <= 0) return;
+    hipLaunchKernelGGL(k_accumulate, dim3(nblk(npix, 256)), dim3(256), 0, st, level0, acc, npix, ns, mode);
+}
+void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int total,
+                     hipStream_t st) {
+    int n = nx * ny;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_finalize, dim3(nblk(n, 256)), dim3(256), 0, st, acc, out, nx, ny, row_offset, row_stride,
+                       total);
+}
+void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, rtg_hit* out,
+                        const int* orig_prim, int n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_hit_details, dim3(nblk(n, 256)), dim3(256), 0, st, sv, rays, hits, out, orig_prim, n);
+}
+
+}  // namespace rtg

@@ -1,0 +1,986 @@
+// rtg_host.cpp — C ABI of librtg: scene flattening for gfx950 and the wavefront driver.
+//
+// rtg_scene_create() performs what Scene::renderScene() does before its pixel loop
+// (src/Scene.cpp:427-458): transformation matrices with glm's arithmetic
+// (src/Helper.cpp:189-280), smooth vertex normals (src/Shape.cpp:378-406) and one
+// median-split BVH per object (src/BVH.cpp:53-135) — reproduced bit-for-bit, then
+// linearised into 64-byte child-box nodes and pre-gathered triangles in BVH order.
+// rtg_render() drives the per-level kernels of rtg_device.hip.
+#include <float.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/rtg.h"
+#include "rtg_internal.h"
+
+using namespace rtg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(RTG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------------ host vector / glm math
+struct V3 { float x, y, z; };
+inline V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+inline V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+inline V3 operator/(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+inline float sqn(V3 a) { return a.x * a.x + (a.y * a.y + a.z * a.z); }   // Eigen redux order
+inline float vnorm(V3 a) { return sqrtf(sqn(a)); }
+inline V3 normalized(V3 a) {
+    float z = sqn(a);
+    return z > 0.0f ? a / sqrtf(z) : a;
+}
+inline V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+inline float comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+struct Mat4 { float c[4][4]; };   // glm column-major
+Mat4 identity() {
+    Mat4 m;
+    memset(&m, 0, sizeof m);
+    m.c[0][0] = m.c[1][1] = m.c[2][2] = m.c[3][3] = 1.0f;
+    return m;
+}
+Mat4 mul(const Mat4& A, const Mat4& B) {             // glm mat4*mat4, columns summed left to right
+    Mat4 R;
+    for (int i = 0; i < 4; i++)
+        for (int r = 0; r < 4; r++)
+            R.c[i][r] = ((A.c[0][r] * B.c[i][0] + A.c[1][r] * B.c[i][1]) + A.c[2][r] * B.c[i][2]) + A.c[3][r] * B.c[i][3];
+    return R;
+}
+Mat4 translate(const Mat4& m, V3 v) {                // glm::translate
+    Mat4 R = m;
+    for (int r = 0; r < 4; r++) R.c[3][r] = ((m.c[0][r] * v.x + m.c[1][r] * v.y) + m.c[2][r] * v.z) + m.c[3][r];
+    return R;
+}
+Mat4 scale(const Mat4& m, V3 v) {                    // glm::scale
+    Mat4 R = m;
+    for (int r = 0; r < 4; r++) {
+        R.c[0][r] = m.c[0][r] * v.x;
+        R.c[1][r] = m.c[1][r] * v.y;
+        R.c[2][r] = m.c[2][r] * v.z;
+    }
+    return R;
+}
+Mat4 rotate(const Mat4& m, float angle, V3 v) {      // glm::rotate
+    float c = (float)cos((double)angle), s = (float)sin((double)angle);
+    float inv = 1.0f / sqrtf((v.x * v.x + v.y * v.y) + v.z * v.z);
+    V3 ax = v3(v.x * inv, v.y * inv, v.z * inv);
+    float omc = 1.0f - c;
+    V3 tp = v3(omc * ax.x, omc * ax.y, omc * ax.z);
+    float r00 = c + tp.x * ax.x, r01 = tp.x * ax.y + s * ax.z, r02 = tp.x * ax.z - s * ax.y;
+    float r10 = tp.y * ax.x - s * ax.z, r11 = c + tp.y * ax.y, r12 = tp.y * ax.z + s * ax.x;
+    float r20 = tp.z * ax.x + s * ax.y, r21 = tp.z * ax.y - s * ax.x, r22 = c + tp.z * ax.z;
+    Mat4 R;
+    for (int r = 0; r < 4; r++) {
+        R.c[0][r] = (m.c[0][r] * r00 + m.c[1][r] * r01) + m.c[2][r] * r02;
+        R.c[1][r] = (m.c[0][r] * r10 + m.c[1][r] * r11) + m.c[2][r] * r12;
+        R.c[2][r] = (m.c[0][r] * r20 + m.c[1][r] * r21) + m.c[2][r] * r22;
+        R.c[3][r] = m.c[3][r];
+    }
+    return R;
+}
+Mat4 inverse(const Mat4& M) {                        // glm compute_inverse<4,4>
+    const float(*m)[4] = M.c;
+    float C00 = m[2][2] * m[3][3] - m[3][2] * m[2][3], C02 = m[1][2] * m[3][3] - m[3][2] * m[1][3];
+    float C03 = m[1][2] * m[2][3] - m[2][2] * m[1][3], C04 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+    float C06 = m[1][1] * m[3][3] - m[3][1] * m[1][3], C07 = m[1][1] * m[2][3] - m[2][1] * m[1][3];
+    float C08 = m[2][1] * m[3][2] - m[3][1] * m[2][2], C10 = m[1][1] * m[3][2] - m[3][1] * m[1][2];
+    float C11 = m[1][1] * m[2][2] - m[2][1] * m[1][2], C12 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+    float C14 = m[1][0] * m[3][3] - m[3][0] * m[1][3], C15 = m[1][0] * m[2][3] - m[2][0] * m[1][3];
+    float C16 = m[2][0] * m[3][2] - m[3][0] * m[2][2], C18 = m[1][0] * m[3][2] - m[3][0] * m[1][2];
+    float C19 = m[1][0] * m[2][2] - m[2][0] * m[1][2], C20 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+    float C22 = m[1][0] * m[3][1] - m[3][0] * m[1][1], C23 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
+    const float F0[4] = {C00, C00, C02, C03}, F1[4] = {C04, C04, C06, C07}, F2[4] = {C08, C08, C10, C11};
+    const float F3[4] = {C12, C12, C14, C15}, F4[4] = {C16, C16, C18, C19}, F5[4] = {C20, C20, C22, C23};
+    const float V0[4] = {m[1][0], m[0][0], m[0][0], m[0][0]}, V1[4] = {m[1][1], m[0][1], m[0][1], m[0][1]};
+    const float V2[4] = {m[1][2], m[0][2], m[0][2], m[0][2]}, V3a[4] = {m[1][3], m[0][3], m[0][3], m[0][3]};
+    const float SA[4] = {+1, -1, +1, -1}, SB[4] = {-1, +1, -1, +1};
+    Mat4 I;
+    for (int i = 0; i < 4; i++) {
+        I.c[0][i] = ((V1[i] * F0[i] - V2[i] * F1[i]) + V3a[i] * F2[i]) * SA[i];
+        I.c[1][i] = ((V0[i] * F0[i] - V2[i] * F3[i]) + V3a[i] * F4[i]) * SB[i];
+        I.c[2][i] = ((V0[i] * F1[i] - V1[i] * F3[i]) + V3a[i] * F5[i]) * SA[i];
+        I.c[3][i] = ((V0[i] * F2[i] - V1[i] * F4[i]) + V2[i] * F5[i]) * SB[i];
+    }
+    float d0 = m[0][0] * I.c[0][0], d1 = m[0][1] * I.c[1][0], d2 = m[0][2] * I.c[2][0], d3 = m[0][3] * I.c[3][0];
+    float ood = 1.0f / ((d0 + d1) + (d2 + d3));
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++) I.c[c][r] = I.c[c][r] * ood;
+    return I;
+}
+Mat4 inverse_transpose(const Mat4& M) {              // glm::inverseTranspose (gtc/matrix_inverse)
+    const float(*m)[4] = M.c;
+    float S00 = m[2][2] * m[3][3] - m[3][2] * m[2][3], S01 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+    float S02 = m[2][1] * m[3][2] - m[3][1] * m[2][2], S03 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+    float S04 = m[2][0] * m[3][2] - m[3][0] * m[2][2], S05 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+    float S06 = m[1][2] * m[3][3] - m[3][2] * m[1][3], S07 = m[1][1] * m[3][3] - m[3][1] * m[1][3];
+    float S08 = m[1][1] * m[3][2] - m[3][1] * m[1][2], S09 = m[1][0] * m[3][3] - m[3][0] * m[1][3];
+    float S10 = m[1][0] * m[3][2] - m[3][0] * m[1][2], S11 = m[1][1] * m[3][3] - m[3][1] * m[1][3];
+    float S12 = m[1][0] * m[3][1] - m[3][0] * m[1][1], S13 = m[1][2] * m[2][3] - m[2][2] * m[1][3];
+    float S14 = m[1][1] * m[2][3] - m[2][1] * m[1][3], S15 = m[1][1] * m[2][2] - m[2][1] * m[1][2];
+    float S16 = m[1][0] * m[2][3] - m[2][0] * m[1][3], S17 = m[1][0] * m[2][2] - m[2][0] * m[1][2];
+    float S18 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
+    Mat4 I;
+    I.c[0][0] = +((m[1][1] * S00 - m[1][2] * S01) + m[1][3] * S02);
+    I.c[0][1] = -((m[1][0] * S00 - m[1][2] * S03) + m[1][3] * S04);
+    I.c[0][2] = +((m[1][0] * S01 - m[1][1] * S03) + m[1][3] * S05);
+    I.c[0][3] = -((m[1][0] * S02 - m[1][1] * S04) + m[1][2] * S05);
+    I.c[1][0] = -((m[0][1] * S00 - m[0][2] * S01) + m[0][3] * S02);
+    I.c[1][1] = +((m[0][0] * S00 - m[0][2] * S03) + m[0][3] * S04);
+    I.c[1][2] = -((m[0][0] * S01 - m[0][1] * S03) + m[0][3] * S05);
+    I.c[1][3] = +((m[0][0] * S02 - m[0][1] * S04) + m[0][2] * S05);
+    I.c[2][0] = +((m[0][1] * S06 - m[0][2] * S07) + m[0][3] * S08);
+    I.c[2][1] = -((m[0][0] * S06 - m[0][2] * S09) + m[0][3] * S10);
+    I.c[2][2] = +((m[0][0] * S11 - m[0][1] * S09) + m[0][3] * S12);
+    I.c[2][3] = -((m[0][0] * S08 - m[0][1] * S10) + m[0][2] * S12);
+    I.c[3][0] = -((m[0][1] * S13 - m[0][2] * S14) + m[0][3] * S15);
+    I.c[3][1] = +((m[0][0] * S13 - m[0][2] * S16) + m[0][3] * S17);
+    I.c[3][2] = -((m[0][0] * S14 - m[0][1] * S16) + m[0][3] * S18);
+    I.c[3][3] = +((m[0][0] * S15 - m[0][1] * S17) + m[0][2] * S18);
+    float det = ((m[0][0] * I.c[0][0] + m[0][1] * I.c[0][1]) + m[0][2] * I.c[0][2]) + m[0][3] * I.c[0][3];
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++) I.c[c][r] = I.c[c][r] / det;
+    return I;
+}
+// ComputeObjectTransformations composition (src/Helper.cpp:207-230): reverse list order,
+// a Composite replaces the accumulated model.
+Mat4 compose(const rtg_scene_desc* d, int first, int count) {
+    Mat4 M = identity();
+    for (int j = count - 1; j >= 0; j--) {
+        const rtg_xform_ref& x = d->xform_refs[first + j];
+        int k = x.index - 1;
+        switch (x.type) {
+        case RTG_XF_TRANSLATION:
+            M = translate(M, v3(d->translations[3 * k], d->translations[3 * k + 1], d->translations[3 * k + 2]));
+            break;
+        case RTG_XF_SCALING:
+            M = scale(M, v3(d->scalings[3 * k], d->scalings[3 * k + 1], d->scalings[3 * k + 2]));
+            break;
+        case RTG_XF_ROTATION: {
+            const float* rr = d->rotations + 4 * k;
+            M = rotate(M, rr[0] * (float)0.01745329251994329576923690768489, v3(rr[1], rr[2], rr[3]));
+            break;
+        }
+        case RTG_XF_COMPOSITE:
+            memcpy(M.c, d->composites + 16 * k, sizeof(float) * 16);
+            break;
+        default:
+            break;
+        }
+    }
+    return M;
+}
+
+// ------------------------------------------------------------------ BVH construction
+inline float min2(float a, float b) { return a <= b ? a : b; }
+inline float max2(float a, float b) { return a >= b ? a : b; }
+inline float minOf3(float a, float b, float c) {
+    if (a <= b && a <= c) return a;
+    else if (b <= a && b <= c) return b;
+    return c;
+}
+inline float maxOf3(float a, float b, float c) {
+    if (a >= b && a >= c) return a;
+    else if (b >= a && b >= c) return b;
+    return c;
+}
+
+struct HNode {            // pre-order node of the reference tree
+    int left, right;      // node numbers, -1 null
+    int start, end;
+    float mn[3], mx[3];
+};
+
+struct ObjBVH {
+    std::vector<int> perm;        // BVH position -> original prim index
+    std::vector<HNode> nodes;     // pre-order
+    int root = -1;
+};
+
+struct BuildCtx {
+    const V3* centers;            // per original prim
+    const V3* bmin;               // per original prim
+    const V3* bmax;
+    std::vector<int>* prims;      // current permutation
+    std::vector<HNode>* nodes;
+    std::vector<float> scratch;
+};
+
+void range_box(BuildCtx& B, int start, int end, float mn[3], float mx[3]) {   // ComputeBoundingBox :268-283
+    float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX, b0 = -FLT_MAX, b1 = -FLT_MAX, b2 = -FLT_MAX;
+    const int* p = B.prims->data();
+    for (int i = start; i < end; i++) {
+        const V3 lo = B.bmin[p[i]], hi = B.bmax[p[i]];
+        a0 = min2(a0, lo.x); a1 = min2(a1, lo.y); a2 = min2(a2, lo.z);
+        b0 = max2(b0, hi.x); b1 = max2(b1, hi.y); b2 = max2(b2, hi.z);
+    }
+    mn[0] = a0; mn[1] = a1; mn[2] = a2; mx[0] = b0; mx[1] = b1; mx[2] = b2;
+}
+
+// BVH::ConstructionHelper (src/BVH.cpp:64-110).  FindMedian's sort (:117-135) is replaced by
+// nth_element selection, which yields the same order statistics.
+int construct(BuildCtx& B, int start, int end, int splitType, int depth) {
+    if (start == end - 1 || depth >= 30) {
+        int n = (int)B.nodes->size();
+        HNode h;
+        h.left = h.right = -1; h.start = start; h.end = end;
+        range_box(B, start, end, h.mn, h.mx);
+        B.nodes->push_back(h);
+        return n;
+    }
+    if (start == end) return -1;
+    if (splitType > 2) splitType = 0;
+    int n = (int)B.nodes->size();
+    {
+        HNode h;
+        h.left = h.right = -1; h.start = start; h.end = end;
+        range_box(B, start, end, h.mn, h.mx);
+        B.nodes->push_back(h);
+    }
+    int* p = B.prims->data();
+    int len = end - start;
+    B.scratch.resize(len);
+    for (int i = 0; i < len; i++) B.scratch[i] = comp(B.centers[p[start + i]], splitType);
+    int mi = len / 2;
+    std::nth_element(B.scratch.begin(), B.scratch.begin() + mi, B.scratch.end());
+    float split = B.scratch[mi];
+    if (len % 2 == 0) {
+        float lower = *std::max_element(B.scratch.begin(), B.scratch.begin() + mi);
+        split = (lower + split) * 0.5f;
+    }
+    int swapIndex = start;
+    for (int i = start; i < end; i++) {
+        if (comp(B.centers[p[i]], splitType) < split) {
+            std::swap(p[swapIndex], p[i]);
+            swapIndex++;
+        }
+    }
+    int l = construct(B, start, swapIndex, splitType + 1, depth + 1);
+    int r = construct(B, swapIndex, end, splitType + 1, depth + 1);
+    (*B.nodes)[n].left = l;
+    (*B.nodes)[n].right = r;
+    return n;
+}
+
+// ------------------------------------------------------------------ device buffer helper
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int grow(size_t need) {
+        if (need <= bytes) return RTG_OK;
+        if (p) hipFree(p);
+        p = nullptr; bytes = 0;
+        size_t want = need + need / 4 + 256;
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            return fail(RTG_ERR_OOM, "hipMalloc failed (" + std::to_string(want) + " bytes)");
+        }
+        bytes = want;
+        return RTG_OK;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+    void release() { if (p) hipFree(p); p = nullptr; bytes = 0; }
+};
+
+template <class T>
+int upload(DBuf& b, const std::vector<T>& v) {
+    size_t n = std::max<size_t>(v.size(), 1) * sizeof(T);
+    int rc = b.grow(n);
+    if (rc) return rc;
+    if (!v.empty()) HIP_TRY(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RTG_OK;
+}
+
+struct Level {
+    DBuf rays, meta, hits, nodes, shadows;
+};
+
+}  // namespace
+
+struct rtg_scene {
+    int device = 0;
+    int num_objects = 0, num_instances = 0, num_vertices = 0;
+    std::vector<ObjBVH> bvh;                 // per object
+    std::vector<Mat4> inv, invT;             // per top-level entry
+    std::vector<float> vnormals;
+    std::vector<int> orig_prim;              // absolute BVH position -> original prim index
+    SceneView sv{};
+    DBuf d_tops, d_geoms, d_nodes, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
+        d_texels, d_lights, d_origprim;
+    // render workspace
+    std::vector<Level> levels;
+    DBuf d_acc, d_counters, d_stats;
+    rtg_render_stats stats{};
+};
+
+extern "C" {
+
+int32_t rtg_abi_version(void) { return RTG_ABI_VERSION; }
+const char* rtg_last_error(void) { return g_err.c_str(); }
+
+int32_t rtg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static int validate(const rtg_scene_desc* d) {
+    if (!d) return fail(RTG_ERR_INVALID, "null scene descriptor");
+    if (d->abi_version != RTG_ABI_VERSION) return fail(RTG_ERR_INVALID, "abi_version mismatch");
+    if (d->num_vertices < 0 || (d->num_vertices && !d->vertices)) return fail(RTG_ERR_INVALID, "bad vertices");
+    if (d->num_objects < 0 || (d->num_objects && !d->objects)) return fail(RTG_ERR_INVALID, "bad objects");
+    if (d->num_lights > kMaxLights) return fail(RTG_ERR_UNSUPPORTED, "more than 64 lights");
+    auto vok = [&](int v) { return v >= 1 && v <= d->num_vertices; };
+    auto xok = [&](int first, int count) {
+        if (count < 0 || first < 0 || first + count > d->num_xform_refs) return false;
+        for (int j = 0; j < count; j++) {
+            const rtg_xform_ref& x = d->xform_refs[first + j];
+            int lim = x.type == RTG_XF_TRANSLATION ? d->num_translations
+                      : x.type == RTG_XF_SCALING   ? d->num_scalings
+                      : x.type == RTG_XF_ROTATION  ? d->num_rotations
+                      : x.type == RTG_XF_COMPOSITE ? d->num_composites : -1;
+            if (lim < 0 || x.index < 1 || x.index > lim) return false;
+        }
+        return true;
+    };
+    for (int i = 0; i < d->num_objects; i++) {
+        const rtg_object_desc& o = d->objects[i];
+        if (o.material < 1 || o.material > d->num_materials)
+            return fail(RTG_ERR_INVALID, "object " + std::to_string(i) + ": material out of range");
+        if (o.num_textures < 0 || o.num_textures > 2) return fail(RTG_ERR_INVALID, "object textures");
+        for (int t = 0; t < o.num_textures; t++)
+            if (o.textures[t] < 1 || o.textures[t] > d->num_textures) return fail(RTG_ERR_INVALID, "object texture index");
+        if (!xok(o.xform_first, o.xform_count)) return fail(RTG_ERR_INVALID, "object transformation reference");
+        if (o.type == RTG_OBJ_SPHERE) {
+            if (!vok(o.center)) return fail(RTG_ERR_INVALID, "sphere center index");
+        } else if (o.type == RTG_OBJ_TRIANGLE) {
+            if (!vok(o.v[0]) || !vok(o.v[1]) || !vok(o.v[2])) return fail(RTG_ERR_INVALID, "triangle index");
+        } else if (o.type == RTG_OBJ_MESH) {
+            if (o.face_first < 0 || o.face_count < 0 || o.face_first + o.face_count > d->num_faces)
+                return fail(RTG_ERR_INVALID, "mesh face range");
+            for (int f = 0; f < o.face_count; f++)
+                for (int q = 0; q < 3; q++)
+                    if (!vok(d->faces[3 * (o.face_first + f) + q])) return fail(RTG_ERR_INVALID, "mesh face index");
+        } else {
+            return fail(RTG_ERR_INVALID, "object type");
+        }
+    }
+    for (int i = 0; i < d->num_instances; i++) {
+        const rtg_instance_desc& in = d->instances[i];
+        if (in.base_object < 0 || in.base_object >= d->num_objects) return fail(RTG_ERR_INVALID, "instance base");
+        if (in.material < 1 || in.material > d->num_materials) return fail(RTG_ERR_INVALID, "instance material");
+        if (!xok(in.xform_first, in.xform_count)) return fail(RTG_ERR_INVALID, "instance transformation reference");
+    }
+    for (int i = 0; i < d->num_textures; i++) {
+        const rtg_texture_desc& t = d->textures[i];
+        if (t.kind == RTG_TEX_IMAGE && (t.width < 1 || t.height < 1 || !t.texels))
+            return fail(RTG_ERR_INVALID, "image texture without texels");
+    }
+    for (int i = 0; i < d->num_lights; i++)
+        if (d->lights[i].type == RTG_LIGHT_ENVIRONMENT &&
+            (d->lights[i].texture < 0 || d->lights[i].texture >= d->num_textures))
+            return fail(RTG_ERR_INVALID, "environment light texture");
+    if (d->background_texture >= d->num_textures) return fail(RTG_ERR_INVALID, "background texture");
+    if (d->environment_light >= d->num_lights) return fail(RTG_ERR_INVALID, "environment light index");
+    return RTG_OK;
+}
+
+static void scene_free(rtg_scene* s) {
+    DBuf* bufs[] = {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_tris, &s->d_primidx, &s->d_vertices, &s->d_vnormals,
+                    &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights, &s->d_origprim,
+                    &s->d_acc, &s->d_counters, &s->d_stats};
+    for (DBuf* b : bufs) b->release();
+    for (Level& l : s->levels) { l.rays.release(); l.meta.release(); l.hits.release(); l.nodes.release(); l.shadows.release(); }
+}
+
+int32_t rtg_scene_destroy(rtg_scene* s) {
+    if (!s) return RTG_OK;
+    if (s->device >= 0) (void)hipSetDevice(s->device);
+    scene_free(s);
+    delete s;
+    return RTG_OK;
+}
+
+static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
+    const int nv = d->num_vertices;
+    std::vector<V3> verts(nv);
+    for (int i = 0; i < nv; i++) verts[i] = v3(d->vertices[3 * i], d->vertices[3 * i + 1], d->vertices[3 * i + 2]);
+    s->num_objects = d->num_objects;
+    s->num_instances = d->num_instances;
+    s->num_vertices = nv;
+
+    // per-object primitive lists in parse order
+    struct ObjPrims { std::vector<int> v; };   // 3 per prim (sphere: center,0,0)
+    std::vector<ObjPrims> op(d->num_objects);
+    for (int i = 0; i < d->num_objects; i++) {
+        const rtg_object_desc& o = d->objects[i];
+        if (o.type == RTG_OBJ_MESH) op[i].v.assign(d->faces + 3 * o.face_first, d->faces + 3 * (o.face_first + o.face_count));
+        else if (o.type == RTG_OBJ_TRIANGLE) op[i].v = {o.v[0], o.v[1], o.v[2]};
+        else op[i].v = {o.center, 0, 0};
+    }
+
+    // matrices (objects, then instances)
+    std::vector<Mat4> model(d->num_objects);
+    s->inv.clear(); s->invT.clear();
+    for (int i = 0; i < d->num_objects; i++) {
+        model[i] = compose(d, d->objects[i].xform_first, d->objects[i].xform_count);
+        s->inv.push_back(inverse(model[i]));
+        s->invT.push_back(inverse_transpose(model[i]));
+    }
+    for (int i = 0; i < d->num_instances; i++) {
+        const rtg_instance_desc& in = d->instances[i];
+        Mat4 m = compose(d, in.xform_first, in.xform_count);
+        if (!in.reset_transform) m = mul(m, model[in.base_object]);
+        s->inv.push_back(inverse(m));
+        s->invT.push_back(inverse_transpose(m));
+    }
+
+    // smooth vertex normals (src/Scene.cpp:433-449)
+    std::vector<V3> vn(nv, v3(0, 0, 0));
+    for (int i = 0; i < d->num_objects; i++) {
+        const rtg_object_desc& o = d->objects[i];
+        if (!(o.type == RTG_OBJ_TRIANGLE || (o.type == RTG_OBJ_MESH && o.smooth))) continue;
+        const std::vector<int>& pv = op[i].v;
+        for (size_t k = 0; k + 2 < pv.size(); k += 3) {
+            V3 a = verts[pv[k] - 1], b = verts[pv[k + 1] - 1], c = verts[pv[k + 2] - 1];
+            V3 n = normalized(cross(c - b, a - b));
+            for (int q = 0; q < 3; q++) vn[pv[k + q] - 1] = vn[pv[k + q] - 1] + n;
+        }
+    }
+    s->vnormals.resize(3 * (size_t)nv);
+    for (int i = 0; i < nv; i++) {
+        V3 n = normalized(vn[i]);
+        s->vnormals[3 * i] = n.x; s->vnormals[3 * i + 1] = n.y; s->vnormals[3 * i + 2] = n.z;
+    }
+
+    // BVHs and device geometry
+    std::vector<Geometry> geoms(d->num_objects);
+    std::vector<Node> dnodes;
+    std::vector<TriGeom> tris;
+    std::vector<int4> primidx;
+    s->orig_prim.clear();
+    s->bvh.assign(d->num_objects, ObjBVH());
+    const float ieps = d->intersection_test_eps;
+    for (int i = 0; i < d->num_objects; i++) {
+        const rtg_object_desc& o = d->objects[i];
+        const std::vector<int>& pv = op[i].v;
+        int np = (int)(pv.size() / 3);
+        std::vector<V3> centers(np), bmin(np), bmax(np);
+        for (int k = 0; k < np; k++) {
+            if (o.type == RTG_OBJ_SPHERE) {                            // Shape.cpp:171-183
+                V3 c = verts[o.center - 1];
+                float R = o.radius;
+                centers[k] = c;
+                bmin[k] = v3(c.x - R, c.y - R, c.z - R);
+                bmax[k] = v3(c.x + R, c.y + R, c.z + R);
+            } else {                                                  // Shape.cpp:278-306
+                V3 a = verts[pv[3 * k] - 1], b = verts[pv[3 * k + 1] - 1], c = verts[pv[3 * k + 2] - 1];
+                centers[k] = v3(((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f);
+                bmin[k] = v3(minOf3(a.x, b.x, c.x), minOf3(a.y, b.y, c.y), minOf3(a.z, b.z, c.z));
+                bmax[k] = v3(maxOf3(a.x, b.x, c.x), maxOf3(a.y, b.y, c.y), maxOf3(a.z, b.z, c.z));
+            }
+        }
+        ObjBVH& ob = s->bvh[i];
+        ob.perm.resize(np);
+        for (int k = 0; k < np; k++) ob.perm[k] = k;
+        BuildCtx B{centers.data(), bmin.data(), bmax.data(), &ob.perm, &ob.nodes, {}};
+        ob.nodes.reserve(2 * (size_t)np + 1);
+        ob.root = construct(B, 0, np, 0, 0);
+
+        Geometry& g = geoms[i];
+        memset(&g, 0, sizeof g);
+        g.type = o.type;
+        g.prim_base = (int)tris.size();
+        g.nprims = np;
+        g.num_textures = o.num_textures;
+        g.textures[0] = o.textures[0];
+        g.textures[1] = o.textures[1];
+        g.texture_offset = (o.type == RTG_OBJ_MESH) ? o.texture_offset : 0;
+        g.smooth = o.smooth;
+        if (o.type == RTG_OBJ_SPHERE) {
+            V3 c = verts[o.center - 1];
+            g.center[0] = c.x; g.center[1] = c.y; g.center[2] = c.z;
+            g.radius = o.radius;
+            g.center_index = o.center;
+        }
+        // primitives in BVH order
+        float pad = 0.0f;
+        for (int k = 0; k < np; k++) {
+            int f = ob.perm[k];
+            TriGeom tg;
+            memset(&tg, 0, sizeof tg);
+            int4 pi;
+            if (o.type == RTG_OBJ_SPHERE) {
+                pi = make_int4(o.center, 0, 0, 0);
+            } else {
+                int i1 = pv[3 * f], i2 = pv[3 * f + 1], i3 = pv[3 * f + 2];
+                V3 a = verts[i1 - 1], b = verts[i2 - 1], c = verts[i3 - 1];
+                V3 amb = a - b, amc = a - c;
+                tg.p0 = make_float4(a.x, a.y, a.z, amb.x);
+                tg.p1 = make_float4(amb.y, amb.z, amc.x, amc.y);
+                float fi;
+                memcpy(&fi, &f, 4);
+                tg.p2 = make_float4(amc.z, fi, 0.0f, 0.0f);
+                int smooth = (o.type == RTG_OBJ_TRIANGLE) ? 1 : o.smooth;   // Shape.cpp:378-392 quirk
+                pi = make_int4(i1, i2, i3, smooth);
+                double e = (double)(ieps > 0 ? ieps : 0.0f);
+                double ext = e * ((double)vnorm(b - a) + (double)vnorm(c - a));
+                pad = std::max(pad, (float)(ext * 1.02 + 1e-7));
+            }
+            tris.push_back(tg);
+            primidx.push_back(pi);
+            s->orig_prim.push_back(f);
+        }
+        g.prune_pad = pad;
+        // linearise interior nodes (pre-order) into child-box nodes
+        const std::vector<HNode>& hn = ob.nodes;
+        std::vector<int> dev_index(hn.size(), -1);
+        int node_base = (int)dnodes.size();
+        int cnt = 0;
+        for (size_t k = 0; k < hn.size(); k++)
+            if (hn[k].left >= 0 || hn[k].right >= 0) dev_index[k] = node_base + cnt++;
+        dnodes.resize(node_base + cnt);
+        for (size_t k = 0; k < hn.size(); k++) {
+            if (dev_index[k] < 0) continue;
+            Node nd;
+            float box[2][6];
+            int ref[2], count[2];
+            int ch[2] = {hn[k].left, hn[k].right};
+            for (int q = 0; q < 2; q++) {
+                int c = ch[q];
+                for (int z = 0; z < 6; z++) box[q][z] = 0.0f;
+                if (c < 0) { ref[q] = 0; count[q] = -1; continue; }
+                const HNode& cn = hn[c];
+                for (int z = 0; z < 3; z++) { box[q][z] = cn.mn[z]; box[q][3 + z] = cn.mx[z]; }
+                if (cn.left < 0 && cn.right < 0) {
+                    int len = cn.end - cn.start;
+                    ref[q] = g.prim_base + cn.start;
+                    count[q] = len > 0 ? len : -1;
+                } else {
+                    ref[q] = dev_index[c];
+                    count[q] = 0;
+                }
+            }
+            nd.a = make_float4(box[0][0], box[0][1], box[0][2], box[0][3]);
+            nd.b = make_float4(box[0][4], box[0][5], box[1][0], box[1][1]);
+            nd.c = make_float4(box[1][2], box[1][3], box[1][4], box[1][5]);
+            nd.d = make_int4(ref[0], ref[1], count[0], count[1]);
+            dnodes[dev_index[k]] = nd;
+        }
+        if (ob.root < 0) {
+            g.node_base = -1; g.root_leaf_start = g.prim_base; g.root_leaf_count = -1;
+        } else if (hn[ob.root].left < 0 && hn[ob.root].right < 0) {
+            int len = hn[ob.root].end - hn[ob.root].start;
+            g.node_base = -1;
+            g.root_leaf_start = g.prim_base + hn[ob.root].start;
+            g.root_leaf_count = len > 0 ? len : -1;
+        } else {
+            g.node_base = dev_index[ob.root];
+            g.root_leaf_start = 0; g.root_leaf_count = -1;
+            for (int z = 0; z < 3; z++) { g.root_min[z] = hn[ob.root].mn[z]; g.root_max[z] = hn[ob.root].mx[z]; }
+        }
+    }
+
+    // top-level entries
+    std::vector<TopObject> tops(d->num_objects + d->num_instances);
+    for (int i = 0; i < d->num_objects + d->num_instances; i++) {
+        TopObject& T = tops[i];
+        memset(&T, 0, sizeof T);
+        memcpy(T.inv, s->inv[i].c, 64);
+        memcpy(T.invT, s->invT[i].c, 64);
+        if (i < d->num_objects) {
+            const rtg_object_desc& o = d->objects[i];
+            T.blur[0] = o.blur[0]; T.blur[1] = o.blur[1]; T.blur[2] = o.blur[2];
+            T.kind = o.type == RTG_OBJ_SPHERE ? 0 : 1;
+            T.material = o.material;
+            T.geom = i;
+        } else {
+            const rtg_instance_desc& in = d->instances[i - d->num_objects];
+            T.blur[0] = in.blur[0]; T.blur[1] = in.blur[1]; T.blur[2] = in.blur[2];
+            T.kind = d->objects[in.base_object].type == RTG_OBJ_SPHERE ? 0 : 1;
+            T.material = in.material;
+            T.geom = in.base_object;
+            T.is_instance = 1;
+        }
+    }
+
+    // materials, textures, lights
+    std::vector<MaterialDev> mats(d->num_materials);
+    for (int i = 0; i < d->num_materials; i++) {
+        const rtg_material_desc& m = d->materials[i];
+        MaterialDev& M = mats[i];
+        M.type = m.type; M.brdf = m.brdf; M.phong_exp = m.phong_exp; M.is_rough = m.is_rough; M.roughness = m.roughness;
+        memcpy(M.ambient, m.ambient, 12); memcpy(M.diffuse, m.diffuse, 12); memcpy(M.specular, m.specular, 12);
+        memcpy(M.mirror, m.mirror, 12);
+        M.refraction_index = m.refraction_index; M.absorption_index = m.absorption_index;
+        memcpy(M.absorption, m.absorption_coeff, 12);
+    }
+    std::vector<TextureDev> texs(d->num_textures);
+    std::vector<float> texels;
+    for (int i = 0; i < d->num_textures; i++) {
+        const rtg_texture_desc& t = d->textures[i];
+        TextureDev& T = texs[i];
+        T.kind = t.kind; T.decal = t.decal; T.interp = t.interp; T.nc = t.noise_conv; T.normalizer = t.normalizer;
+        T.noise_scale = t.noise_scale; T.bump = t.bump_factor; T.w = t.width; T.h = t.height;
+        T.texel_offset = (long long)texels.size();
+        if (t.kind == RTG_TEX_IMAGE && t.texels) texels.insert(texels.end(), t.texels, t.texels + (size_t)t.width * t.height * 3);
+    }
+    std::vector<LightDev> lights(d->num_lights);
+    for (int i = 0; i < d->num_lights; i++) {
+        const rtg_light_desc& l = d->lights[i];
+        LightDev& L = lights[i];
+        memset(&L, 0, sizeof L);
+        L.type = l.type;
+        memcpy(L.pos, l.position, 12); memcpy(L.inten, l.intensity, 12);
+        L.size = l.size; L.tex = l.texture;
+        V3 dir = v3(l.direction[0], l.direction[1], l.direction[2]);
+        if (l.type == RTG_LIGHT_DIRECTIONAL || l.type == RTG_LIGHT_SPOT) {   // Light.cpp:394-398, 465-474
+            V3 n = normalized(dir);
+            L.dir[0] = n.x; L.dir[1] = n.y; L.dir[2] = n.z;
+        }
+        if (l.type == RTG_LIGHT_SPOT) {
+            L.coverage = (float)((double)(l.coverage_deg * 0.5f) * (3.14159265358979323846 / 180.0f));
+            L.fall = (float)((double)(l.falloff_deg * 0.5f) * (3.14159265358979323846 / 180.0f));
+            L.cos_fall = (float)cos((double)L.fall);
+            L.cos_cov = (float)cos((double)L.coverage);
+        }
+        if (l.type == RTG_LIGHT_AREA) {                                      // Light.cpp:580-593
+            V3 n = normalized(dir);
+            float a0 = fabsf(n.x), a1 = fabsf(n.y), a2 = fabsf(n.z);
+            V3 nl = n;
+            if (a0 <= a1 && a0 <= a2) nl.x = 1.0f;
+            else if (a1 <= a0 && a1 <= a2) nl.y = 1.0f;
+            else nl.z = 1.0f;
+            V3 u = normalized(cross(n, nl));
+            V3 v = cross(n, u);
+            L.normal[0] = n.x; L.normal[1] = n.y; L.normal[2] = n.z;
+            L.u[0] = u.x; L.u[1] = u.y; L.u[2] = u.z;
+            L.v[0] = v.x; L.v[1] = v.y; L.v[2] = v.z;
+        }
+    }
+
+    if (s->device < 0) return RTG_OK;   // host-only build (introspection / CPU tests)
+    std::vector<float> vflat(d->vertices, d->vertices + 3 * (size_t)nv);
+    std::vector<float> tcflat;
+    if (d->num_texcoords > 0) tcflat.assign(d->texcoords, d->texcoords + 2 * (size_t)d->num_texcoords);
+    int rc;
+    if ((rc = upload(s->d_tops, tops)) || (rc = upload(s->d_geoms, geoms)) || (rc = upload(s->d_nodes, dnodes)) ||
+        (rc = upload(s->d_tris, tris)) || (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_vertices, vflat)) ||
+        (rc = upload(s->d_vnormals, s->vnormals)) || (rc = upload(s->d_texcoords, tcflat)) ||
+        (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
+        (rc = upload(s->d_lights, lights)) || (rc = upload(s->d_origprim, s->orig_prim)))
+        return rc;
+
+    SceneView& sv = s->sv;
+    sv.tops = s->d_tops.as<TopObject>(); sv.num_tops = (int)tops.size(); sv.num_objects = d->num_objects;
+    sv.geoms = s->d_geoms.as<Geometry>();
+    sv.nodes = s->d_nodes.as<Node>();
+    sv.tris = s->d_tris.as<TriGeom>();
+    sv.prim_idx = s->d_primidx.as<int4>();
+    sv.vertices = s->d_vertices.as<float>();
+    sv.vnormals = s->d_vnormals.as<float>();
+    sv.texcoords = s->d_texcoords.as<float>();
+    sv.num_texcoords = d->num_texcoords;
+    sv.materials = s->d_materials.as<MaterialDev>(); sv.num_materials = d->num_materials;
+    sv.textures = s->d_textures.as<TextureDev>(); sv.num_textures = d->num_textures;
+    sv.texels = s->d_texels.as<float>();
+    sv.lights = s->d_lights.as<LightDev>(); sv.num_lights = d->num_lights;
+    sv.max_depth = d->max_recursion_depth;
+    sv.shadow_eps = d->shadow_ray_eps;
+    sv.int_eps = d->intersection_test_eps;
+    memcpy(sv.background, d->background, 12);
+    memcpy(sv.ambient, d->ambient_light, 12);
+    sv.bg_texture = d->background_texture;
+    sv.env_light = d->environment_light;
+    return RTG_OK;
+}
+
+int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene** out) {
+    if (!out) return fail(RTG_ERR_INVALID, "null out pointer");
+    *out = nullptr;
+    int rc = validate(desc);
+    if (rc) return rc;
+    if (device >= 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RTG_ERR_NO_DEVICE, "no HIP device");
+        if (device >= n) return fail(RTG_ERR_NO_DEVICE, "device index out of range");
+        HIP_TRY(hipSetDevice(device));
+    } else if (device != RTG_DEVICE_HOST_ONLY) {
+        return fail(RTG_ERR_INVALID, "device index");
+    }
+    rtg_scene* s = new (std::nothrow) rtg_scene();
+    if (!s) return fail(RTG_ERR_OOM, "host allocation");
+    s->device = device;
+    rc = build_scene(s, desc);
+    if (rc) {
+        scene_free(s);
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return RTG_OK;
+}
+
+// Camera::Camera (src/Camera.cpp:7-61)
+static CameraDev make_camera(const rtg_camera_desc* c) {
+    CameraDev k;
+    memset(&k, 0, sizeof k);
+    int i = 1;
+    k.sample_count = 1;
+    while (i < 1000) {
+        if (i * i >= c->num_samples) { k.sample_count = i; break; }
+        i++;
+    }
+    V3 gz = v3(c->gaze[0], c->gaze[1], c->gaze[2]), up = v3(c->up[0], c->up[1], c->up[2]);
+    V3 g = normalized(gz);
+    V3 w = c->left_handed ? normalized(gz) : normalized(v3(-gz.x, -gz.y, -gz.z));
+    V3 right = normalized(cross(up, w));
+    V3 u2 = cross(w, right);
+    memcpy(k.pos, c->position, 12);
+    k.gaze[0] = g.x; k.gaze[1] = g.y; k.gaze[2] = g.z;
+    k.up[0] = u2.x; k.up[1] = u2.y; k.up[2] = u2.z;
+    k.right[0] = right.x; k.right[1] = right.y; k.right[2] = right.z;
+    k.l = c->left; k.r = c->right; k.b = c->bottom; k.t = c->top; k.dist = c->near_distance;
+    k.nx = c->nx; k.ny = c->ny;
+    k.nxDA = 1.0f / (float)c->nx;
+    k.nyDA = 1.0f / (float)c->ny;
+    k.pw = (k.r - k.l) * k.nxDA;
+    k.ph = (k.t - k.b) * k.nyDA;
+    k.sw = k.pw / (float)k.sample_count;
+    k.sh = k.ph / (float)k.sample_count;
+    k.total = c->num_samples;
+    k.dof = c->is_dof;
+    k.focus = c->focus_distance;
+    k.aperture = c->aperture_size;
+    return k;
+}
+
+static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, float* out_dev,
+                       hipStream_t st) {
+    if (cam->nx < 1 || cam->ny < 1 || cam->num_samples < 1) return fail(RTG_ERR_INVALID, "bad camera");
+    rtg_render_opts o{};
+    if (opts) o = *opts;
+    int stride = o.row_stride > 1 ? o.row_stride : 1;
+    int off = o.row_offset;
+    if (off < 0 || off >= stride) return fail(RTG_ERR_INVALID, "row_offset out of range");
+    CameraDev cd = make_camera(cam);
+    int rows_owned = (cam->ny - off + stride - 1) / stride;
+    if (rows_owned < 0) rows_owned = 0;
+    long long npix_ll = (long long)rows_owned * cam->nx;
+    if (npix_ll > (1LL << 30)) return fail(RTG_ERR_UNSUPPORTED, "image too large");
+    int npix = (int)npix_ll;
+    int total = cam->num_samples;
+    long long max_batch = o.max_batch_rays > 0 ? o.max_batch_rays : (4LL << 20);
+    int ns_pass = npix > 0 ? (int)std::max<long long>(1, std::min<long long>(total, max_batch / std::max(npix, 1))) : 1;
+    int exhaustive = o.traversal == 1;
+    const int nL = s->sv.num_lights;
+
+    int rc;
+    if ((rc = s->d_acc.grow(sizeof(float) * 3 * std::max<size_t>(npix, 1)))) return rc;
+    if ((rc = s->d_counters.grow(sizeof(unsigned) * 64))) return rc;
+    if ((rc = s->d_stats.grow(sizeof(Counters)))) return rc;
+    unsigned* d_cnt = s->d_counters.as<unsigned>();
+    Counters* d_stats = s->d_stats.as<Counters>();
+    HIP_TRY(hipMemsetAsync(s->d_counters.p, 0, sizeof(unsigned) * 64, st));
+    HIP_TRY(hipMemsetAsync(s->d_stats.p, 0, sizeof(Counters), st));
+
+    struct Events {                     // RAII: released on every return path
+        hipEvent_t e[6] = {};
+        ~Events() { for (hipEvent_t x : e) if (x) (void)hipEventDestroy(x); }
+    } ev;
+    for (hipEvent_t& x : ev.e) HIP_TRY(hipEventCreate(&x));
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
+    HIP_TRY(hipEventRecord(e0, st));
+    const bool timing = o.collect_timing != 0;
+    Counters* sctr = o.collect_stats ? d_stats : nullptr;
+
+    rtg_render_stats stt{};
+    std::vector<int> counts;
+    const int max_levels = std::max(0, s->sv.max_depth) + 1;
+    for (int s0 = 0; s0 < total && npix > 0; s0 += ns_pass) {
+        int ns = std::min(ns_pass, total - s0);
+        int n0 = ns * npix;
+        counts.assign(1, n0);
+        if ((int)s->levels.size() < 1) s->levels.resize(1);
+        Level& L0 = s->levels[0];
+        if ((rc = L0.rays.grow(sizeof(RayRec) * (size_t)n0)) || (rc = L0.meta.grow(sizeof(RayMeta) * (size_t)n0)))
+            return rc;
+        launch_raygen(s->sv, cd, s0, ns, off, stride, rows_owned, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(),
+                      n0, st);
+        stt.primary_rays += (uint64_t)n0;
+        int level = 0;
+        for (;; level++) {
+            int n = counts[level];
+            if ((int)s->levels.size() < level + 2) s->levels.resize(level + 2);
+            Level& Lc = s->levels[level];
+            Level& Ln = s->levels[level + 1];
+            if ((rc = Lc.hits.grow(sizeof(HitRec) * (size_t)n)) || (rc = Lc.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
+                (rc = Lc.shadows.grow(sizeof(ShadowRec) * (size_t)n * std::max(nL, 1))))
+                return rc;
+            bool may_spawn = level + 1 < max_levels;
+            size_t cap = may_spawn ? 2 * (size_t)n : 1;
+            if ((rc = Ln.rays.grow(sizeof(RayRec) * cap)) || (rc = Ln.meta.grow(sizeof(RayMeta) * cap))) return rc;
+            if (timing) HIP_TRY(hipEventRecord(ev.e[2], st));
+            launch_trace(s->sv, Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, st);
+            if (timing) HIP_TRY(hipEventRecord(ev.e[3], st));
+            HIP_TRY(hipMemsetAsync(d_cnt + 1 + level, 0, sizeof(unsigned), st));
+            launch_shade(s->sv, cd, level, s0, off, stride, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(),
+                         Lc.hits.as<HitRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Ln.rays.as<RayRec>(),
+                         Ln.meta.as<RayMeta>(), d_cnt + 1 + level, n, st);
+            if (timing) HIP_TRY(hipEventRecord(ev.e[4], st));
+            launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, st);
+            if (timing) HIP_TRY(hipEventRecord(ev.e[5], st));
+            HIP_TRY(hipGetLastError());
+            unsigned next = 0;
+            HIP_TRY(hipMemcpyAsync(&next, d_cnt + 1 + level, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (timing) {
+                float a = 0.0f, b = 0.0f;
+                HIP_TRY(hipEventElapsedTime(&a, ev.e[2], ev.e[3]));
+                stt.trace_ms += a;
+                stt.trace_launches++;
+                if (nL > 0) {
+                    HIP_TRY(hipEventElapsedTime(&b, ev.e[4], ev.e[5]));
+                    stt.shadow_ms += b;
+                    stt.shadow_launches++;
+                }
+            }
+            if (next > cap) return fail(RTG_ERR_HIP, "secondary queue overflow");
+            if (next == 0 || !may_spawn) break;
+            counts.push_back((int)next);
+            stt.secondary_rays += next;
+            if (level + 1 >= 62) return fail(RTG_ERR_UNSUPPORTED, "recursion deeper than 62 levels");
+        }
+        stt.max_level = std::max(stt.max_level, level);
+        for (int l = level - 1; l >= 0; l--)
+            launch_resolve(s->sv, s->levels[l].nodes.as<NodeRec>(), s->levels[l + 1].nodes.as<NodeRec>(), counts[l], st);
+        int mode = (total == 1) ? 2 : (s0 == 0 ? 1 : 0);
+        launch_accumulate(s->levels[0].nodes.as<NodeRec>(), s->d_acc.as<float>(), npix, ns, mode, st);
+        stt.passes++;
+    }
+    launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, cam->ny, off, stride, total, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e1, st));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    unsigned shadow_cnt = 0;
+    Counters ctr{};
+    HIP_TRY(hipMemcpy(&shadow_cnt, d_cnt, sizeof(unsigned), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&ctr, d_stats, sizeof(Counters), hipMemcpyDeviceToHost));
+    stt.shadow_rays = shadow_cnt;
+    stt.total_rays = stt.primary_rays + stt.secondary_rays + stt.shadow_rays;
+    stt.render_ms = ms;
+    stt.node_visits = ctr.node_visits;
+    stt.tri_tests = ctr.tri_tests;
+    stt.shadow_node_visits = ctr.shadow_node_visits;
+    stt.shadow_tri_tests = ctr.shadow_tri_tests;
+    s->stats = stt;
+    return RTG_OK;
+}
+
+int32_t rtg_render_device(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, float* rgb_out_device,
+                          void* stream) {
+    if (!s || !cam || !rgb_out_device) return fail(RTG_ERR_INVALID, "null argument");
+    if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
+    HIP_TRY(hipSetDevice(s->device));
+    return render_impl(s, cam, opts, rgb_out_device, (hipStream_t)stream);
+}
+
+int32_t rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, float* rgb_out) {
+    if (!s || !cam || !rgb_out) return fail(RTG_ERR_INVALID, "null argument");
+    if (cam->nx < 1 || cam->ny < 1) return fail(RTG_ERR_INVALID, "bad camera");
+    if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
+    HIP_TRY(hipSetDevice(s->device));
+    size_t bytes = sizeof(float) * 3 * (size_t)cam->nx * cam->ny;
+    float* d_out = nullptr;
+    HIP_TRY(hipMalloc(&d_out, bytes));
+    int rc = render_impl(s, cam, opts, d_out, nullptr);
+    if (rc == RTG_OK) {
+        hipError_t e = hipMemcpy(rgb_out, d_out, bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(RTG_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    }
+    hipFree(d_out);
+    return rc;
+}
+
+int32_t rtg_last_render_stats(const rtg_scene* s, rtg_render_stats* out) {
+    if (!s || !out) return fail(RTG_ERR_INVALID, "null argument");
+    *out = s->stats;
+    return RTG_OK;
+}
+
+int32_t rtg_trace_closest(rtg_scene* s, const rtg_ray* rays, int32_t n, rtg_hit* hits, int32_t traversal) {
+    if (!s || n < 0 || (n && (!rays || !hits))) return fail(RTG_ERR_INVALID, "bad arguments");
+    if (n == 0) return RTG_OK;
+    if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot trace");
+    HIP_TRY(hipSetDevice(s->device));
+    std::vector<RayRec> rr(n);
+    for (int i = 0; i < n; i++) {
+        rr[i].o_t = make_float4(rays[i].origin[0], rays[i].origin[1], rays[i].origin[2], rays[i].time);
+        rr[i].d = make_float4(rays[i].direction[0], rays[i].direction[1], rays[i].direction[2], FLT_MAX);
+    }
+    DBuf dr, dh, dout;
+    int rc;
+    if ((rc = upload(dr, rr)) || (rc = dh.grow(sizeof(HitRec) * (size_t)n)) || (rc = dout.grow(sizeof(rtg_hit) * (size_t)n))) {
+        dr.release(); dh.release(); dout.release();
+        return rc;
+    }
+    launch_trace(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), n, traversal == 1, nullptr, nullptr);
+    launch_hit_details(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), dout.as<rtg_hit>(), s->d_origprim.as<int>(), n, nullptr);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(hits, dout.p, sizeof(rtg_hit) * (size_t)n, hipMemcpyDeviceToHost);
+    dr.release(); dh.release(); dout.release();
+    if (e != hipSuccess) return fail(RTG_ERR_HIP, std::string("trace: ") + hipGetErrorString(e));
+    return RTG_OK;
+}
+
+int32_t rtg_scene_object_bvh(const rtg_scene* s, int32_t object, int32_t* num_prims, int32_t* num_nodes, int32_t* perm,
+                             int32_t* nodes, float* boxes) {
+    if (!s || object < 0 || object >= s->num_objects) return fail(RTG_ERR_INVALID, "object index");
+    const ObjBVH& b = s->bvh[object];
+    if (num_prims) *num_prims = (int)b.perm.size();
+    if (num_nodes) *num_nodes = (int)b.nodes.size();
+    if (perm) memcpy(perm, b.perm.data(), sizeof(int) * b.perm.size());
+    for (size_t k = 0; k < b.nodes.size(); k++) {
+        const HNode& h = b.nodes[k];
+        if (nodes) { nodes[4 * k] = h.left; nodes[4 * k + 1] = h.right; nodes[4 * k + 2] = h.start; nodes[4 * k + 3] = h.end; }
+        if (boxes) for (int z = 0; z < 3; z++) { boxes[6 * k + z] = h.mn[z]; boxes[6 * k + 3 + z] = h.mx[z]; }
+    }
+    return RTG_OK;
+}
+
+int32_t rtg_scene_object_matrices(const rtg_scene* s, int32_t top, float* inv16, float* invT16) {
+    if (!s || top < 0 || top >= (int)s->inv.size()) return fail(RTG_ERR_INVALID, "object index");
+    if (inv16) memcpy(inv16, s->inv[top].c, 64);
+    if (invT16) memcpy(invT16, s->invT[top].c, 64);
+    return RTG_OK;
+}
+
+int32_t rtg_scene_vertex_normals(const rtg_scene* s, float* normals) {
+    if (!s || !normals) return fail(RTG_ERR_INVALID, "null argument");
+    memcpy(normals, s->vnormals.data(), sizeof(float) * s->vnormals.size());
+    return RTG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,194 @@
+// rtg_internal.h — layouts shared by the host scene builder (rtg_host.cpp) and the
+// HIP kernels (rtg_device.hip).  Everything here is device-resident, read-only data
+// laid out for gfx950 gathers, plus the per-level wavefront queue records.
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/rtg.h"
+
+namespace rtg {
+
+constexpr int kMaxLights = 64;      // per-node shadow slots are statically strided
+constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
+constexpr int kTraceBlock = 256;
+
+// One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:86-127):
+// objects first, then instances.  Read with scalar loads (wave-uniform loop).
+struct TopObject {
+    float inv[16];          // glm::inverse(model), column-major
+    float invT[16];         // glm::inverseTranspose(model)
+    float blur[3];
+    int kind;               // 0 = sphere, 1 = triangle BVH (Triangle or Mesh)
+    int material;           // 1-based (instance override applied)
+    int geom;               // index of the geometry (base mesh for instances)
+    int is_instance;
+    int pad0;
+};
+
+// Per geometry (one per object; instances share their base mesh's geometry).
+struct Geometry {
+    int type;               // rtg_object_type
+    int node_base;          // absolute index of the BVH root in the node array (-1 if root is a leaf)
+    int root_leaf_start;    // absolute prim range when the root is a leaf (no box test)
+    int root_leaf_count;    // -1: no primitives at all
+    float root_min[3];      // root box (tested only when the root is interior)
+    float root_max[3];
+    int prim_base;          // absolute index of BVH position 0
+    int nprims;
+    float prune_pad;        // max distance a hit point can lie outside its primitive's box
+    int num_textures;
+    int textures[2];        // 1-based
+    int texture_offset;
+    int smooth;
+    // sphere
+    float center[3];
+    float radius;
+    int center_index;       // 1-based vertex index
+    int pad1;
+};
+
+// 64-byte BVH2 node holding both children's boxes (the reference tests a node's own box
+// when it is visited; testing the child's box from its parent is the same predicate).
+// a = {Lmin.xyz, Lmax.x}, b = {Lmax.yz, Rmin.xy}, c = {Rmin.z, Rmax.xyz},
+// d = {lref, rref, lcount, rcount}: count 0 -> interior child (ref = absolute node index),
+// count > 0 -> leaf child with prims [ref, ref+count) (absolute), count < 0 -> null child.
+// A leaf child's box is the range box of its primitives, used only for pruning.
+struct Node {
+    float4 a, b, c;
+    int4 d;
+};
+
+// Triangle in BVH order: the Cramer-rule operands of Triangle::bvhIntersect
+// (src/Shape.cpp:415-432): a, a-b, a-c.  w lanes: x = original face index.
+struct TriGeom {
+    float4 p0;  // a.xyz, (a-b).x
+    float4 p1;  // (a-b).yz, (a-c).xy
+    float4 p2;  // (a-c).z, orig_index (bits), 0, 0
+};
+
+struct LightDev {
+    int type;
+    float pos[3], dir[3], inten[3];
+    float coverage, fall, size;
+    float normal[3], u[3], v[3];
+    int tex;
+    float cos_fall, cos_cov;   // host-computed cos() of fall/coverage (same convention)
+};
+
+struct TextureDev {
+    int kind, decal, interp, nc, normalizer;
+    float noise_scale, bump;
+    int w, h;
+    long long texel_offset;    // into the texel pool (floats)
+};
+
+struct MaterialDev {
+    int type, brdf, phong_exp, is_rough;
+    float roughness;
+    float ambient[3], diffuse[3], specular[3], mirror[3];
+    float refraction_index, absorption_index;
+    float absorption[3];
+};
+
+// Everything a kernel needs, passed by value.
+struct SceneView {
+    const TopObject* tops; int num_tops; int num_objects;
+    const Geometry* geoms;
+    const Node* nodes;
+    const TriGeom* tris;
+    const int4* prim_idx;          // BVH order: {v1,v2,v3 (1-based), smooth}; spheres {c,0,0,0}
+    const float* vertices;         // xyz
+    const float* vnormals;         // xyz
+    const float* texcoords;        // uv
+    int num_texcoords;
+    const MaterialDev* materials; int num_materials;
+    const TextureDev* textures; int num_textures;
+    const float* texels;
+    const LightDev* lights; int num_lights;
+    int max_depth;
+    float shadow_eps, int_eps;
+    float background[3], ambient[3];
+    int bg_texture, env_light;
+};
+
+struct CameraDev {
+    float pos[3], gaze[3], up[3], right[3];
+    float l, r, b, t, dist;
+    int nx, ny;
+    float nxDA, nyDA, pw, ph, sw, sh;
+    int sample_count, total;
+    int dof;
+    float focus, aperture;
+};
+
+// Wavefront queue records -------------------------------------------------------
+struct RayRec {         // 32 B: the Ray of src/Ray.h
+    float4 o_t;         // origin.xyz, time
+    float4 d;           // direction.xyz, tmax bound (world t) for shadow queries
+};
+struct RayMeta {        // 16 B
+    int slot;           // sample slot in the batch
+    unsigned path_lo, path_hi;
+    int depth;          // remaining recursion depth (RecursiveShading's `depth`)
+};
+struct HitRec {         // 16 B
+    int obj;            // top-level index, -1 miss
+    int prim;           // BVH-order absolute prim index
+    float t;            // gett distance
+    int pad;
+};
+
+enum NodeKind : int {
+    NK_FINAL = 0,       // color final (basic-only leaf, background, replace_all, miss)
+    NK_MIRROR = 1,
+    NK_DIEL_ENTER = 2,
+    NK_DIEL_TIR = 3,
+    NK_DIEL_EXIT = 4,
+    NK_CONDUCTOR = 5
+};
+
+struct NodeRec {        // 48 B, one per traced ray
+    float px, py, pz;   // world hit point ((0,0,0) on a miss, src/Helper.cpp:75)
+    float cr, cg, cb;   // basic shading, then the resolved color
+    int kind;
+    float F;            // dielectric Fresnel / conductor Fresnel
+    int child0, child1; // refracted / reflected child index in the next level (-1 none)
+    int material;
+    int slot;
+};
+
+struct ShadowRec {      // 64 B, nLights per shading node
+    float4 o;           // origin.xyz, time
+    float4 d;           // direction.xyz, tmax (world t bound; +inf for directional/env)
+    float4 c;           // contribution rgb, mode (0 none, 1 distance test, 2 any hit)
+    float4 L;           // light point for the distance test, pad
+};
+
+struct Counters {
+    unsigned long long node_visits, tri_tests;           // closest-hit kernel
+    unsigned long long shadow_node_visits, shadow_tri_tests;
+};
+
+// Host-side launchers (rtg_device.hip) ------------------------------------------------
+struct LevelBuffers;
+void launch_raygen(const SceneView& sv, const CameraDev& cam, int s0, int ns, int row_offset, int row_stride,
+                   int rows_owned, uint64_t seed, RayRec* rays, RayMeta* meta, int n, hipStream_t st);
+void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive,
+                  Counters* ctr, hipStream_t st);
+void launch_shade(const SceneView& sv, const CameraDev& cam, int level, int s0, int row_offset, int row_stride,
+                  uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
+                  ShadowRec* shadows, RayRec* next_rays, RayMeta* next_meta, unsigned* next_count, int n,
+                  hipStream_t st);
+void launch_shadow(const SceneView& sv, const ShadowRec* shadows, NodeRec* nodes, int n, int exhaustive,
+                   Counters* ctr, unsigned* traced, hipStream_t st);
+void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st);
+// mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
+void launch_accumulate(const NodeRec* level0, float* acc, int npix, int ns, int mode, hipStream_t st);
+void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int total,
+                     hipStream_t st);
+void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,
+                        const int* orig_prim, int n, hipStream_t st);
+
+}  // namespace rtg
