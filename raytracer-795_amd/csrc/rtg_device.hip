@@ -110,13 +110,38 @@ DEV bool box_test(f3 o, f3 d, float mnx, float mny, float mnz, float mxx, float 
     float le = max3(txe, tye, tze);
     return !(sl < le);
 }
-// Conservative lower bound of |p - o| over points p within `pad` of the box (pruning only).
-DEV float box_lb(f3 o, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float pad, float oabs) {
+// Same predicate, decided with reciprocal multiplies when that is provably safe.
+// q = fl(fl(b-o) * fl(1/d)) is within 3 ulp of the exact t = fl(fl(b-o)/d), so the min3/max3
+// of either set differ by < 2^-21 (|sl|+|le|); outside that band the fast answer equals the
+// exact one, inside it (and whenever 1/d is not finite: d = +-0, denormal d) the exact
+// division test decides.  NaN cannot arise on the fast path (all operands finite).
+DEV bool box_hit(f3 o, f3 d, f3 inv, bool fast_ok, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
+    if (fast_ok) {
+        float ax = (mnx - o.x) * inv.x, bx = (mxx - o.x) * inv.x;
+        float ay = (mny - o.y) * inv.y, by = (mxy - o.y) * inv.y;
+        float az = (mnz - o.z) * inv.z, bz = (mxz - o.z) * inv.z;
+        float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+        if (sl < le - e) return false;
+        if (sl >= le + e) return true;
+    }
+    return box_test(o, d, mnx, mny, mnz, mxx, mxy, mxz);
+}
+// Squared Euclidean distance from o to the box (pruning / ordering only).
+DEV float box_dist2(f3 o, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
     float dx = fmaxf(fmaxf(mnx - o.x, o.x - mxx), 0.0f);
     float dy = fmaxf(fmaxf(mny - o.y, o.y - mxy), 0.0f);
     float dz = fmaxf(fmaxf(mnz - o.z, o.z - mxz), 0.0f);
-    float l = __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
-    return l * (1.0f - 1e-5f) - pad - 1e-6f * (oabs + l);
+    return dx * dx + dy * dy + dz * dz;
+}
+// Subtrees whose squared box distance exceeds this can hold no candidate at distance <= bound:
+// candidates lie within `pad` of their primitive's box; margins cover rounding of p = o+d*t,
+// of |p-o| and of the squared distance itself.
+DEV float prune_threshold2(float bound, float pad, float oabs) {
+    if (!(bound < FLT_MAX)) return INFINITY;
+    float r = (bound + pad) * (1.0f + 1e-5f) + 1e-6f * (oabs + bound) + 1e-30f;
+    return r * r * (1.0f + 1e-5f);
 }
 // Eigen 3x3 determinant (row-0 expansion) of the matrix with columns c0, c1, c2
 DEV float det3(f3 c0, f3 c1, f3 c2) {
@@ -225,10 +250,21 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     if (!(boundD == boundD)) boundD = FLT_MAX;
                 }
             }
-            float oabs = fmaxf(fmaxf(fabsf(o2.x), fabsf(o2.y)), fabsf(o2.z));
             const float pad = g.prune_pad;
             float best_d = FLT_MAX;
             int best_leaf = -1;
+            const f3 inv = mk(1.0f / d2.x, 1.0f / d2.y, 1.0f / d2.z);
+            const bool fast = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+            // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
+            // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
+            // skipped when its box, expanded by `pad`, meets the line only outside that window.
+            const float padt = fast ? pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z)) : 0.0f;
+            const float tlo = -(fabsf(eps) + 1e-6f);
+            const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+            const float inv_dn = 1.0f / dnorm;
+            float thi = INFINITY;
+            if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
+            const float tm_global = thi;
             auto leaf = [&](int start, int count) {
                 for (int k = start; k < start + count; k++) {
                     const TriGeom tg = sv.tris[k];
@@ -239,54 +275,66 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         if (dist < FLT_MAX &&
                             (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
                             best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                            if (!EXHAUSTIVE) thi = fminf(tm_global, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                         }
                     }
                 }
             };
+            // one child box: reachability (interior, exact predicate) + window pruning + entry key
+            auto child = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool interior,
+                             float& key) -> bool {
+                key = 0.0f;
+                if (!EXHAUSTIVE && fast) {
+                    float ax = (mnx - o2.x) * inv.x, bx = (mxx - o2.x) * inv.x;
+                    float ay = (mny - o2.y) * inv.y, by = (mxy - o2.y) * inv.y;
+                    float az = (mnz - o2.z) * inv.z, bz = (mxz - o2.z) * inv.z;
+                    float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                    float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                    float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                    float lo = le - e - padt, hi = sl + e + padt;
+                    key = lo;
+                    if (hi < lo || hi < tlo || lo > thi) return false;
+                    if (!interior) return true;
+                    if (sl < le - e) return false;
+                    if (sl >= le + e) return true;
+                    return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+                }
+                if (!interior) return true;
+                return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+            };
             if (g.node_base < 0) {
                 if (g.root_leaf_count > 0) leaf(g.root_leaf_start, g.root_leaf_count);
-            } else if (box_test(o2, d2, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0], g.root_max[1],
-                                g.root_max[2])) {
+            } else if (box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
+                               g.root_max[1], g.root_max[2])) {
                 int sp = 0;
                 int cur = g.node_base;
                 while (true) {
                     if (STATS) st.nodes += 2;   // one 64-B node = two 32-B child records
                     const Node nd = sv.nodes[cur];
                     const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
-                    float bound = EXHAUSTIVE ? FLT_MAX : fminf(best_d, boundD);
-                    bool lok = false, rok = false;
-                    float llb = 0.0f, rlb = 0.0f;
-                    if (lcnt >= 0) {
-                        if (!EXHAUSTIVE) llb = box_lb(o2, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, pad, oabs);
-                        lok = EXHAUSTIVE || !(llb > bound);
-                        if (lok && lcnt == 0) lok = box_test(o2, d2, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y);
-                    }
-                    if (rcnt >= 0) {
-                        if (!EXHAUSTIVE) rlb = box_lb(o2, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, pad, oabs);
-                        rok = EXHAUSTIVE || !(rlb > bound);
-                        if (rok && rcnt == 0) rok = box_test(o2, d2, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w);
-                    }
+                    float lk = 0.0f, rk = 0.0f;
+                    bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
+                    bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
                     // leaf children are resolved immediately, nearer first
                     bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
-                    if (lleaf && rleaf && rlb < llb) {
+                    if (lleaf && rleaf && rk < lk) {
                         leaf(rref, rcnt);
-                        if (EXHAUSTIVE || !(llb > fminf(best_d, boundD))) leaf(lref, lcnt);
+                        if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
                         lok = rok = false;
                     } else {
                         if (lleaf) { leaf(lref, lcnt); lok = false; }
                         if (rleaf) {
-                            if (EXHAUSTIVE || !(rlb > fminf(best_d, boundD))) leaf(rref, rcnt);
+                            if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
                             rok = false;
                         }
                     }
-                    if (!EXHAUSTIVE && (lok || rok)) {
-                        bound = fminf(best_d, boundD);
-                        lok = lok && !(llb > bound);
-                        rok = rok && !(rlb > bound);
+                    if (!EXHAUSTIVE) {
+                        lok = lok && !(lk > thi);
+                        rok = rok && !(rk > thi);
                     }
                     if (lok && rok) {
                         int nearc = lref, farc = rref;
-                        if (rlb < llb) { nearc = rref; farc = lref; }
+                        if (rk < lk) { nearc = rref; farc = lref; }
                         stack[sp * sstride] = farc;
                         sp++;
                         cur = nearc;
