@@ -128,3 +128,15 @@ class Oracle:
 
 def rng_uniform(seed, pixel, sample, path, purpose, light, it, lane):
     return load().orc_rng_uniform(seed, pixel, sample, path, purpose, light, it, lane)
+
+
+def philox4x32_10(ctr, key):
+    lib = load()
+    f = lib.orc_philox4x32_10
+    f.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    f.restype = None
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    f(c, k, o)
+    return list(o)

@@ -254,14 +254,21 @@ static inline void philox_round(uint32_t c[4], const uint32_t k[2]) {
     uint32_t n0 = hi1 ^ c[1] ^ k[0], n2 = hi0 ^ c[3] ^ k[1];
     c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
 }
-static void rng4(uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, uint32_t purpose,
-                 uint32_t light, uint32_t iter, float out[4]) {
-    uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(path >> 32)};
-    uint32_t c[4] = {pixel, sample, (uint32_t)path, (purpose << 28) | ((light & 0xFFFu) << 16) | (iter & 0xFFFFu)};
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 philox4x32_R(10)) */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    uint32_t k[2] = {key[0], key[1]};
     for (int r = 0; r < 10; r++) {
         philox_round(c, k);
         k[0] += 0x9E3779B9u; k[1] += 0xBB67AE85u;
     }
+    memcpy(out, c, sizeof c);
+}
+static void rng4(uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, uint32_t purpose,
+                 uint32_t light, uint32_t iter, float out[4]) {
+    uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(path >> 32)};
+    uint32_t c[4] = {pixel, sample, (uint32_t)path, (purpose << 28) | ((light & 0xFFFu) << 16) | (iter & 0xFFFFu)};
+    orc_philox4x32_10(c, k, c);
     for (int i = 0; i < 4; i++) {
         /* libstdc++ generate_canonical<float,24>: (float)u / 2^32, clamped below 1 */
         float f = (float)c[i] / 4294967296.0f;

@@ -41,6 +41,8 @@ int orc_object_bvh(const orc_scene* s, int object, int32_t* num_prims, int32_t* 
 int orc_object_matrices(const orc_scene* s, int top_object, float* inv16, float* invT16);
 int orc_vertex_normals(const orc_scene* s, float* normals);
 
+/* Raw Philox4x32-10 block (checked against the Random123 known-answer vectors). */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* Philox4x32-10 uniform draw shared bit-for-bit with the device code (for tests). */
 float orc_rng_uniform(uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path,
                       uint32_t purpose, uint32_t light, uint32_t iter, int lane);

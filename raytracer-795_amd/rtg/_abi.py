@@ -11,6 +11,7 @@ import os
 RTG_ABI_VERSION = 1
 
 RTG_OK = 0
+RTG_DEVICE_HOST_ONLY = -1
 STATUS = {0: "RTG_OK", -1: "RTG_ERR_INVALID", -2: "RTG_ERR_NO_DEVICE", -3: "RTG_ERR_OOM",
           -4: "RTG_ERR_HIP", -5: "RTG_ERR_UNSUPPORTED"}
 
@@ -155,6 +156,14 @@ def load_library(path: str | None = None):
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise RtgError(f"librtg.so not found at {p}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # PyTorch-ROCm ships its own libamdhip64.so.7.  Loading torch first makes librtg bind to
+    # that same HIP runtime (one runtime per process), so torch streams / allocations can be
+    # handed to rtg_render_device.  Loading librtg first would pull /opt/rocm's runtime in as
+    # a second instance and torch would then see no GPU.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     lib = C.CDLL(p)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(lib, name)

@@ -904,12 +904,12 @@ def write_xml(sc: Scene, xml_path: str, images: dict | None = None) -> str:
         for t in maps:
             ty = "image" if t.kind == A.TEX_IMAGE else "perlin"
             out.append(f'<TextureMap type="{ty}">')
+            # every field is written: Parser.h carries unset fields over from the previous map
             if t.kind == A.TEX_IMAGE:
                 out.append(f"<ImageId>{t.image_id}</ImageId>")
-                out.append(f"<Interpolation>{'bilinear' if t.interp == A.INTERP_BILINEAR else 'nearest'}</Interpolation>")
-            else:
-                out.append(f"<NoiseConversion>{'absval' if t.noise_conv == A.NC_ABSVAL else 'linear'}</NoiseConversion>")
-                out.append(f"<NoiseScale>{_fmt(t.noise_scale)}</NoiseScale>")
+            out.append(f"<Interpolation>{'bilinear' if t.interp == A.INTERP_BILINEAR else 'nearest'}</Interpolation>")
+            out.append(f"<NoiseConversion>{'absval' if t.noise_conv == A.NC_ABSVAL else 'linear'}</NoiseConversion>")
+            out.append(f"<NoiseScale>{_fmt(t.noise_scale)}</NoiseScale>")
             if t.decal in dnames:
                 out.append(f"<DecalMode>{dnames[t.decal]}</DecalMode>")
             out.append(f"<Normalizer>{t.normalizer}</Normalizer>")

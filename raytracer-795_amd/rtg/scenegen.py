@@ -175,7 +175,8 @@ def dragon1m(nx=1920, ny=1080, spp=64, nu=1000, nv=500) -> Scene:
     v, f = uv_sphere(nu, nv)
     b = _add_vertices(sc, v)
     sc.objects.append(Object(type=A.OBJ_MESH, id=1, material=1, faces=(f + b).astype(np.int32),
-                             ply_file="dragon1m.ply"))
+                             ply_file="dragon1m.ply",
+                             texture_offset=len(sc.texcoords) + 1 - b))   # what Parser.h:1087-1147 derives
     sc.lights.append(Light(type=A.LIGHT_POINT, position=(3, 5, 4), intensity=(22000, 22000, 22000)))
     return sc
 
