@@ -59,7 +59,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=64)
-    ap.add_argument("--cpu-rows", type=int, default=2)
+    ap.add_argument("--cpu-rows", type=int, default=540)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -159,6 +159,8 @@ def main():
                            "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
                            "parallelism": f"row-interleaved pixel shards x{world} + RCCL reduce"},
                 "rays_per_frame": rays // max(args.steps, 1),
+                "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
+                "kernel_ms_rank0": {"trace": round(st["trace_ms"], 2), "shadow": round(st["shadow_ms"], 2)},
                 "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     r.close()
