@@ -558,6 +558,8 @@ DEV void triangle_texture(const SceneView& sv, const Geometry& g, int4 vi, f3 e1
 // Re-derive the full ReturnVal of a hit found by closest_hit: the winning primitive's
 // object-space intersection (identical arithmetic), texturing, then the top-level
 // world point and TransformNormal (src/Helper.cpp:93-131).
+// FULL = false: the scene has no textures (the host checks), so texturing is compiled out.
+template <bool FULL = true>
 DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h) {
     const TopObject& T = sv.tops[h.obj];
     const Geometry& g = sv.geoms[T.geom];
@@ -565,6 +567,7 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h)
     transform_ray(T, o, d, time, o2, d2);
     Ret ret;
     ret.matIndex = T.material;
+    ret.dm = RTG_DECAL_NONE;
     ret.tc = mk(0, 0, 0);
     ret.tn = 0;
     if (g.type == RTG_OBJ_SPHERE) {
@@ -573,7 +576,7 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h)
         ret.point = ip;
         f3 pc = ip - ld3(g.center);
         ret.normal = pc / norm(pc);
-        sphere_texture(sv, g, ret);
+        if (FULL) sphere_texture(sv, g, ret);
     } else {
         const TriGeom tg = sv.tris[h.prim];
         Cand c = tri_test(tg, o2, d2, sv.int_eps);
@@ -591,7 +594,7 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h)
         }
         ret.normal = normal / norm(normal);
         ret.point = c.p;
-        triangle_texture(sv, g, vi, b - a, cc - a, c.beta, c.gamma, ret);
+        if (FULL) triangle_texture(sv, g, vi, b - a, cc - a, c.beta, c.gamma, ret);
     }
     float t = gett(o2, d2, ret.point);
     ret.point = o + d * t;
@@ -691,8 +694,9 @@ DEV f3 specular_term(f3 LC, f3 wo, f3 wi, const Ret& ret, const MaterialDev& m) 
     float alpha = fmax0(dot(ret.normal, h));
     return cw(LC, ld3(m.specular) * f_powi(alpha, m.phong_exp));
 }
+template <bool FULL = true>
 DEV f3 phong_or_brdf(f3 LC, f3 wo, f3 wi, const Ret& ret, const MaterialDev& m) {
-    if (m.brdf != RTG_BRDF_NONE) return brdf(wi, wo, ret.normal, LC, m);
+    if (FULL && m.brdf != RTG_BRDF_NONE) return brdf(wi, wo, ret.normal, LC, m);
     float alpha = fmax0(dot(ret.normal, wi));
     return diffuse_term(LC, ret, m, alpha) + specular_term(LC, wo, wi, ret, m);
 }
@@ -706,6 +710,7 @@ DEV f3 env_radiance(const SceneView& sv, const LightDev& L, f3 dir) {   // Light
 }
 
 // Unshadowed contribution of light li plus the shadow query it needs.
+template <bool FULL = true>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
                       uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
     const LightDev& L = sv.lights[li];
@@ -723,13 +728,13 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         mode = 1.0f;
         float dist = norm(ret.point - pos);
         f3 LC = ld3(L.inten) / (dist * dist);
-        c = phong_or_brdf(LC, wo, normalized(pos - ret.point), ret, m);
+        c = phong_or_brdf<FULL>(LC, wo, normalized(pos - ret.point), ret, m);
         break;
     }
     case RTG_LIGHT_DIRECTIONAL: {                               // :447-459
         dir = -ld3(L.dir);
         mode = 2.0f;
-        c = phong_or_brdf(ld3(L.inten), wo, dir, ret, m);
+        c = phong_or_brdf<FULL>(ld3(L.inten), wo, dir, ret, m);
         break;
     }
     case RTG_LIGHT_SPOT: {                                      // :547-574
@@ -743,7 +748,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
             mode = 1.0f;
             float dist = norm(ret.point - pos);
             f3 LC = ld3(L.inten) / (dist * dist);
-            c = phong_or_brdf(LC, wo, normalized(pos - ret.point), ret, m);
+            c = phong_or_brdf<FULL>(LC, wo, normalized(pos - ret.point), ret, m);
             if (!(angle < L.fall)) {
                 float fo = (float)pow((cos((double)angle) - (double)L.cos_cov) / (double)(L.cos_fall - L.cos_cov), 4.0);
                 c = c * fo;
@@ -751,7 +756,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         }
         break;
     }
-    case RTG_LIGHT_AREA: {                                      // :660-683
+    case RTG_LIGHT_AREA: if constexpr (FULL) {                 // :660-683
         float xi[4];
         rng4(seed, pixel, sample, path, RNG_AREA, (uint32_t)li, 0, xi);
         float uChi = xi[0] - 0.5f, vChi = xi[1] - 0.5f;
@@ -765,10 +770,10 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         float dSq = norm(pms);
         dSq = dSq * dSq;
         f3 LC = ld3(L.inten) * ((L.size * L.size) * (cosTheta / dSq));
-        c = phong_or_brdf(LC, wo, normalized(smp - ret.point), ret, m);
+        c = phong_or_brdf<FULL>(LC, wo, normalized(smp - ret.point), ret, m);
         break;
     }
-    case RTG_LIGHT_ENVIRONMENT: {                               // :766-798
+    case RTG_LIGHT_ENVIRONMENT: if constexpr (FULL) {          // :766-798
         f3 n = ret.normal;
         f3 u = ortho_u(n);
         f3 w = cross(n, u);
@@ -783,7 +788,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         }
         dir = direction;
         mode = 2.0f;
-        c = phong_or_brdf(env_radiance(sv, L, direction), wo, direction, ret, m);
+        c = phong_or_brdf<FULL>(env_radiance(sv, L, direction), wo, direction, ret, m);
         break;
     }
     }
@@ -951,6 +956,7 @@ DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialD
     rd = wr;
 }
 
+template <bool FULL>
 __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraDev cam, int level, int s0,
                                                int row_offset, int row_stride, int npix, uint64_t seed,
                                                const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
@@ -984,11 +990,12 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
         if (h.obj < 0) {
             if (level == 0) {
                 // SingleSample passes (row=x, col=y) (Scene.cpp:496-511); MultiSample (row=y, col=x)
-                f3 bg = (cam.total > 1) ? background(sv, cam, y, x, d) : background(sv, cam, x, y, d);
+                f3 bg = !FULL ? ld3(sv.background)
+                      : (cam.total > 1) ? background(sv, cam, y, x, d) : background(sv, cam, x, y, d);
                 nd.cr = bg.x; nd.cg = bg.y; nd.cb = bg.z;
             }
         } else {
-            Ret ret = hit_record(sv, o, d, time, h);
+            Ret ret = hit_record<FULL>(sv, o, d, time, h);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading :361-372
@@ -1057,7 +1064,7 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
                     f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
                     for (int li = 0; li < sv.num_lights; li++)
-                        light_sample(sv, li, d, time, ret, m, seed, pixel, sample, path,
+                        light_sample<FULL>(sv, li, d, time, ret, m, seed, pixel, sample, path,
                                      shadows[(size_t)i * sv.num_lights + li]);
                 }
             }
@@ -1261,8 +1268,12 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, int s0, 
     if (n <= 0) return;
     int rows_owned = (cam.ny - row_offset + row_stride - 1) / row_stride;
     int npix = rows_owned * cam.nx;
-    hipLaunchKernelGGL(k_shade, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, s0, row_offset, row_stride,
-                       npix, seed, rays, meta, hits, nodes, shadows, next_rays, next_meta, next_count, n);
+    if (sv.full)
+        hipLaunchKernelGGL(k_shade<true>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, s0, row_offset,
+                           row_stride, npix, seed, rays, meta, hits, nodes, shadows, next_rays, next_meta, next_count, n);
+    else
+        hipLaunchKernelGGL(k_shade<false>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, s0, row_offset,
+                           row_stride, npix, seed, rays, meta, hits, nodes, shadows, next_rays, next_meta, next_count, n);
 }
 void launch_shadow(const SceneView& sv, const ShadowRec* shadows, NodeRec* nodes, int n, int exhaustive,
                    Counters* ctr, unsigned* traced, hipStream_t st) {

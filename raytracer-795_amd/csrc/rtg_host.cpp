@@ -712,6 +712,11 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     memcpy(sv.ambient, d->ambient_light, 12);
     sv.bg_texture = d->background_texture;
     sv.env_light = d->environment_light;
+    // The simple shading variant compiles out texturing, BRDFs and area/environment lights.
+    sv.full = d->num_textures > 0 || d->background_texture != -1 || d->environment_light != -1;
+    for (int i = 0; i < d->num_materials; i++) sv.full |= d->materials[i].brdf != RTG_BRDF_NONE;
+    for (int i = 0; i < d->num_lights; i++)
+        sv.full |= d->lights[i].type == RTG_LIGHT_AREA || d->lights[i].type == RTG_LIGHT_ENVIRONMENT;
     return RTG_OK;
 }
 

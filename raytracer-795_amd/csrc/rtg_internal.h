@@ -111,6 +111,7 @@ struct SceneView {
     float shadow_eps, int_eps;
     float background[3], ambient[3];
     int bg_texture, env_light;
+    int full;                      // 0: no textures / BRDFs / area or environment lights
 };
 
 struct CameraDev {
