@@ -222,6 +222,10 @@ typedef struct rtg_render_stats {
     double shadow_ms;        /* collect_timing: summed device time of shadow launches */
     int32_t trace_launches;
     int32_t shadow_launches;
+    uint64_t trace_steps;          /* collect_stats: BVH node steps (loop iterations) of closest-hit rays */
+    uint64_t shadow_steps;
+    uint64_t trace_lane_slots;     /* collect_stats: sum over waves of 64 x the wave's longest walk */
+    uint64_t shadow_lane_slots;    /*   (SIMD efficiency = trace_steps / trace_lane_slots) */
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */

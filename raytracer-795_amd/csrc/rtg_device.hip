@@ -17,6 +17,12 @@
 namespace rtg {
 
 #define DEV __device__ __forceinline__
+#ifndef RTG_BVH4
+#define RTG_BVH4 1       // 1: 4-wide collapsed BVH walk (BVH2 walk as overflow fallback); 0: BVH2 only
+#endif
+#ifndef RTG_TRACE_ATTR
+#define RTG_TRACE_ATTR   // occupancy experiments: -DRTG_TRACE_ATTR='__attribute__((amdgpu_waves_per_eu(5)))'
+#endif
 constexpr double PI_D = 3.14159265358979323846;
 
 // ------------------------------------------------------------------ vectors (Eigen order)
@@ -110,6 +116,11 @@ DEV bool box_test(f3 o, f3 d, float mnx, float mny, float mnz, float mxx, float 
     float le = max3(txe, tye, tze);
     return !(sl < le);
 }
+// Out-of-line copy for the rare fallbacks inside the traversal loops (keeps the hot loop small).
+__device__ __attribute__((noinline)) bool box_test_slow(f3 o, f3 d, float mnx, float mny, float mnz, float mxx,
+                                                        float mxy, float mxz) {
+    return box_test(o, d, mnx, mny, mnz, mxx, mxy, mxz);
+}
 // Same predicate, decided with reciprocal multiplies when that is provably safe.
 // q = fl(fl(b-o) * fl(1/d)) is within 3 ulp of the exact t = fl(fl(b-o)/d), so the min3/max3
 // of either set differ by < 2^-21 (|sl|+|le|); outside that band the fast answer equals the
@@ -163,9 +174,28 @@ DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps) {
     f3 amo = a - o;
     Cand c;
     float det = det3(amb, amc, d);
-    c.beta = det3(amo, amc, d) / det;
-    c.gamma = det3(amb, amo, d) / det;
-    c.t = det3(amb, amc, amo) / det;
+    float nb = det3(amo, amc, d), ng = det3(amb, amo, d), nt = det3(amb, amc, amo);
+    // Fast rejection: quotients formed with v_rcp_f32 (1 ulp) lie within 2^-21 (relative) of
+    // the correctly rounded ones, so a quotient that misses the acceptance bounds by more than
+    // 2^-20 of its magnitude is rejected by the exact test too.  Everything else (and any
+    // det outside [1e-30, 1e30] or non-finite operand, whose comparisons come out false)
+    // takes the exact divisions below.
+    const float ad = fabsf(det);
+    if (ad >= 1e-30f && ad <= 1e30f) {
+        const float r = __builtin_amdgcn_rcpf(det);
+        const float bq = nb * r, gq = ng * r, tq = nt * r;
+        const float m = 9.5367431640625e-7f;   // 2^-20
+        if (tq < (-eps - fabsf(tq) * m) - 1e-37f || bq < (-eps - fabsf(bq) * m) - 1e-37f ||
+            gq < (-eps - fabsf(gq) * m) - 1e-37f || bq + gq > (1.0f + (fabsf(bq) + fabsf(gq)) * (2.0f * m)) + m) {
+            c.ok = false;
+            c.beta = c.gamma = c.t = 0.0f;
+            c.p = o;
+            return c;
+        }
+    }
+    c.beta = nb / det;
+    c.gamma = ng / det;
+    c.t = nt / det;
     c.ok = (c.t >= -eps && (c.beta + c.gamma <= 1) && c.beta >= -eps && c.gamma >= -eps);
     c.p = o + d * c.t;
     return c;
@@ -196,6 +226,14 @@ DEV float gett(f3 o, f3 d, f3 p) {
 }
 // Transforming::TransformRay (src/Helper.cpp:164-187)
 DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d2) {
+    if (T.ident && __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z) &&
+        __builtin_isfinite(d.x) && __builtin_isfinite(d.y) && __builtin_isfinite(d.z) && __builtin_isfinite(time)) {
+        // identity inverse, +0 blur: (x*1 + y*0) + (z*0 + w*0) == x + 0 for finite inputs
+        // (the only effect is -0 -> +0)
+        o2 = mk(o.x + 0.0f, o.y + 0.0f, o.z + 0.0f);
+        d2 = mk(d.x + 0.0f, d.y + 0.0f, d.z + 0.0f);
+        return;
+    }
     f3 b = mk(T.blur[0] * time, T.blur[1] * time, T.blur[2] * time);
     f3 oo = o;
     oo.x -= b.x; oo.y -= b.y; oo.z -= b.z;
@@ -203,7 +241,7 @@ DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d
     d2 = xform(T.inv, d, 0.0f);
 }
 
-struct Stats { unsigned nodes, tris; };
+struct Stats { unsigned nodes, tris, steps; };
 
 // ------------------------------------------------------------------ closest hit
 // BVHMethods::FindIntersection (src/Helper.cpp:72-134) with the per-object nearest
@@ -253,30 +291,33 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
             const float pad = g.prune_pad;
             float best_d = FLT_MAX;
             int best_leaf = -1;
-            const f3 inv = mk(1.0f / d2.x, 1.0f / d2.y, 1.0f / d2.z);
-            const bool fast = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z);
+            // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
+            // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
+            // send every box to the exact division test instead.
+            const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
+            const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
+                              adz <= 1e30f;
+            const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
             // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
             // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
             // skipped when its box, expanded by `pad`, meets the line only outside that window.
-            const float padt = fast ? pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z)) : 0.0f;
+            const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
             const float tlo = -(fabsf(eps) + 1e-6f);
             const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
             const float inv_dn = 1.0f / dnorm;
             float thi = INFINITY;
             if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
             const float tm_global = thi;
-            auto leaf = [&](int start, int count) {
-                for (int k = start; k < start + count; k++) {
-                    const TriGeom tg = sv.tris[k];
-                    if (STATS) st.tris++;
-                    Cand c = tri_test(tg, o2, d2, eps);
-                    if (c.ok) {
-                        float dist = norm(c.p - o2);
-                        if (dist < FLT_MAX &&
-                            (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
-                            best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
-                            if (!EXHAUSTIVE) thi = fminf(tm_global, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                        }
+            // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
+            auto test_prim = [&](const TriGeom& tg, int k, int start) {
+                if (STATS) st.tris++;
+                Cand c = tri_test(tg, o2, d2, eps);
+                if (c.ok) {
+                    float dist = norm(c.p - o2);
+                    if (dist < FLT_MAX &&
+                        (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
+                        best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                        if (!EXHAUSTIVE) thi = fminf(tm_global, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                     }
                 }
             };
@@ -303,51 +344,208 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
             };
             if (g.node_base < 0) {
-                if (g.root_leaf_count > 0) leaf(g.root_leaf_start, g.root_leaf_count);
+                for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
+                    test_prim(sv.tris[k], k, g.root_leaf_start);
             } else if (box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
                                g.root_max[1], g.root_max[2])) {
-                int sp = 0;
-                int cur = g.node_base;
-                while (true) {
-                    if (STATS) st.nodes += 2;   // one 64-B node = two 32-B child records
-                    const Node nd = sv.nodes[cur];
-                    const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
-                    float lk = 0.0f, rk = 0.0f;
-                    bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
-                    bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
-                    // leaf children are resolved immediately, nearer first
-                    bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
-                    if (lleaf && rleaf && rk < lk) {
-                        leaf(rref, rcnt);
-                        if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
-                        lok = rok = false;
-                    } else {
-                        if (lleaf) { leaf(lref, lcnt); lok = false; }
-                        if (rleaf) {
-                            if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
-                            rok = false;
+                // Leaf children are resolved as soon as they are reached.
+                auto leaf = [&](int start, int count) {
+                    for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
+                };
+                // BVH2 walk (ordered, pruned): the reference tree node by node.
+                auto walk2 = [&]() {
+                    int sp = 0;
+                    int cur = g.node_base;
+                    while (true) {
+                        if (STATS) { st.nodes += 2; st.steps++; }   // one 64-B node = two 32-B child records
+                        const Node nd = sv.nodes[cur];
+                        const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
+                        float lk = 0.0f, rk = 0.0f;
+                        bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
+                        bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
+                        bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
+                        if (lleaf && rleaf && rk < lk) {
+                            leaf(rref, rcnt);
+                            if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
+                            lok = rok = false;
+                        } else {
+                            if (lleaf) { leaf(lref, lcnt); lok = false; }
+                            if (rleaf) {
+                                if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
+                                rok = false;
+                            }
+                        }
+                        if (!EXHAUSTIVE) {
+                            lok = lok && !(lk > thi);
+                            rok = rok && !(rk > thi);
+                        }
+                        if (lok && rok) {
+                            int nearc = lref, farc = rref;
+                            if (rk < lk) { nearc = rref; farc = lref; }
+                            stack[sp * sstride] = farc;
+                            sp++;
+                            cur = nearc;
+                        } else if (lok) {
+                            cur = lref;
+                        } else if (rok) {
+                            cur = rref;
+                        } else {
+                            if (sp == 0) break;
+                            sp--;
+                            cur = stack[sp * sstride];
                         }
                     }
-                    if (!EXHAUSTIVE) {
-                        lok = lok && !(lk > thi);
-                        rok = rok && !(rk > thi);
-                    }
-                    if (lok && rok) {
-                        int nearc = lref, farc = rref;
-                        if (rk < lk) { nearc = rref; farc = lref; }
-                        stack[sp * sstride] = farc;
-                        sp++;
-                        cur = nearc;
-                    } else if (lok) {
-                        cur = lref;
-                    } else if (rok) {
-                        cur = rref;
-                    } else {
-                        if (sp == 0) break;
-                        sp--;
-                        cur = stack[sp * sstride];
+                };
+#if RTG_BVH4
+                // 4-wide walk over the collapsed tree.  Slots of a collapsed child c need c's box
+                // hit too.  On the fast path the exact slab predicate is monotone under box
+                // containment (no zero direction component), so a slot whose own box -- or whose
+                // pair sibling's box -- is certainly hit implies c's hit; interior slots are
+                // themselves box-tested; only a leaf slot without such a witness tests the pair
+                // union (= c's range box) explicitly.  The exact / exhaustive paths test the union
+                // for every gated slot.  A stack that would overflow (> kStackDepth entries: up to
+                // 3 pushes per level) restarts the object on the BVH2 walk, whose depth bound
+                // fits; candidates already found stay valid.
+                bool overflow = false;
+                {
+                    int sp = 0;
+                    int cur = g.node4_base;
+                    while (true) {
+                        if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
+                        const Node4 nd = sv.nodes4[cur];
+                        const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
+                        const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
+                        const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
+                        const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
+                        const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
+                        const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
+                        const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
+                        const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
+                        float key[4];
+                        bool ok[4], sure[4];
+                        int gate_mask = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const int cnt = inf[j] & kSlotCount;
+                            const bool interior = cnt == 0;
+                            key[j] = 0.0f;
+                            sure[j] = false;
+                            ok[j] = false;
+                            if (inf[j] < 0) continue;
+                            if (!EXHAUSTIVE && fast) {
+                                const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
+                                const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
+                                const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
+                                const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                                const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                                const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                                const float lo = le - e - padt, hi = sl + e + padt;
+                                key[j] = lo;
+                                sure[j] = sl >= le + e;
+                                const bool win = !(hi < lo || hi < tlo || lo > thi);
+                                const bool miss = sl < le - e;
+                                ok[j] = win && !(interior && miss);
+                                // interior slot in the uncertain band: exact predicate
+                                if (ok[j] && interior && !sure[j]) gate_mask |= 1 << j;
+                            } else {
+                                ok[j] = true;
+                                if (interior) gate_mask |= 1 << j;
+                            }
+                        }
+                        // own exact tests of uncertain interior slots (rare on the fast path)
+                        while (gate_mask) {
+                            const int j = __builtin_ctz(gate_mask);
+                            gate_mask &= gate_mask - 1;
+                            const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
+                            const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
+                            const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
+                            const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
+                            const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
+                            const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
+                            const bool hit = box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2);
+                            if (!hit) {
+                                if (j == 0) ok[0] = false; else if (j == 1) ok[1] = false;
+                                else if (j == 2) ok[2] = false; else ok[3] = false;
+                            } else {
+                                if (j == 0) sure[0] = true; else if (j == 1) sure[1] = true;
+                                else if (j == 2) sure[2] = true; else sure[3] = true;
+                            }
+                        }
+                        // collapsed-child gates (pair union box), once per pair
+#pragma unroll
+                        for (int p = 0; p < 4; p += 2) {
+                            const int g0 = inf[p], g1 = inf[p + 1];
+                            const bool gated = ((g0 >= 0 && (g0 & kSlotGate)) || (g1 >= 0 && (g1 & kSlotGate)));
+                            if (!gated) continue;
+                            bool need;
+                            if (!EXHAUSTIVE && fast)
+                                need = ((ok[p] && (g0 & kSlotCount) > 0) || (ok[p + 1] && (g1 & kSlotCount) > 0)) &&
+                                       !sure[p] && !sure[p + 1];
+                            else
+                                need = ok[p] || ok[p + 1];
+                            if (need) {
+                                const bool b0 = g0 >= 0, b1 = g1 >= 0;
+                                const float ux = b0 && b1 ? fminf(lx[p], lx[p + 1]) : (b0 ? lx[p] : lx[p + 1]);
+                                const float uy = b0 && b1 ? fminf(ly[p], ly[p + 1]) : (b0 ? ly[p] : ly[p + 1]);
+                                const float uz = b0 && b1 ? fminf(lz[p], lz[p + 1]) : (b0 ? lz[p] : lz[p + 1]);
+                                const float vx = b0 && b1 ? fmaxf(hx[p], hx[p + 1]) : (b0 ? hx[p] : hx[p + 1]);
+                                const float vy = b0 && b1 ? fmaxf(hy[p], hy[p + 1]) : (b0 ? hy[p] : hy[p + 1]);
+                                const float vz = b0 && b1 ? fmaxf(hz[p], hz[p + 1]) : (b0 ? hz[p] : hz[p + 1]);
+                                if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) ok[p] = ok[p + 1] = false;
+                            }
+                        }
+                        // interior candidates first, so the node's boxes are dead during leaf tests
+                        float k4[4];
+                        int r4[4];
+                        int leaf_mask = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const bool isleaf = (inf[j] & kSlotCount) > 0;
+                            const bool take = ok[j] && !isleaf;
+                            k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
+                            r4[j] = take ? rf[j] : -1;
+                            if (ok[j] && isleaf && (EXHAUSTIVE || !(key[j] > thi))) leaf_mask |= 1 << j;
+                        }
+                        // leaves now, one code site (thi may shrink between them)
+                        while (leaf_mask) {
+                            const int j = __builtin_ctz(leaf_mask);
+                            leaf_mask &= leaf_mask - 1;
+                            const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
+                            const int info = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
+                            leaf(start, info & kSlotCount);
+                        }
+                        if (!EXHAUSTIVE) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++)
+                                if (k4[j] > thi) { k4[j] = INFINITY; r4[j] = -1; }
+                        }
+                        // interior slots, nearest first: sort (key, ref), push the others farthest first
+                        auto ce = [&](int a, int b) {
+                            const bool sw = k4[b] < k4[a];
+                            const float ka = k4[a], kb = k4[b];
+                            const int ra = r4[a], rb = r4[b];
+                            k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
+                            r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
+                        };
+                        ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+                        const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
+                        if (sp + npush > kStackDepth) { overflow = true; break; }
+                        if (r4[3] >= 0) { stack[sp * sstride] = r4[3]; sp++; }
+                        if (r4[2] >= 0) { stack[sp * sstride] = r4[2]; sp++; }
+                        if (r4[1] >= 0) { stack[sp * sstride] = r4[1]; sp++; }
+                        if (r4[0] >= 0) {
+                            cur = r4[0];
+                        } else {
+                            if (sp == 0) break;
+                            sp--;
+                            cur = stack[sp * sstride];
+                        }
                     }
                 }
+                if (overflow) walk2();
+#else
+                walk2();
+#endif
             }
         }
         if (found) {
@@ -806,14 +1004,27 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
 }
 
 // ------------------------------------------------------------------ camera / background
-DEV void slot_pixel(const CameraDev& cam, int slot, int s0, int row_offset, int row_stride, int npix, uint32_t& pixel,
-                    uint32_t& sample, int& x, int& y) {
-    int sl = slot / npix, pl = slot - sl * npix;
-    int k = pl / cam.nx;
-    x = pl - k * cam.nx;
-    y = row_offset + k * row_stride;
+// Tiled order of the owned pixels: bands of 8 owned rows, each band in blocks of 8 columns
+// (edge bands/blocks narrower), row-major inside a block.  t -> (x, k = owned-row index).
+DEV void tile_pixel(int t, int nx, int rows_owned, int& x, int& k) {
+    const int band = t / (8 * nx);
+    const int u = t - band * 8 * nx;
+    const int hb = min(8, rows_owned - 8 * band);
+    const int c = u / (8 * hb);
+    const int u2 = u - c * 8 * hb;
+    const int wb = min(8, nx - 8 * c);
+    const int r = u2 / wb;
+    x = 8 * c + (u2 - r * wb);
+    k = 8 * band + r;
+}
+DEV void slot_pixel(const CameraDev& cam, const PassDev& ps, int slot, uint32_t& pixel, uint32_t& sample, int& x,
+                    int& y) {
+    const int pl = slot / ps.ns, sl = slot - pl * ps.ns;
+    int k;
+    tile_pixel(ps.p0 + pl, cam.nx, ps.rows_owned, x, k);
+    y = ps.row_offset + k * ps.row_stride;
     pixel = (uint32_t)(y * cam.nx + x);
-    sample = (uint32_t)(s0 + sl);
+    sample = (uint32_t)(ps.s0 + sl);
 }
 DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f3 dir) {   // Scene.cpp:544-566
     if (sv.env_light != -1) {
@@ -832,14 +1043,14 @@ DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, int s0, int row_offset, int row_stride, int npix,
-                                                uint64_t seed, RayRec* __restrict__ rays, RayMeta* __restrict__ meta,
-                                                int n, int max_depth) {
+__global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassDev ps, uint64_t seed,
+                                                RayRec* __restrict__ rays, RayMeta* __restrict__ meta, int n,
+                                                int max_depth) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t pixel, sample;
     int x, y;
-    slot_pixel(cam, i, s0, row_offset, row_stride, npix, pixel, sample, x, y);
+    slot_pixel(cam, ps, i, pixel, sample, x, y);
     f3 pos = ld3(cam.pos), gaze = ld3(cam.gaze), right = ld3(cam.right), up = ld3(cam.up);
     f3 o = pos, d;
     float time = 0.0f;
@@ -891,11 +1102,11 @@ __global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, int s0, int
 }
 
 template <bool EXHAUSTIVE, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayRec* __restrict__ rays,
+__global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayRec* __restrict__ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Stats st = {0, 0};
+    Stats st = {0, 0, 0};
     if (i < n) {
         RayRec r = rays[i];
         HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, mk(r.o_t.x, r.o_t.y, r.o_t.z), mk(r.d.x, r.d.y, r.d.z), r.o_t.w,
@@ -903,14 +1114,19 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
         hits[i] = h;
     }
     if (STATS) {
-        unsigned long long nv = st.nodes, nt = st.tris;
+        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
+        unsigned mx = st.steps;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
+            ns += __shfl_down(ns, off);
+            mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
         }
         if ((threadIdx.x & 63) == 0) {
             atomicAdd(&ctr->node_visits, nv);
             atomicAdd(&ctr->tri_tests, nt);
+            atomicAdd(&ctr->trace_lane_slots, 64ull * mx);
+            atomicAdd(&ctr->trace_steps, ns);
         }
     }
 }
@@ -957,11 +1173,12 @@ DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialD
 }
 
 template <bool FULL>
-__global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraDev cam, int level, int s0,
-                                               int row_offset, int row_stride, int npix, uint64_t seed,
+__global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+                                               uint64_t seed,
                                                const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
                                                const HitRec* __restrict__ hits, NodeRec* __restrict__ nodes,
-                                               ShadowRec* __restrict__ shadows, RayRec* __restrict__ next_rays,
+                                               ShadowRec* __restrict__ shadows, int* __restrict__ slist,
+                                               unsigned* scount, RayRec* __restrict__ next_rays,
                                                RayMeta* __restrict__ next_meta, unsigned* next_count, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     int nchild = 0;
@@ -969,6 +1186,7 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
     RayMeta c0m, c1m;
     bool has0 = false, has1 = false;
     NodeRec nd;
+    unsigned long long smask = 0;   // lights whose shadow query must be traced
     if (i < n) {
         RayRec r = rays[i];
         RayMeta mt = meta[i];
@@ -977,7 +1195,7 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
         float time = r.o_t.w;
         uint32_t pixel, sample;
         int x, y;
-        slot_pixel(cam, mt.slot, s0, row_offset, row_stride, npix, pixel, sample, x, y);
+        slot_pixel(cam, ps, mt.slot, pixel, sample, x, y);
         uint64_t path = ((uint64_t)mt.path_hi << 32) | mt.path_lo;
         nd.px = nd.py = nd.pz = 0.0f;
         nd.cr = nd.cg = nd.cb = 0.0f;
@@ -1060,12 +1278,17 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
                     }
                 }
                 if (basic) {
-                    // Scene::ambient :153-161 (0 + La*ka), lights added by k_shadow in order
+                    // Scene::ambient :153-161 (0 + La*ka); the lights are added in order by
+                    // k_shadow (one light) or k_light_sum (several)
                     f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
-                    for (int li = 0; li < sv.num_lights; li++)
-                        light_sample<FULL>(sv, li, d, time, ret, m, seed, pixel, sample, path,
-                                     shadows[(size_t)i * sv.num_lights + li]);
+                    for (int li = 0; li < sv.num_lights; li++) {
+                        ShadowRec sr;
+                        light_sample<FULL>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
+                        shadows[(size_t)i * sv.num_lights + li] = sr;
+                        if (sr.c.w != 0.0f) smask |= 1ull << li;
+                        else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
+                    }
                 }
             }
         }
@@ -1079,62 +1302,93 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
         if (has1) { next_rays[idx] = c1r; next_meta[idx] = c1m; nd.child1 = idx; }
         nodes[i] = nd;
     }
+    // compacted shadow-query list (entries i * nLights + li)
+    for (int li = 0; li < sv.num_lights; li++) {
+        const bool need = (smask >> li) & 1ull;
+        const int q = wave_append(need ? 1 : 0, scount);
+        if (need) slist[q] = i * sv.num_lights + li;
+    }
 }
 
 // Shadow queries + in-order light sum of Scene::BasicShading (src/Scene.cpp:374-398).
+// One thread per traced shadow query (compacted by k_shade).  With one light the result is
+// added to the node colour here (col + c or col + 0, as Scene::RecursiveShading's light loop
+// does); with several, the visibility is recorded and k_light_sum adds them in light order.
 template <bool EXHAUSTIVE, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock) k_shadow(const SceneView sv, const ShadowRec* __restrict__ shadows,
-                                                        NodeRec* __restrict__ nodes, int n, unsigned* traced,
-                                                        Counters* ctr) {
+__global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_shadow(const SceneView sv,
+                                                                       ShadowRec* __restrict__ shadows,
+                                                                       const int* __restrict__ slist,
+                                                                       const unsigned* scount,
+                                                                       NodeRec* __restrict__ nodes,
+                                                                       unsigned* traced, Counters* ctr) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned cnt = 0;
-    Stats st = {0, 0};
-    if (i < n) {
-        NodeRec nd = nodes[i];
-        if (nd.kind & 0x100) {
-            f3 col = mk(nd.cr, nd.cg, nd.cb);
-            f3 p = mk(nd.px, nd.py, nd.pz);
-            for (int li = 0; li < sv.num_lights; li++) {
-                const ShadowRec sr = shadows[(size_t)i * sv.num_lights + li];
-                f3 add = mk(0, 0, 0);
-                if (sr.c.w != 0.0f) {
-                    f3 o = mk(sr.o.x, sr.o.y, sr.o.z), d = mk(sr.d.x, sr.d.y, sr.d.z);
-                    if (!(isnan3(o) || isnan3(d))) cnt++;
-                    HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
-                                                              s_stack + threadIdx.x, kTraceBlock, st);
-                    bool blocked;
-                    if (sr.c.w == 1.0f) {
-                        blocked = false;
-                        if (h.obj >= 0) {
-                            f3 hp = o + d * h.t;
-                            blocked = norm(p - mk(sr.L.x, sr.L.y, sr.L.z)) > norm(p - hp);
-                        }
-                    } else {
-                        blocked = h.obj >= 0;
-                    }
-                    if (!blocked) add = mk(sr.c.x, sr.c.y, sr.c.z);
-                }
-                col = col + add;
+    Stats st = {0, 0, 0};
+    if (j < (int)*scount) {
+        const int idx = slist[j];
+        const ShadowRec sr = shadows[idx];
+        const f3 o = mk(sr.o.x, sr.o.y, sr.o.z), d = mk(sr.d.x, sr.d.y, sr.d.z);
+        if (!(isnan3(o) || isnan3(d))) cnt++;
+        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
+                                                  s_stack + threadIdx.x, kTraceBlock, st);
+        const int i = idx / sv.num_lights;
+        bool blocked;
+        if (sr.c.w == 1.0f) {
+            blocked = false;
+            if (h.obj >= 0) {
+                const NodeRec& nr = nodes[i];
+                f3 p = mk(nr.px, nr.py, nr.pz);
+                f3 hp = o + d * h.t;
+                blocked = norm(p - mk(sr.L.x, sr.L.y, sr.L.z)) > norm(p - hp);
             }
-            nd.cr = col.x; nd.cg = col.y; nd.cb = col.z;
-            nodes[i].cr = nd.cr; nodes[i].cg = nd.cg; nodes[i].cb = nd.cb;
+        } else {
+            blocked = h.obj >= 0;
+        }
+        if (sv.num_lights == 1) {
+            f3 add = blocked ? mk(0, 0, 0) : mk(sr.c.x, sr.c.y, sr.c.z);
+            nodes[i].cr = nodes[i].cr + add.x;
+            nodes[i].cg = nodes[i].cg + add.y;
+            nodes[i].cb = nodes[i].cb + add.z;
+        } else {
+            shadows[idx].L.w = blocked ? 0.0f : 1.0f;
         }
     }
     // per-wave reduction of the traced-ray count
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
     if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(traced, cnt);
     if (STATS) {
-        unsigned long long nv = st.nodes, nt = st.tris;
+        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
+        unsigned mx = st.steps;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
+            ns += __shfl_down(ns, off);
+            mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
         }
         if ((threadIdx.x & 63) == 0) {
             atomicAdd(&ctr->shadow_node_visits, nv);
             atomicAdd(&ctr->shadow_tri_tests, nt);
+            atomicAdd(&ctr->shadow_lane_slots, 64ull * mx);
+            atomicAdd(&ctr->shadow_steps, ns);
         }
     }
+}
+
+// Several lights: Scene::RecursiveShading's in-order sum col = ((amb + L0) + L1) + ...
+__global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const ShadowRec* __restrict__ shadows,
+                                                   NodeRec* __restrict__ nodes, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NodeRec nd = nodes[i];
+    if (!(nd.kind & 0x100)) return;
+    f3 col = mk(nd.cr, nd.cg, nd.cb);
+    for (int li = 0; li < sv.num_lights; li++) {
+        const ShadowRec sr = shadows[(size_t)i * sv.num_lights + li];
+        const bool lit = sr.c.w != 0.0f && sr.L.w == 1.0f;
+        col = col + (lit ? mk(sr.c.x, sr.c.y, sr.c.z) : mk(0, 0, 0));
+    }
+    nodes[i].cr = col.x; nodes[i].cg = col.y; nodes[i].cb = col.z;
 }
 
 DEV f3 nan_check(f3 c) { return isnan3(c) ? mk(0, 0, 0) : c; }   // Scene::NanCheck :352-359
@@ -1183,13 +1437,16 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __
 
 // Scene::MultiSample sum order: color += sample_i in sample order (src/Scene.cpp:519-540).
 __global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ level0, float* __restrict__ acc,
-                                                    int npix, int ns, int mode) {
-    int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= npix) return;
+                                                    const PassDev ps, int nx, int mode) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ps.npass) return;
+    int x, k;
+    tile_pixel(ps.p0 + j, nx, ps.rows_owned, x, k);
+    const size_t p = (size_t)k * nx + x;        // acc is in natural owned-row order
     f3 a;
     int s = 0;
     if (mode == 2) {            // SingleSample: the colour itself
-        const NodeRec& r = level0[p];
+        const NodeRec& r = level0[(size_t)j * ps.ns];
         a = mk(r.cr, r.cg, r.cb);
         s = 1;
     } else if (mode == 1) {     // MultiSample: Vector3f color = {0,0,0}; color += ...
@@ -1197,8 +1454,8 @@ __global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ 
     } else {
         a = mk(acc[3 * p], acc[3 * p + 1], acc[3 * p + 2]);
     }
-    for (; s < ns; s++) {
-        const NodeRec& r = level0[(size_t)s * npix + p];
+    for (; s < ps.ns; s++) {
+        const NodeRec& r = level0[(size_t)j * ps.ns + s];
         a = a + mk(r.cr, r.cg, r.cb);
     }
     acc[3 * p] = a.x; acc[3 * p + 1] = a.y; acc[3 * p + 2] = a.z;
@@ -1245,13 +1502,10 @@ __global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const R
 // ------------------------------------------------------------------ launchers
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 
-void launch_raygen(const SceneView& sv, const CameraDev& cam, int s0, int ns, int row_offset, int row_stride,
-                   int rows_owned, uint64_t seed, RayRec* rays, RayMeta* meta, int n, hipStream_t st) {
-    (void)ns;
+void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps, uint64_t seed, RayRec* rays,
+                   RayMeta* meta, int n, hipStream_t st) {
     if (n <= 0) return;
-    int npix = rows_owned * cam.nx;
-    hipLaunchKernelGGL(k_raygen, dim3(nblk(n, 256)), dim3(256), 0, st, cam, s0, row_offset, row_stride, npix, seed,
-                       rays, meta, n, sv.max_depth);
+    hipLaunchKernelGGL(k_raygen, dim3(nblk(n, 256)), dim3(256), 0, st, cam, ps, seed, rays, meta, n, sv.max_depth);
 }
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
                   hipStream_t st) {
@@ -1261,35 +1515,38 @@ void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, 
     else if (ctr) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, st, sv, rays, hits, n, ctr);
     else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, st, sv, rays, hits, n, ctr);
 }
-void launch_shade(const SceneView& sv, const CameraDev& cam, int level, int s0, int row_offset, int row_stride,
-                  uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
-                  ShadowRec* shadows, RayRec* next_rays, RayMeta* next_meta, unsigned* next_count, int n,
-                  hipStream_t st) {
+void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
+                  const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
+                  ShadowRec* shadows, int* slist, unsigned* scount, RayRec* next_rays, RayMeta* next_meta,
+                  unsigned* next_count, int n, hipStream_t st) {
     if (n <= 0) return;
-    int rows_owned = (cam.ny - row_offset + row_stride - 1) / row_stride;
-    int npix = rows_owned * cam.nx;
     if (sv.full)
-        hipLaunchKernelGGL(k_shade<true>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, s0, row_offset,
-                           row_stride, npix, seed, rays, meta, hits, nodes, shadows, next_rays, next_meta, next_count, n);
+        hipLaunchKernelGGL(k_shade<true>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta,
+                           hits, nodes, shadows, slist, scount, next_rays, next_meta,
+                           next_count, n);
     else
-        hipLaunchKernelGGL(k_shade<false>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, s0, row_offset,
-                           row_stride, npix, seed, rays, meta, hits, nodes, shadows, next_rays, next_meta, next_count, n);
+        hipLaunchKernelGGL(k_shade<false>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta,
+                           hits, nodes, shadows, slist, scount, next_rays, next_meta,
+                           next_count, n);
 }
-void launch_shadow(const SceneView& sv, const ShadowRec* shadows, NodeRec* nodes, int n, int exhaustive,
-                   Counters* ctr, unsigned* traced, hipStream_t st) {
+void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
+                   int n, int exhaustive, Counters* ctr, unsigned* traced, hipStream_t st) {
     if (n <= 0 || sv.num_lights == 0) return;
-    dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, nodes, n, traced, ctr);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, nodes, n, traced, ctr);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, nodes, n, traced, ctr);
+    const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
+    dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, traced, ctr);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, slist, scount, nodes, traced, ctr);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, traced, ctr);
+    if (sv.num_lights > 1)
+        hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, shadows, nodes, n);
 }
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, nodes, child_nodes, n);
 }
-void launch_accumulate(const NodeRec* level0, float* acc, int npix, int ns, int mode, hipStream_t st) {
-    if (npix <= 0) return;
-    hipLaunchKernelGGL(k_accumulate, dim3(nblk(npix, 256)), dim3(256), 0, st, level0, acc, npix, ns, mode);
+void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st) {
+    if (ps.npass <= 0) return;
+    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, 256)), dim3(256), 0, st, level0, acc, ps, nx, mode);
 }
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int total,
                      hipStream_t st) {

@@ -282,6 +282,56 @@ int construct(BuildCtx& B, int start, int end, int splitType, int depth) {
     return n;
 }
 
+// Collapse the BVH2 below interior node n into 4-wide nodes (pre-order, returns the index).
+int build_node4(const std::vector<HNode>& hn, int n, int prim_base, std::vector<Node4>& out) {
+    int me = (int)out.size();
+    out.emplace_back();
+    float lo[3][4], hi[3][4];
+    int ref[4], info[4];
+    int pending[4] = {-1, -1, -1, -1};    // interior grandchildren to build after this node
+    auto set_slot = [&](int j, int c, bool gated) {
+        if (c < 0) {
+            for (int z = 0; z < 3; z++) { lo[z][j] = 0.0f; hi[z][j] = 0.0f; }
+            ref[j] = 0; info[j] = -1;
+            return;
+        }
+        const HNode& h = hn[c];
+        for (int z = 0; z < 3; z++) { lo[z][j] = h.mn[z]; hi[z][j] = h.mx[z]; }
+        if (h.left < 0 && h.right < 0) {
+            int len = h.end - h.start;
+            ref[j] = prim_base + h.start;
+            info[j] = len > 0 ? (len | (gated ? kSlotGate : 0)) : -1;
+        } else {
+            ref[j] = 0;
+            info[j] = gated ? kSlotGate : 0;
+            pending[j] = c;
+        }
+    };
+    const int ch[2] = {hn[n].left, hn[n].right};
+    for (int q = 0; q < 2; q++) {
+        int c = ch[q];
+        if (c >= 0 && (hn[c].left >= 0 || hn[c].right >= 0)) {
+            set_slot(2 * q, hn[c].left, true);
+            set_slot(2 * q + 1, hn[c].right, true);
+        } else {
+            set_slot(2 * q, c, false);
+            set_slot(2 * q + 1, -1, false);
+        }
+    }
+    for (int j = 0; j < 4; j++)
+        if (pending[j] >= 0) ref[j] = build_node4(hn, pending[j], prim_base, out);
+    Node4& nd = out[me];
+    nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+    nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+    nd.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+    nd.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+    nd.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+    nd.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    nd.ref = make_int4(ref[0], ref[1], ref[2], ref[3]);
+    nd.info = make_int4(info[0], info[1], info[2], info[3]);
+    return me;
+}
+
 // ------------------------------------------------------------------ device buffer helper
 struct DBuf {
     void* p = nullptr;
@@ -312,7 +362,7 @@ int upload(DBuf& b, const std::vector<T>& v) {
 }
 
 struct Level {
-    DBuf rays, meta, hits, nodes, shadows;
+    DBuf rays, meta, hits, nodes, shadows, slist;
 };
 
 }  // namespace
@@ -325,7 +375,7 @@ struct rtg_scene {
     std::vector<float> vnormals;
     std::vector<int> orig_prim;              // absolute BVH position -> original prim index
     SceneView sv{};
-    DBuf d_tops, d_geoms, d_nodes, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
+    DBuf d_tops, d_geoms, d_nodes, d_nodes4, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
         d_texels, d_lights, d_origprim;
     // render workspace
     std::vector<Level> levels;
@@ -406,11 +456,11 @@ static int validate(const rtg_scene_desc* d) {
 }
 
 static void scene_free(rtg_scene* s) {
-    DBuf* bufs[] = {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_tris, &s->d_primidx, &s->d_vertices, &s->d_vnormals,
+    DBuf* bufs[] = {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices, &s->d_vnormals,
                     &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights, &s->d_origprim,
                     &s->d_acc, &s->d_counters, &s->d_stats};
     for (DBuf* b : bufs) b->release();
-    for (Level& l : s->levels) { l.rays.release(); l.meta.release(); l.hits.release(); l.nodes.release(); l.shadows.release(); }
+    for (Level& l : s->levels) { l.rays.release(); l.meta.release(); l.hits.release(); l.nodes.release(); l.shadows.release(); l.slist.release(); }
 }
 
 int32_t rtg_scene_destroy(rtg_scene* s) {
@@ -476,6 +526,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     // BVHs and device geometry
     std::vector<Geometry> geoms(d->num_objects);
     std::vector<Node> dnodes;
+    std::vector<Node4> dnodes4;
     std::vector<TriGeom> tris;
     std::vector<int4> primidx;
     s->orig_prim.clear();
@@ -554,6 +605,11 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         g.prune_pad = pad;
         // linearise interior nodes (pre-order) into child-box nodes
         const std::vector<HNode>& hn = ob.nodes;
+        for (const HNode& h : hn) {            // leaf length travels with the leaf's first triangle
+            if (h.left >= 0 || h.right >= 0 || h.end <= h.start) continue;
+            int len = h.end - h.start;
+            memcpy(&tris[g.prim_base + h.start].p2.z, &len, 4);
+        }
         std::vector<int> dev_index(hn.size(), -1);
         int node_base = (int)dnodes.size();
         int cnt = 0;
@@ -587,6 +643,9 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             nd.d = make_int4(ref[0], ref[1], count[0], count[1]);
             dnodes[dev_index[k]] = nd;
         }
+        g.node4_base = -1;
+        if (ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0))
+            g.node4_base = build_node4(hn, ob.root, g.prim_base, dnodes4);
         if (ob.root < 0) {
             g.node_base = -1; g.root_leaf_start = g.prim_base; g.root_leaf_count = -1;
         } else if (hn[ob.root].left < 0 && hn[ob.root].right < 0) {
@@ -622,6 +681,19 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             T.geom = in.base_object;
             T.is_instance = 1;
         }
+        // identity fast path of transform_ray: rows 0-2 of inv exactly the identity with +0
+        // off-diagonal entries, and +0 blur
+        bool ident = true;
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 3; r++) {
+                float want = (c == r) ? 1.0f : 0.0f;
+                ident = ident && memcmp(&T.inv[c * 4 + r], &want, 4) == 0;
+            }
+        for (int k = 0; k < 3; k++) {
+            float z = 0.0f;
+            ident = ident && memcmp(&T.blur[k], &z, 4) == 0;
+        }
+        T.ident = ident ? 1 : 0;
     }
 
     // materials, textures, lights
@@ -685,6 +757,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     if (d->num_texcoords > 0) tcflat.assign(d->texcoords, d->texcoords + 2 * (size_t)d->num_texcoords);
     int rc;
     if ((rc = upload(s->d_tops, tops)) || (rc = upload(s->d_geoms, geoms)) || (rc = upload(s->d_nodes, dnodes)) ||
+        (rc = upload(s->d_nodes4, dnodes4)) ||
         (rc = upload(s->d_tris, tris)) || (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_vertices, vflat)) ||
         (rc = upload(s->d_vnormals, s->vnormals)) || (rc = upload(s->d_texcoords, tcflat)) ||
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
@@ -695,6 +768,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.tops = s->d_tops.as<TopObject>(); sv.num_tops = (int)tops.size(); sv.num_objects = d->num_objects;
     sv.geoms = s->d_geoms.as<Geometry>();
     sv.nodes = s->d_nodes.as<Node>();
+    sv.nodes4 = s->d_nodes4.as<Node4>();
     sv.tris = s->d_tris.as<TriGeom>();
     sv.prim_idx = s->d_primidx.as<int4>();
     sv.vertices = s->d_vertices.as<float>();
@@ -796,17 +870,19 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     int npix = (int)npix_ll;
     int total = cam->num_samples;
     long long max_batch = o.max_batch_rays > 0 ? o.max_batch_rays : (4LL << 20);
-    int ns_pass = npix > 0 ? (int)std::max<long long>(1, std::min<long long>(total, max_batch / std::max(npix, 1))) : 1;
+    // passes: all samples of a pixel range (chunks of samples only when spp exceeds the batch)
+    const int ns_chunk = (int)std::max<long long>(1, std::min<long long>(total, max_batch));
+    const int np_pass = (int)std::max<long long>(1, std::min<long long>(npix, max_batch / ns_chunk));
     int exhaustive = o.traversal == 1;
     const int nL = s->sv.num_lights;
 
     int rc;
     if ((rc = s->d_acc.grow(sizeof(float) * 3 * std::max<size_t>(npix, 1)))) return rc;
-    if ((rc = s->d_counters.grow(sizeof(unsigned) * 64))) return rc;
+    if ((rc = s->d_counters.grow(sizeof(unsigned) * 128))) return rc;
     if ((rc = s->d_stats.grow(sizeof(Counters)))) return rc;
     unsigned* d_cnt = s->d_counters.as<unsigned>();
     Counters* d_stats = s->d_stats.as<Counters>();
-    HIP_TRY(hipMemsetAsync(s->d_counters.p, 0, sizeof(unsigned) * 64, st));
+    HIP_TRY(hipMemsetAsync(s->d_counters.p, 0, sizeof(unsigned) * 128, st));
     HIP_TRY(hipMemsetAsync(s->d_stats.p, 0, sizeof(Counters), st));
 
     struct Events {                     // RAII: released on every return path
@@ -822,16 +898,19 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     rtg_render_stats stt{};
     std::vector<int> counts;
     const int max_levels = std::max(0, s->sv.max_depth) + 1;
-    for (int s0 = 0; s0 < total && npix > 0; s0 += ns_pass) {
-        int ns = std::min(ns_pass, total - s0);
-        int n0 = ns * npix;
+    for (int s0 = 0; s0 < total && npix > 0; s0 += ns_chunk)
+    for (int p0 = 0; p0 < npix; p0 += np_pass) {
+        PassDev ps;
+        ps.s0 = s0; ps.ns = std::min(ns_chunk, total - s0);
+        ps.p0 = p0; ps.npass = std::min(np_pass, npix - p0);
+        ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned;
+        const int n0 = ps.ns * ps.npass;
         counts.assign(1, n0);
         if ((int)s->levels.size() < 1) s->levels.resize(1);
         Level& L0 = s->levels[0];
         if ((rc = L0.rays.grow(sizeof(RayRec) * (size_t)n0)) || (rc = L0.meta.grow(sizeof(RayMeta) * (size_t)n0)))
             return rc;
-        launch_raygen(s->sv, cd, s0, ns, off, stride, rows_owned, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(),
-                      n0, st);
+        launch_raygen(s->sv, cd, ps, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(), n0, st);
         stt.primary_rays += (uint64_t)n0;
         int level = 0;
         for (;; level++) {
@@ -840,7 +919,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             Level& Lc = s->levels[level];
             Level& Ln = s->levels[level + 1];
             if ((rc = Lc.hits.grow(sizeof(HitRec) * (size_t)n)) || (rc = Lc.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
-                (rc = Lc.shadows.grow(sizeof(ShadowRec) * (size_t)n * std::max(nL, 1))))
+                (rc = Lc.shadows.grow(sizeof(ShadowRec) * (size_t)n * std::max(nL, 1))) ||
+                (rc = Lc.slist.grow(sizeof(int) * (size_t)n * std::max(nL, 1))))
                 return rc;
             bool may_spawn = level + 1 < max_levels;
             size_t cap = may_spawn ? 2 * (size_t)n : 1;
@@ -849,11 +929,14 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             launch_trace(s->sv, Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, st);
             if (timing) HIP_TRY(hipEventRecord(ev.e[3], st));
             HIP_TRY(hipMemsetAsync(d_cnt + 1 + level, 0, sizeof(unsigned), st));
-            launch_shade(s->sv, cd, level, s0, off, stride, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(),
-                         Lc.hits.as<HitRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Ln.rays.as<RayRec>(),
+            HIP_TRY(hipMemsetAsync(d_cnt + 64 + level, 0, sizeof(unsigned), st));
+            launch_shade(s->sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(),
+                         Lc.hits.as<HitRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
+                         d_cnt + 64 + level, Ln.rays.as<RayRec>(),
                          Ln.meta.as<RayMeta>(), d_cnt + 1 + level, n, st);
             if (timing) HIP_TRY(hipEventRecord(ev.e[4], st));
-            launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, st);
+            launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), d_cnt + 64 + level,
+                          Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, st);
             if (timing) HIP_TRY(hipEventRecord(ev.e[5], st));
             HIP_TRY(hipGetLastError());
             unsigned next = 0;
@@ -880,7 +963,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         for (int l = level - 1; l >= 0; l--)
             launch_resolve(s->sv, s->levels[l].nodes.as<NodeRec>(), s->levels[l + 1].nodes.as<NodeRec>(), counts[l], st);
         int mode = (total == 1) ? 2 : (s0 == 0 ? 1 : 0);
-        launch_accumulate(s->levels[0].nodes.as<NodeRec>(), s->d_acc.as<float>(), npix, ns, mode, st);
+        launch_accumulate(s->levels[0].nodes.as<NodeRec>(), s->d_acc.as<float>(), ps, cam->nx, mode, st);
         stt.passes++;
     }
     launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, cam->ny, off, stride, total, st);
@@ -900,6 +983,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     stt.tri_tests = ctr.tri_tests;
     stt.shadow_node_visits = ctr.shadow_node_visits;
     stt.shadow_tri_tests = ctr.shadow_tri_tests;
+    stt.trace_steps = ctr.trace_steps;
+    stt.shadow_steps = ctr.shadow_steps;
+    stt.trace_lane_slots = ctr.trace_lane_slots;
+    stt.shadow_lane_slots = ctr.shadow_lane_slots;
     s->stats = stt;
     return RTG_OK;
 }

@@ -24,13 +24,14 @@ struct TopObject {
     int material;           // 1-based (instance override applied)
     int geom;               // index of the geometry (base mesh for instances)
     int is_instance;
-    int pad0;
+    int ident;              // inv is exactly the identity (+0 off-diagonal) and blur is +0
 };
 
 // Per geometry (one per object; instances share their base mesh's geometry).
 struct Geometry {
     int type;               // rtg_object_type
     int node_base;          // absolute index of the BVH root in the node array (-1 if root is a leaf)
+    int node4_base;         // same in the Node4 array
     int root_leaf_start;    // absolute prim range when the root is a leaf (no box test)
     int root_leaf_count;    // -1: no primitives at all
     float root_min[3];      // root box (tested only when the root is interior)
@@ -60,12 +61,26 @@ struct Node {
     int4 d;
 };
 
+// 128-byte 4-wide node: the BVH2 node N with each interior child c replaced by c's two
+// children (slots 2q, 2q+1 come from N's child q).  Per-slot boxes in SoA form.
+// info: < 0 empty; 0 interior (ref = absolute Node4 index); > 0 leaf of `info & kSlotCount`
+// prims starting at ref (absolute).  kSlotGate marks a slot that came from a collapsed
+// interior child c: the reference reaches it only through c's box test, and c's box is the
+// union of the pair's two slot boxes (range boxes are unions of their children's).
+constexpr int kSlotGate = 0x40000000;
+constexpr int kSlotCount = 0x3fffffff;
+struct Node4 {
+    float4 lox, loy, loz, hix, hiy, hiz;
+    int4 ref;
+    int4 info;
+};
+
 // Triangle in BVH order: the Cramer-rule operands of Triangle::bvhIntersect
 // (src/Shape.cpp:415-432): a, a-b, a-c.  w lanes: x = original face index.
 struct TriGeom {
     float4 p0;  // a.xyz, (a-b).x
     float4 p1;  // (a-b).yz, (a-c).xy
-    float4 p2;  // (a-c).z, orig_index (bits), 0, 0
+    float4 p2;  // (a-c).z, orig_index (bits), leaf length (int bits, first prim of each leaf), 0
 };
 
 struct LightDev {
@@ -97,6 +112,7 @@ struct SceneView {
     const TopObject* tops; int num_tops; int num_objects;
     const Geometry* geoms;
     const Node* nodes;
+    const Node4* nodes4;
     const TriGeom* tris;
     const int4* prim_idx;          // BVH order: {v1,v2,v3 (1-based), smooth}; spheres {c,0,0,0}
     const float* vertices;         // xyz
@@ -112,6 +128,14 @@ struct SceneView {
     float background[3], ambient[3];
     int bg_texture, env_light;
     int full;                      // 0: no textures / BRDFs / area or environment lights
+};
+
+// One batch ("pass") of the frame: pixels [p0, p0 + npass) of the tiled pixel order (8x8
+// blocks over the rank's owned rows) x samples [s0, s0 + ns).  Ray slot = (t - p0) * ns + (s - s0):
+// all samples of a pixel are adjacent, so a wavefront traces near-identical rays.
+struct PassDev {
+    int s0, ns, p0, npass;
+    int row_offset, row_stride, rows_owned;
 };
 
 struct CameraDev {
@@ -170,23 +194,23 @@ struct ShadowRec {      // 64 B, nLights per shading node
 struct Counters {
     unsigned long long node_visits, tri_tests;           // closest-hit kernel
     unsigned long long shadow_node_visits, shadow_tri_tests;
+    unsigned long long trace_lane_slots, shadow_lane_slots, trace_steps, shadow_steps;
 };
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
 struct LevelBuffers;
-void launch_raygen(const SceneView& sv, const CameraDev& cam, int s0, int ns, int row_offset, int row_stride,
-                   int rows_owned, uint64_t seed, RayRec* rays, RayMeta* meta, int n, hipStream_t st);
+void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps, uint64_t seed, RayRec* rays,
+                   RayMeta* meta, int n, hipStream_t st);
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st);
-void launch_shade(const SceneView& sv, const CameraDev& cam, int level, int s0, int row_offset, int row_stride,
-                  uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
-                  ShadowRec* shadows, RayRec* next_rays, RayMeta* next_meta, unsigned* next_count, int n,
-                  hipStream_t st);
-void launch_shadow(const SceneView& sv, const ShadowRec* shadows, NodeRec* nodes, int n, int exhaustive,
-                   Counters* ctr, unsigned* traced, hipStream_t st);
+void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
+                  ShadowRec* shadows, int* slist, unsigned* scount, RayRec* next_rays, RayMeta* next_meta,
+                  unsigned* next_count, int n, hipStream_t st);
+void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
+                   int n, int exhaustive, Counters* ctr, unsigned* traced, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
-void launch_accumulate(const NodeRec* level0, float* acc, int npix, int ns, int mode, hipStream_t st);
+void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int total,
                      hipStream_t st);
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,

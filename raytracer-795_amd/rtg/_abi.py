@@ -109,7 +109,9 @@ class RenderStats(C.Structure):
                 ("total_rays", C.c_uint64), ("render_ms", C.c_double), ("passes", C.c_int32),
                 ("max_level", C.c_int32), ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("shadow_node_visits", C.c_uint64), ("shadow_tri_tests", C.c_uint64), ("trace_ms", C.c_double),
-                ("shadow_ms", C.c_double), ("trace_launches", C.c_int32), ("shadow_launches", C.c_int32)]
+                ("shadow_ms", C.c_double), ("trace_launches", C.c_int32), ("shadow_launches", C.c_int32),
+                ("trace_steps", C.c_uint64), ("shadow_steps", C.c_uint64),
+                ("trace_lane_slots", C.c_uint64), ("shadow_lane_slots", C.c_uint64)]
 
 
 class Ray(C.Structure):
@@ -153,7 +155,7 @@ def load_library(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("RTG_LIBRARY") or LIB_PATH   # RTG_LIBRARY: dev builds of variants
     if not os.path.exists(p):
         raise RtgError(f"librtg.so not found at {p}: run `python -c 'import __graft_entry__ as g; g.build()'`")
     # PyTorch-ROCm ships its own libamdhip64.so.7.  Loading torch first makes librtg bind to

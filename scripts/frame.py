@@ -1,0 +1,15 @@
+"""Render the bench frame N times (no stats, no timing) — the workload for PMC passes."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracer-795_amd"))
+import rtg  # noqa: E402
+from rtg import scenegen  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+sc = scenegen.dragon1m(1920, 1080, spp=64)
+r = rtg.Renderer(sc, 0)
+for _ in range(n):
+    r.render(0)
+print("frame ms", round(r.stats()["render_ms"], 1))

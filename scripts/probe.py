@@ -27,4 +27,10 @@ for kw in ({"collect_stats": 1}, {"collect_timing": 1}, {}):
     st = r.stats()
     st["wall_ms"] = round((time.time() - t0) * 1e3, 1)
     st["Mray_s"] = round(st["total_rays"] / st["render_ms"] / 1e3, 1)
+    if st["trace_lane_slots"]:
+        st["simd_eff_trace"] = round(st["trace_steps"] / st["trace_lane_slots"], 3)
+        st["simd_eff_shadow"] = round(st["shadow_steps"] / st["shadow_lane_slots"], 3)
+        tr = st["primary_rays"] + st["secondary_rays"]
+        st["steps_per_ray"] = round(st["trace_steps"] / tr, 2)
+        st["steps_per_shadow"] = round(st["shadow_steps"] / max(st["shadow_rays"], 1), 2)
     print(json.dumps({"opts": kw, **st}), flush=True)
