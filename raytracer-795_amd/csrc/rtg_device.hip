@@ -55,7 +55,22 @@ DEV float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x);
 DEV float f_cos(float x) { return (float)cos((double)x); }
 DEV float f_sin(float x) { return (float)sin((double)x); }
 DEV float f_exp(float x) { return (float)exp((double)x); }
-DEV float f_powi(float x, int n) { return (float)pow((double)x, (double)n); }
+// std::pow(float, int) == (float)pow(double, double).  Integer exponent by binary powering in
+// double: within ~log2(n) double ulps of the exact power, so the float result is the
+// correctly rounded one except within ~1e-15 of a float rounding boundary.
+DEV float f_powi(float x, int n) {
+    if (n == 0) return 1.0f;
+    double b = (double)x, r = 1.0;
+    unsigned e = n < 0 ? 0u - (unsigned)n : (unsigned)n;
+    while (e) {
+        if (e & 1u) r *= b;
+        e >>= 1;
+        if (e) b *= b;
+    }
+    return (float)(n < 0 ? 1.0 / r : r);
+}
+// pow(double(f), 2.0): the square of a float is exact in double
+DEV double sq_d(float x) { const double d = (double)x; return d * d; }
 
 // glm mat4 (column-major) * (v, w): (c0*x + c1*y) + (c2*z + c3*w)
 DEV f3 xform(const float* m, f3 v, float w) {
@@ -804,8 +819,8 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h)
 DEV float conductor_fresnel(float n_t, float k_t, f3 ray, f3 normal) {   // Light.cpp:156-166, Scene.cpp:266-277
     float cos_t = -dot(ray, normal);
     float twoNtCost = (2 * n_t) * cos_t;
-    float cosSquared = (float)pow((double)cos_t, 2.0);
-    float ntk = (float)(pow((double)n_t, 2.0) + pow((double)k_t, 2.0));
+    float cosSquared = (float)sq_d(cos_t);
+    float ntk = (float)(sq_d(n_t) + sq_d(k_t));
     float rs = ((ntk - twoNtCost) + cosSquared) / ((ntk + twoNtCost) + cosSquared);
     float rp = ((ntk * cosSquared - twoNtCost) + 1) / ((ntk * cosSquared + twoNtCost) + 1);
     return 0.5f * (rs + rp);
@@ -908,7 +923,7 @@ DEV f3 env_radiance(const SceneView& sv, const LightDev& L, f3 dir) {   // Light
 }
 
 // Unshadowed contribution of light li plus the shadow query it needs.
-template <bool FULL = true>
+template <bool FULL = true, bool SPOT = true>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
                       uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
     const LightDev& L = sv.lights[li];
@@ -935,7 +950,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         c = phong_or_brdf<FULL>(ld3(L.inten), wo, dir, ret, m);
         break;
     }
-    case RTG_LIGHT_SPOT: {                                      // :547-574
+    case RTG_LIGHT_SPOT: if constexpr (FULL || SPOT) {          // :547-574
         f3 pos = ld3(L.pos);
         f3 dv = pos - ret.point;
         dir = dv / norm(dv);
@@ -1172,14 +1187,14 @@ DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialD
     rd = wr;
 }
 
-template <bool FULL>
-__global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock>
+__global__ void __launch_bounds__(BLOCK) k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                uint64_t seed,
                                                const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
                                                const HitRec* __restrict__ hits, NodeRec* __restrict__ nodes,
                                                ShadowRec* __restrict__ shadows, int* __restrict__ slist,
-                                               unsigned* scount, RayRec* __restrict__ next_rays,
-                                               RayMeta* __restrict__ next_meta, unsigned* next_count, int n) {
+                                               RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
+                                               unsigned long long* qcount, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     int nchild = 0;
     RayRec c0r, c1r;
@@ -1243,7 +1258,7 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
                     else { snell = nt; normal = -ret.normal; n_t = 1; n_i = nt; entering = false; }
                     float cosTheta = -dot(d, normal);
                     f3 leftPart = (d + normal * cosTheta) * snell;
-                    float srp = (float)(1 - pow((double)snell, 2.0) * (1 - pow((double)cosTheta, 2.0)));
+                    float srp = (float)(1 - sq_d(snell) * (1 - sq_d(cosTheta)));
                     bool isTir = srp < 0;
                     srp = sqrtf(srp);
                     f3 tdir = normalized(leftPart - normal * srp);
@@ -1252,7 +1267,7 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
                     float cos_i = -dot(d, normal);
                     float rPar = (n_t * cos_i - n_i * cos_t) / (n_t * cos_i + n_i * cos_t);
                     float rPer = (n_i * cos_i - n_t * cos_t) / (n_i * cos_i + n_t * cos_t);
-                    nd.F = (float)(0.5f * (pow((double)rPar, 2.0) + pow((double)rPer, 2.0)));
+                    nd.F = (float)(0.5f * (sq_d(rPar) + sq_d(rPer)));
                     nd.kind = entering ? NK_DIEL_ENTER : (isTir ? NK_DIEL_TIR : NK_DIEL_EXIT);
                     basic = entering;
                     if (!(isnan3(torg) || isnan3(tdir))) {
@@ -1284,7 +1299,7 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
-                        light_sample<FULL>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
+                        light_sample<FULL, SPOT>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         shadows[(size_t)i * sv.num_lights + li] = sr;
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
@@ -1295,18 +1310,43 @@ __global__ void __launch_bounds__(256) k_shade(const SceneView sv, const CameraD
         if (basic) nd.kind |= 0x100;
         nchild = (has0 ? 1 : 0) + (has1 ? 1 : 0);
     }
-    // ballot/prefix-sum compaction of the next level's rays
-    int idx = wave_append(nchild, next_count);
+    // Compaction of the next level's rays and of the shadow-query list (entries
+    // i * nLights + li, light-major within a wave): ballot prefixes inside each wave, wave
+    // totals combined in LDS, ONE 64-bit atomic per block on the level's queue counter
+    // (low word: rays, high word: shadow entries).  Same-address atomics serialise at the L2
+    // (~11 ns each), so they are kept to one per block.
+    __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64];
+    __shared__ unsigned long long s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = __lanemask_lt();
+    const unsigned long long m1 = __ballot(nchild >= 1), m2 = __ballot(nchild >= 2);
+    const unsigned coff = __popcll(m1 & lt) + __popcll(m2 & lt);
+    unsigned stot = 0;
+    for (int li = 0; li < sv.num_lights; li++) stot += __popcll(__ballot((smask >> li) & 1ull));
+    if (lane == 0) { s_wc[w] = __popcll(m1) + __popcll(m2); s_ws[w] = stot; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned c = 0, sh = 0;
+        for (int k = 0; k < BLOCK / 64; k++) {
+            const unsigned a = s_wc[k], b = s_ws[k];
+            s_wc[k] = c; s_ws[k] = sh;
+            c += a; sh += b;
+        }
+        s_base = (c | sh) ? atomicAdd(qcount, ((unsigned long long)sh << 32) | c) : 0ull;
+    }
+    __syncthreads();
+    int idx = (int)((unsigned)s_base + s_wc[w] + coff);
     if (i < n) {
         if (has0) { next_rays[idx] = c0r; next_meta[idx] = c0m; nd.child0 = idx; idx++; }
         if (has1) { next_rays[idx] = c1r; next_meta[idx] = c1m; nd.child1 = idx; }
         nodes[i] = nd;
     }
-    // compacted shadow-query list (entries i * nLights + li)
+    unsigned sb = (unsigned)(s_base >> 32) + s_ws[w];
     for (int li = 0; li < sv.num_lights; li++) {
         const bool need = (smask >> li) & 1ull;
-        const int q = wave_append(need ? 1 : 0, scount);
-        if (need) slist[q] = i * sv.num_lights + li;
+        const unsigned long long m = __ballot(need);
+        if (need) slist[sb + __popcll(m & lt)] = i * sv.num_lights + li;
+        sb += __popcll(m);
     }
 }
 
@@ -1320,16 +1360,16 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_shadow(const Sce
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount,
                                                                        NodeRec* __restrict__ nodes,
-                                                                       unsigned* traced, Counters* ctr) {
+                                                                       unsigned* nan_queries, Counters* ctr) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned cnt = 0;
+    unsigned nanq = 0;
     Stats st = {0, 0, 0};
     if (j < (int)*scount) {
         const int idx = slist[j];
         const ShadowRec sr = shadows[idx];
         const f3 o = mk(sr.o.x, sr.o.y, sr.o.z), d = mk(sr.d.x, sr.d.y, sr.d.z);
-        if (!(isnan3(o) || isnan3(d))) cnt++;
+        if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
         HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
                                                   s_stack + threadIdx.x, kTraceBlock, st);
         const int i = idx / sv.num_lights;
@@ -1354,9 +1394,9 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_shadow(const Sce
             shadows[idx].L.w = blocked ? 0.0f : 1.0f;
         }
     }
-    // per-wave reduction of the traced-ray count
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off);
-    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(traced, cnt);
+    // NaN queries are rare: one atomic per wave that has any
+    const unsigned long long nm = __ballot(nanq != 0);
+    if (nm && (threadIdx.x & 63) == 0) atomicAdd(nan_queries, (unsigned)__popcll(nm));
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
         unsigned mx = st.steps;
@@ -1517,26 +1557,28 @@ void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, 
 }
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
-                  ShadowRec* shadows, int* slist, unsigned* scount, RayRec* next_rays, RayMeta* next_meta,
-                  unsigned* next_count, int n, hipStream_t st) {
+                  ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta,
+                  unsigned long long* qcount, int n, hipStream_t st) {
     if (n <= 0) return;
+    dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
     if (sv.full)
-        hipLaunchKernelGGL(k_shade<true>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta,
-                           hits, nodes, shadows, slist, scount, next_rays, next_meta,
-                           next_count, n);
+        hipLaunchKernelGGL((k_shade<true, true>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta, hits, nodes, shadows,
+                           slist, next_rays, next_meta, qcount, n);
+    else if (sv.spot)
+        hipLaunchKernelGGL((k_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, nodes,
+                           shadows, slist, next_rays, next_meta, qcount, n);
     else
-        hipLaunchKernelGGL(k_shade<false>, dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta,
-                           hits, nodes, shadows, slist, scount, next_rays, next_meta,
-                           next_count, n);
+        hipLaunchKernelGGL((k_shade<false, false>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, nodes,
+                           shadows, slist, next_rays, next_meta, qcount, n);
 }
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* traced, hipStream_t st) {
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st) {
     if (n <= 0 || sv.num_lights == 0) return;
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, traced, ctr);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, slist, scount, nodes, traced, ctr);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, traced, ctr);
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
     if (sv.num_lights > 1)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, shadows, nodes, n);
 }

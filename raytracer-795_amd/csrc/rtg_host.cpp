@@ -791,6 +791,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     for (int i = 0; i < d->num_materials; i++) sv.full |= d->materials[i].brdf != RTG_BRDF_NONE;
     for (int i = 0; i < d->num_lights; i++)
         sv.full |= d->lights[i].type == RTG_LIGHT_AREA || d->lights[i].type == RTG_LIGHT_ENVIRONMENT;
+    sv.spot = 0;
+    for (int i = 0; i < d->num_lights; i++) sv.spot |= d->lights[i].type == RTG_LIGHT_SPOT;
     return RTG_OK;
 }
 
@@ -878,11 +880,15 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
 
     int rc;
     if ((rc = s->d_acc.grow(sizeof(float) * 3 * std::max<size_t>(npix, 1)))) return rc;
-    if ((rc = s->d_counters.grow(sizeof(unsigned) * 128))) return rc;
+    // d_cnt[0]: NaN shadow queries; qcnt[level] (64-bit, from d_cnt + 64): next-level rays (low
+    // word) and shadow-query list length (high word) of each level of the current pass
+    if ((rc = s->d_counters.grow(sizeof(unsigned) * 64 + sizeof(unsigned long long) * 64))) return rc;
     if ((rc = s->d_stats.grow(sizeof(Counters)))) return rc;
     unsigned* d_cnt = s->d_counters.as<unsigned>();
     Counters* d_stats = s->d_stats.as<Counters>();
-    HIP_TRY(hipMemsetAsync(s->d_counters.p, 0, sizeof(unsigned) * 128, st));
+    HIP_TRY(hipMemsetAsync(s->d_counters.p, 0, sizeof(unsigned) * 64, st));
+    unsigned long long* qcnt = reinterpret_cast<unsigned long long*>(d_cnt + 64);
+    uint64_t shadow_listed = 0;
     HIP_TRY(hipMemsetAsync(s->d_stats.p, 0, sizeof(Counters), st));
 
     struct Events {                     // RAII: released on every return path
@@ -905,6 +911,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         ps.p0 = p0; ps.npass = std::min(np_pass, npix - p0);
         ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned;
         const int n0 = ps.ns * ps.npass;
+        HIP_TRY(hipMemsetAsync(qcnt, 0, sizeof(unsigned long long) * 64, st));
         counts.assign(1, n0);
         if ((int)s->levels.size() < 1) s->levels.resize(1);
         Level& L0 = s->levels[0];
@@ -928,20 +935,20 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             if (timing) HIP_TRY(hipEventRecord(ev.e[2], st));
             launch_trace(s->sv, Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, st);
             if (timing) HIP_TRY(hipEventRecord(ev.e[3], st));
-            HIP_TRY(hipMemsetAsync(d_cnt + 1 + level, 0, sizeof(unsigned), st));
-            HIP_TRY(hipMemsetAsync(d_cnt + 64 + level, 0, sizeof(unsigned), st));
             launch_shade(s->sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(),
                          Lc.hits.as<HitRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
-                         d_cnt + 64 + level, Ln.rays.as<RayRec>(),
-                         Ln.meta.as<RayMeta>(), d_cnt + 1 + level, n, st);
+                         Ln.rays.as<RayRec>(), Ln.meta.as<RayMeta>(), qcnt + level, n, st);
             if (timing) HIP_TRY(hipEventRecord(ev.e[4], st));
-            launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), d_cnt + 64 + level,
+            launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
+                          reinterpret_cast<const unsigned*>(qcnt + level) + 1,   // high word (little endian)
                           Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, st);
             if (timing) HIP_TRY(hipEventRecord(ev.e[5], st));
             HIP_TRY(hipGetLastError());
-            unsigned next = 0;
-            HIP_TRY(hipMemcpyAsync(&next, d_cnt + 1 + level, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+            unsigned long long q = 0;
+            HIP_TRY(hipMemcpyAsync(&q, qcnt + level, sizeof(q), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
+            const unsigned next = (unsigned)q;
+            shadow_listed += q >> 32;
             if (timing) {
                 float a = 0.0f, b = 0.0f;
                 HIP_TRY(hipEventElapsedTime(&a, ev.e[2], ev.e[3]));
@@ -972,11 +979,11 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     HIP_TRY(hipEventSynchronize(e1));
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-    unsigned shadow_cnt = 0;
+    unsigned nan_queries = 0;
     Counters ctr{};
-    HIP_TRY(hipMemcpy(&shadow_cnt, d_cnt, sizeof(unsigned), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&nan_queries, d_cnt, sizeof(unsigned), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&ctr, d_stats, sizeof(Counters), hipMemcpyDeviceToHost));
-    stt.shadow_rays = shadow_cnt;
+    stt.shadow_rays = shadow_listed - nan_queries;
     stt.total_rays = stt.primary_rays + stt.secondary_rays + stt.shadow_rays;
     stt.render_ms = ms;
     stt.node_visits = ctr.node_visits;

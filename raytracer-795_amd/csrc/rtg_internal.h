@@ -13,6 +13,7 @@ namespace rtg {
 constexpr int kMaxLights = 64;      // per-node shadow slots are statically strided
 constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
 constexpr int kTraceBlock = 256;
+constexpr int kShadeBlock = 512;
 
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:86-127):
 // objects first, then instances.  Read with scalar loads (wave-uniform loop).
@@ -128,6 +129,7 @@ struct SceneView {
     float background[3], ambient[3];
     int bg_texture, env_light;
     int full;                      // 0: no textures / BRDFs / area or environment lights
+    int spot;                      // any spot light (its double-precision cone math is compiled in)
 };
 
 // One batch ("pass") of the frame: pixels [p0, p0 + npass) of the tiled pixel order (8x8
@@ -204,10 +206,10 @@ void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps,
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st);
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
-                  ShadowRec* shadows, int* slist, unsigned* scount, RayRec* next_rays, RayMeta* next_meta,
-                  unsigned* next_count, int n, hipStream_t st);
+                  ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta,
+                  unsigned long long* qcount, int n, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* traced, hipStream_t st);
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
 void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);

@@ -283,6 +283,43 @@ def textured(nx=96, ny=72, spp=1) -> Scene:
     return sc
 
 
+def multilight(nx=320, ny=240, spp=1) -> Scene:
+    """Untextured scene with several light kinds (point, directional, two spots) and every
+    material type (rough mirror, conductor, dielectric): exercises the untextured shading
+    variant with spot lights and the in-order multi-light sum."""
+    sc = Scene(max_depth=4, background=(5, 5, 12), ambient=(12, 12, 12))
+    sc.cameras.append(_cam((0, 1.6, 6.0), (0, -0.2, -1), (0, 1, 0), nx, ny, fov_deg=50, spp=spp,
+                           name="multilight.png"))
+    sc.materials += [
+        Material(ambient=(1, 1, 1), diffuse=(0.7, 0.7, 0.7), specular=(0.2, 0.2, 0.2), phong_exp=8),
+        Material(type=A.MAT_MIRROR, ambient=(0.05, 0.05, 0.05), diffuse=(0.1, 0.1, 0.1),
+                 specular=(0.4, 0.4, 0.4), mirror=(0.7, 0.7, 0.7), phong_exp=40, is_rough=True, roughness=0.1),
+        Material(type=A.MAT_CONDUCTOR, ambient=(0.1, 0.1, 0.1), diffuse=(0.1, 0.1, 0.1),
+                 specular=(0.5, 0.5, 0.5), mirror=(0.9, 0.6, 0.3), phong_exp=70, refraction_index=0.27,
+                 absorption_index=2.77),
+        Material(type=A.MAT_DIELECTRIC, ambient=(0, 0, 0), diffuse=(0, 0, 0), specular=(0, 0, 0),
+                 refraction_index=1.45, absorption_coeff=(0.1, 0.05, 0.02)),
+        Material(ambient=(1, 1, 1), diffuse=(0.3, 0.5, 0.8), specular=(0.8, 0.8, 0.8), phong_exp=120),
+    ]
+    c = _add_vertices(sc, [(-1.6, 0.6, -0.5), (0.0, 0.6, -1.2), (1.6, 0.6, -0.5), (0.6, 0.35, 1.0)])
+    for k, mat in enumerate([2, 3, 4, 5]):
+        sc.objects.append(Object(type=A.OBJ_SPHERE, id=k + 1, material=mat, center=c + k,
+                                 radius=0.6 if k < 3 else 0.35))
+    fl = _add_vertices(sc, [(-6, 0, 6), (6, 0, 6), (6, 0, -6), (-6, 0, -6)])
+    sc.objects.append(Object(type=A.OBJ_MESH, id=1, material=1,
+                             faces=np.array([[fl, fl + 1, fl + 2], [fl, fl + 2, fl + 3]], np.int32)))
+    v, f = icosphere(2)
+    b = _add_vertices(sc, v * 0.45 + np.array([-0.7, 0.45, 1.3], f32))
+    sc.objects.append(Object(type=A.OBJ_MESH, id=2, material=5, faces=(f + b).astype(np.int32), smooth=True))
+    sc.lights.append(Light(type=A.LIGHT_POINT, position=(2, 5, 4), intensity=(9000, 9000, 9000)))
+    sc.lights.append(Light(type=A.LIGHT_DIRECTIONAL, direction=(0.4, -1, -0.3), intensity=(0.8, 0.8, 0.9)))
+    sc.lights.append(Light(type=A.LIGHT_SPOT, position=(-3, 4, 2), direction=(0.6, -1, -0.5),
+                           intensity=(20000, 15000, 12000), coverage_deg=40, falloff_deg=20))
+    sc.lights.append(Light(type=A.LIGHT_SPOT, position=(3, 3, -2), direction=(-0.7, -1, 0.4),
+                           intensity=(8000, 12000, 16000), coverage_deg=60, falloff_deg=45))
+    return sc
+
+
 CONFIGS = {
     "simple": simple,
     "bunny5k": bunny5k,
@@ -290,4 +327,5 @@ CONFIGS = {
     "cornell_dynamic": cornell,
     "cornell_pt": cornell_pt,
     "textured": textured,
+    "multilight": multilight,
 }

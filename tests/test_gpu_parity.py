@@ -24,6 +24,8 @@ SCENES = {
     "cornell_nodof": lambda: scenegen.cornell(48, 36, spp=3, dof=False),
     "textured": lambda: scenegen.textured(64, 48),
     "textured_ms": lambda: scenegen.textured(32, 24, spp=2),
+    "multilight": lambda: scenegen.multilight(64, 48),
+    "multilight_ms": lambda: scenegen.multilight(32, 24, spp=3),
 }
 
 
@@ -47,7 +49,7 @@ def test_render_matches_oracle(gpu, name, traversal):
     assert linf < TOL
 
 
-@pytest.mark.parametrize("name", ["simple", "bunny", "dragon", "cornell", "textured"])
+@pytest.mark.parametrize("name", ["simple", "bunny", "dragon", "cornell", "textured", "multilight"])
 def test_trace_matches_oracle(gpu, name):
     sc = SCENES[name]()
     rng = np.random.default_rng(11)
