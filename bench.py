@@ -33,6 +33,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the last committed PMC passes (separate
+    `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of this bench, gfx950-corrected by
+    scripts/pmc_traffic.py); None when absent."""
+    p = os.path.join(ROOT, "profiles", "traffic_current.json")
+    try:
+        with open(p) as f:
+            k = json.load(f)["kernels"].get(kernel)
+        return None if k is None else k["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(scene, rows: int, threads: int) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
@@ -139,7 +152,8 @@ def main():
     bytes_per_launch = bytes_per_ray * trace_rays / max(trace_launches, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("rtg::k_trace<false, false>"),
+            "traffic_unit": "bytes/launch (PMC, profiles/traffic_current.json)",
             "kernel": "k_trace<false,false> (closest hit, primary+secondary)",
             "avg_launch_ms": round(avg_launch_ms, 3), "launches": trace_launches,
             "bytes_per_ray": round(bytes_per_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Official bench line + rocprofv3 kernel-trace summary + separate PMC passes (FETCH_SIZE, WRITE_SIZE).
+# Afterwards (in the container): scripts/save_profile.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
