@@ -23,6 +23,12 @@ namespace rtg {
 #ifndef RTG_TRACE_ATTR
 #define RTG_TRACE_ATTR   // occupancy experiments: -DRTG_TRACE_ATTR='__attribute__((amdgpu_waves_per_eu(5)))'
 #endif
+#ifndef RTG_SHADOW_ATTR  // 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
+#define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+#ifndef RTG_SHADOW_ANY    // 1: certified early exit for blocked shadow queries (closest_hit ANY).  Off: on
+#define RTG_SHADOW_ANY 0  // dragon1m it saves 5% of the steps but costs 12 VGPRs (35.3 vs 32.6 ms)
+#endif
 constexpr double PI_D = 3.14159265358979323846;
 
 // ------------------------------------------------------------------ vectors (Eigen order)
@@ -266,9 +272,19 @@ struct Stats { unsigned nodes, tris, steps; };
 // the leaf.  This ordered traversal computes the same total order and prunes subtrees
 // whose distance lower bound exceeds the current best (EXHAUSTIVE disables pruning).
 // `tmax`: hits with gett() >= tmax are irrelevant to the caller (shadow queries).
-template <bool EXHAUSTIVE, bool STATS>
+//
+// ANY (shadow queries): `t_cert` > 0 is a parameter bound such that any object whose winning
+// candidate has 0 < gett() <= t_cert already decides the query as blocked (k_shadow derives it
+// from the light distance with rounding margins).  Inside a mesh, once a candidate c with
+// t_c (1 + 1e-4) <= t_cert is accepted, the object's winner has distance <= |c| and hence
+// t <= t_cert; the only way the object could still contribute nothing is a winner behind the
+// origin (gett <= 0, the src/BVH.cpp:159-173 quirk), which needs t <= t0w.  So the rest of
+// the object is walked with the window shrunk to [tlo, t0w]; if the winner seen then has
+// gett > 0 the query returns blocked (out.pad = 1), otherwise the object is walked again
+// without certification (exact closest-hit semantics).
+template <bool EXHAUSTIVE, bool STATS, bool ANY = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride,
-                       Stats& st) {
+                       Stats& st, float t_cert = 0.0f) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
@@ -293,9 +309,9 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         } else {
             // distance bound from the best hit so far (see DESIGN.md "pruning")
             float boundD = FLT_MAX;
+            const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
+            const float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
             if (!EXHAUSTIVE && nearest < FLT_MAX) {
-                float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
-                float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
                 float dl = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
                 if (da != 0.0f) {
                     float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * (1.0f + 1e-5f);
@@ -303,151 +319,159 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     if (!(boundD == boundD)) boundD = FLT_MAX;
                 }
             }
-            const float pad = g.prune_pad;
-            float best_d = FLT_MAX;
-            int best_leaf = -1;
-            // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
-            // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
-            // send every box to the exact division test instead.
-            const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
-            const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
-                              adz <= 1e30f;
-            const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
-            // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
-            // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
-            // skipped when its box, expanded by `pad`, meets the line only outside that window.
-            const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
-            const float tlo = -(fabsf(eps) + 1e-6f);
-            const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
-            const float inv_dn = 1.0f / dnorm;
-            float thi = INFINITY;
-            if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
-            const float tm_global = thi;
-            // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
-            auto test_prim = [&](const TriGeom& tg, int k, int start) {
-                if (STATS) st.tris++;
-                Cand c = tri_test(tg, o2, d2, eps);
-                if (c.ok) {
-                    float dist = norm(c.p - o2);
-                    if (dist < FLT_MAX &&
-                        (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
-                        best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
-                        if (!EXHAUSTIVE) thi = fminf(tm_global, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+            // gett() of a candidate with t <= t0w may come out <= 0 (error of p = o + d t in the
+            // first nonzero direction component); certification needs this to be excluded.
+            const float t0w = (8.0f * 5.9604645e-8f) * fabsf(oa) / fabsf(da) + 1e-30f;
+            bool allow_cert = ANY && t_cert > 0.0f && da != 0.0f && t0w < INFINITY;
+            for (;;) {
+                bool cert = false;
+                found = false; bprim = -1; bp = mk(0, 0, 0);
+                const float pad = g.prune_pad;
+                float best_d = FLT_MAX;
+                int best_leaf = -1;
+                // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
+                // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
+                // send every box to the exact division test instead.
+                const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
+                const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
+                                  adz <= 1e30f;
+                const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
+                // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
+                // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
+                // skipped when its box, expanded by `pad`, meets the line only outside that window.
+                const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
+                const float tlo = -(fabsf(eps) + 1e-6f);
+                const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+                const float inv_dn = 1.0f / dnorm;
+                float thi = INFINITY;
+                if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
+                const float tm_global = thi;
+                float tcap = tm_global;     // thi never exceeds this (shrinks to t0w once certified)
+                // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
+                auto test_prim = [&](const TriGeom& tg, int k, int start) {
+                    if (STATS) st.tris++;
+                    Cand c = tri_test(tg, o2, d2, eps);
+                    if (c.ok) {
+                        float dist = norm(c.p - o2);
+                        if (dist < FLT_MAX &&
+                            (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
+                            best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                            if (!EXHAUSTIVE) thi = fminf(tcap, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+                        }
+                        if (ANY && allow_cert && !cert && c.t > 2.0f * t0w && c.t * (1.0f + 1e-4f) <= t_cert) {
+                            cert = true;
+                            tcap = t0w;
+                            thi = fminf(thi, t0w);
+                        }
                     }
-                }
-            };
-            // one child box: reachability (interior, exact predicate) + window pruning + entry key
-            auto child = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool interior,
-                             float& key) -> bool {
-                key = 0.0f;
-                if (!EXHAUSTIVE && fast) {
-                    float ax = (mnx - o2.x) * inv.x, bx = (mxx - o2.x) * inv.x;
-                    float ay = (mny - o2.y) * inv.y, by = (mxy - o2.y) * inv.y;
-                    float az = (mnz - o2.z) * inv.z, bz = (mxz - o2.z) * inv.z;
-                    float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                    float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                    float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                    float lo = le - e - padt, hi = sl + e + padt;
-                    key = lo;
-                    if (hi < lo || hi < tlo || lo > thi) return false;
-                    if (!interior) return true;
-                    if (sl < le - e) return false;
-                    if (sl >= le + e) return true;
-                    return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
-                }
-                if (!interior) return true;
-                return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
-            };
-            if (g.node_base < 0) {
-                for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
-                    test_prim(sv.tris[k], k, g.root_leaf_start);
-            } else if (box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
-                               g.root_max[1], g.root_max[2])) {
-                // Leaf children are resolved as soon as they are reached.
-                auto leaf = [&](int start, int count) {
-                    for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
                 };
-                // BVH2 walk (ordered, pruned): the reference tree node by node.
-                auto walk2 = [&]() {
-                    int sp = 0;
-                    int cur = g.node_base;
-                    while (true) {
-                        if (STATS) { st.nodes += 2; st.steps++; }   // one 64-B node = two 32-B child records
-                        const Node nd = sv.nodes[cur];
-                        const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
-                        float lk = 0.0f, rk = 0.0f;
-                        bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
-                        bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
-                        bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
-                        if (lleaf && rleaf && rk < lk) {
-                            leaf(rref, rcnt);
-                            if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
-                            lok = rok = false;
-                        } else {
-                            if (lleaf) { leaf(lref, lcnt); lok = false; }
-                            if (rleaf) {
-                                if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
-                                rok = false;
+                // one child box: reachability (interior, exact predicate) + window pruning + entry key
+                auto child = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool interior,
+                                 float& key) -> bool {
+                    key = 0.0f;
+                    if (!EXHAUSTIVE && fast) {
+                        float ax = (mnx - o2.x) * inv.x, bx = (mxx - o2.x) * inv.x;
+                        float ay = (mny - o2.y) * inv.y, by = (mxy - o2.y) * inv.y;
+                        float az = (mnz - o2.z) * inv.z, bz = (mxz - o2.z) * inv.z;
+                        float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                        float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                        float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                        float lo = le - e - padt, hi = sl + e + padt;
+                        key = lo;
+                        if (hi < lo || hi < tlo || lo > thi) return false;
+                        if (!interior) return true;
+                        if (sl < le - e) return false;
+                        if (sl >= le + e) return true;
+                        return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+                    }
+                    if (!interior) return true;
+                    return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+                };
+                if (g.node_base < 0) {
+                    for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
+                        test_prim(sv.tris[k], k, g.root_leaf_start);
+                } else if (box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
+                                   g.root_max[1], g.root_max[2])) {
+                    // Leaf children are resolved as soon as they are reached.
+                    auto leaf = [&](int start, int count) {
+                        for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
+                    };
+                    // BVH2 walk (ordered, pruned): the reference tree node by node.
+                    auto walk2 = [&]() {
+                        int sp = 0;
+                        int cur = g.node_base;
+                        while (true) {
+                            if (STATS) { st.nodes += 2; st.steps++; }   // one 64-B node = two 32-B child records
+                            const Node nd = sv.nodes[cur];
+                            const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
+                            float lk = 0.0f, rk = 0.0f;
+                            bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
+                            bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
+                            bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
+                            if (lleaf && rleaf && rk < lk) {
+                                leaf(rref, rcnt);
+                                if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
+                                lok = rok = false;
+                            } else {
+                                if (lleaf) { leaf(lref, lcnt); lok = false; }
+                                if (rleaf) {
+                                    if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
+                                    rok = false;
+                                }
+                            }
+                            if (!EXHAUSTIVE) {
+                                lok = lok && !(lk > thi);
+                                rok = rok && !(rk > thi);
+                            }
+                            if (lok && rok) {
+                                int nearc = lref, farc = rref;
+                                if (rk < lk) { nearc = rref; farc = lref; }
+                                stack[sp * sstride] = farc;
+                                sp++;
+                                cur = nearc;
+                            } else if (lok) {
+                                cur = lref;
+                            } else if (rok) {
+                                cur = rref;
+                            } else {
+                                if (sp == 0) break;
+                                sp--;
+                                cur = stack[sp * sstride];
                             }
                         }
-                        if (!EXHAUSTIVE) {
-                            lok = lok && !(lk > thi);
-                            rok = rok && !(rk > thi);
-                        }
-                        if (lok && rok) {
-                            int nearc = lref, farc = rref;
-                            if (rk < lk) { nearc = rref; farc = lref; }
-                            stack[sp * sstride] = farc;
-                            sp++;
-                            cur = nearc;
-                        } else if (lok) {
-                            cur = lref;
-                        } else if (rok) {
-                            cur = rref;
-                        } else {
-                            if (sp == 0) break;
-                            sp--;
-                            cur = stack[sp * sstride];
-                        }
-                    }
-                };
+                    };
 #if RTG_BVH4
-                // 4-wide walk over the collapsed tree.  Slots of a collapsed child c need c's box
-                // hit too.  On the fast path the exact slab predicate is monotone under box
-                // containment (no zero direction component), so a slot whose own box -- or whose
-                // pair sibling's box -- is certainly hit implies c's hit; interior slots are
-                // themselves box-tested; only a leaf slot without such a witness tests the pair
-                // union (= c's range box) explicitly.  The exact / exhaustive paths test the union
-                // for every gated slot.  A stack that would overflow (> kStackDepth entries: up to
-                // 3 pushes per level) restarts the object on the BVH2 walk, whose depth bound
-                // fits; candidates already found stay valid.
-                bool overflow = false;
-                {
-                    int sp = 0;
-                    int cur = g.node4_base;
-                    while (true) {
-                        if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
-                        const Node4 nd = sv.nodes4[cur];
-                        const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
-                        const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
-                        const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
-                        const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
-                        const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
-                        const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
-                        const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
-                        const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
-                        float key[4];
-                        bool ok[4], sure[4];
-                        int gate_mask = 0;
+                    // 4-wide walk over the collapsed tree (fast reciprocal path only; exhaustive
+                    // traversal and rays with a zero / denormal / huge direction component use the
+                    // exact BVH2 walk).  Slots of a collapsed child c need c's box hit too.  The
+                    // exact slab predicate is monotone under box containment here (no zero direction
+                    // component), so a slot whose own box -- or whose pair sibling's box -- is
+                    // certainly hit implies c's hit; interior slots are themselves box-tested; only a
+                    // leaf slot without such a witness tests the pair union (= c's range box)
+                    // explicitly.  A stack that would overflow (> kStackDepth entries: up to 3
+                    // pushes per level) restarts the object on the BVH2 walk, whose depth bound
+                    // fits; candidates already found stay valid.
+                    bool use2 = EXHAUSTIVE || !fast;
+                    if (!use2) {
+                        int sp = 0;
+                        int cur = g.node4_base;
+                        while (true) {
+                            if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
+                            const Node4 nd = sv.nodes4[cur];
+                            const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
+                            const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
+                            const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
+                            const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
+                            const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
+                            const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
+                            const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
+                            const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
+                            // branch-free slot tests: ok (reachable and inside the window), sure (box
+                            // certainly hit), gate (interior slot in the uncertain band)
+                            float key[4];
+                            int okm = 0, surem = 0, gate_mask = 0, leafm = 0;
 #pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const int cnt = inf[j] & kSlotCount;
-                            const bool interior = cnt == 0;
-                            key[j] = 0.0f;
-                            sure[j] = false;
-                            ok[j] = false;
-                            if (inf[j] < 0) continue;
-                            if (!EXHAUSTIVE && fast) {
+                            for (int j = 0; j < 4; j++) {
                                 const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
                                 const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
                                 const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
@@ -456,115 +480,108 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                                 const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
                                 const float lo = le - e - padt, hi = sl + e + padt;
                                 key[j] = lo;
-                                sure[j] = sl >= le + e;
+                                const bool valid = inf[j] >= 0;
+                                const bool isleaf = (inf[j] & kSlotCount) != 0;
                                 const bool win = !(hi < lo || hi < tlo || lo > thi);
                                 const bool miss = sl < le - e;
-                                ok[j] = win && !(interior && miss);
-                                // interior slot in the uncertain band: exact predicate
-                                if (ok[j] && interior && !sure[j]) gate_mask |= 1 << j;
-                            } else {
-                                ok[j] = true;
-                                if (interior) gate_mask |= 1 << j;
+                                const bool sure = sl >= le + e;
+                                const bool ok = valid & win & (isleaf | !miss);
+                                okm |= ok << j;
+                                surem |= sure << j;
+                                gate_mask |= (ok & !isleaf & !sure) << j;
+                                leafm |= (valid & isleaf) << j;
                             }
-                        }
-                        // own exact tests of uncertain interior slots (rare on the fast path)
-                        while (gate_mask) {
-                            const int j = __builtin_ctz(gate_mask);
-                            gate_mask &= gate_mask - 1;
-                            const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
-                            const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
-                            const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
-                            const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
-                            const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
-                            const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
-                            const bool hit = box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2);
-                            if (!hit) {
-                                if (j == 0) ok[0] = false; else if (j == 1) ok[1] = false;
-                                else if (j == 2) ok[2] = false; else ok[3] = false;
-                            } else {
-                                if (j == 0) sure[0] = true; else if (j == 1) sure[1] = true;
-                                else if (j == 2) sure[2] = true; else sure[3] = true;
+                            // own exact tests of uncertain interior slots (rare)
+                            while (gate_mask) {
+                                const int j = __builtin_ctz(gate_mask);
+                                gate_mask &= gate_mask - 1;
+                                const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
+                                const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
+                                const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
+                                const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
+                                const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
+                                const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
+                                if (box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2)) surem |= 1 << j;
+                                else okm &= ~(1 << j);
                             }
-                        }
-                        // collapsed-child gates (pair union box), once per pair
+                            // collapsed-child gates (pair union box), once per pair: needed only for a
+                            // reachable leaf slot when neither slot of the pair is certainly hit
 #pragma unroll
-                        for (int p = 0; p < 4; p += 2) {
-                            const int g0 = inf[p], g1 = inf[p + 1];
-                            const bool gated = ((g0 >= 0 && (g0 & kSlotGate)) || (g1 >= 0 && (g1 & kSlotGate)));
-                            if (!gated) continue;
-                            bool need;
-                            if (!EXHAUSTIVE && fast)
-                                need = ((ok[p] && (g0 & kSlotCount) > 0) || (ok[p + 1] && (g1 & kSlotCount) > 0)) &&
-                                       !sure[p] && !sure[p + 1];
-                            else
-                                need = ok[p] || ok[p + 1];
-                            if (need) {
-                                const bool b0 = g0 >= 0, b1 = g1 >= 0;
-                                const float ux = b0 && b1 ? fminf(lx[p], lx[p + 1]) : (b0 ? lx[p] : lx[p + 1]);
-                                const float uy = b0 && b1 ? fminf(ly[p], ly[p + 1]) : (b0 ? ly[p] : ly[p + 1]);
-                                const float uz = b0 && b1 ? fminf(lz[p], lz[p + 1]) : (b0 ? lz[p] : lz[p + 1]);
-                                const float vx = b0 && b1 ? fmaxf(hx[p], hx[p + 1]) : (b0 ? hx[p] : hx[p + 1]);
-                                const float vy = b0 && b1 ? fmaxf(hy[p], hy[p + 1]) : (b0 ? hy[p] : hy[p + 1]);
-                                const float vz = b0 && b1 ? fmaxf(hz[p], hz[p + 1]) : (b0 ? hz[p] : hz[p + 1]);
-                                if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) ok[p] = ok[p + 1] = false;
+                            for (int q = 0; q < 4; q += 2) {
+                                const int g0 = inf[q], g1 = inf[q + 1];
+                                const bool gated = ((g0 >= 0) & ((g0 & kSlotGate) != 0)) | ((g1 >= 0) & ((g1 & kSlotGate) != 0));
+                                const int pm = 3 << q;
+                                if (gated && (okm & leafm & pm) && !(surem & pm)) {
+                                    const bool b0 = g0 >= 0, b1 = g1 >= 0;
+                                    const float ux = b0 && b1 ? fminf(lx[q], lx[q + 1]) : (b0 ? lx[q] : lx[q + 1]);
+                                    const float uy = b0 && b1 ? fminf(ly[q], ly[q + 1]) : (b0 ? ly[q] : ly[q + 1]);
+                                    const float uz = b0 && b1 ? fminf(lz[q], lz[q + 1]) : (b0 ? lz[q] : lz[q + 1]);
+                                    const float vx = b0 && b1 ? fmaxf(hx[q], hx[q + 1]) : (b0 ? hx[q] : hx[q + 1]);
+                                    const float vy = b0 && b1 ? fmaxf(hy[q], hy[q + 1]) : (b0 ? hy[q] : hy[q + 1]);
+                                    const float vz = b0 && b1 ? fmaxf(hz[q], hz[q + 1]) : (b0 ? hz[q] : hz[q + 1]);
+                                    if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) okm &= ~pm;
+                                }
                             }
-                        }
-                        // interior candidates first, so the node's boxes are dead during leaf tests
-                        float k4[4];
-                        int r4[4];
-                        int leaf_mask = 0;
+                            // interior candidates first, so the node's boxes are dead during leaf tests
+                            float k4[4];
+                            int r4[4];
 #pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const bool isleaf = (inf[j] & kSlotCount) > 0;
-                            const bool take = ok[j] && !isleaf;
-                            k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
-                            r4[j] = take ? rf[j] : -1;
-                            if (ok[j] && isleaf && (EXHAUSTIVE || !(key[j] > thi))) leaf_mask |= 1 << j;
-                        }
-                        // leaves now, one code site (thi may shrink between them)
-                        while (leaf_mask) {
-                            const int j = __builtin_ctz(leaf_mask);
-                            leaf_mask &= leaf_mask - 1;
-                            const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
-                            const int info = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
-                            leaf(start, info & kSlotCount);
-                        }
-                        if (!EXHAUSTIVE) {
+                            for (int j = 0; j < 4; j++) {
+                                const bool take = ((okm >> j) & 1) && !((leafm >> j) & 1);
+                                k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
+                                r4[j] = take ? rf[j] : -1;
+                            }
+                            int leaf_mask = okm & leafm;
+                            // leaves now, one code site (thi may shrink between them)
+                            while (leaf_mask) {
+                                const int j = __builtin_ctz(leaf_mask);
+                                leaf_mask &= leaf_mask - 1;
+                                const float kj = j == 0 ? key[0] : j == 1 ? key[1] : j == 2 ? key[2] : key[3];
+                                if (kj > thi) continue;
+                                const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
+                                const int info = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
+                                leaf(start, info & kSlotCount);
+                            }
 #pragma unroll
                             for (int j = 0; j < 4; j++)
                                 if (k4[j] > thi) { k4[j] = INFINITY; r4[j] = -1; }
-                        }
-                        // interior slots, nearest first: sort (key, ref), push the others farthest first
-                        auto ce = [&](int a, int b) {
-                            const bool sw = k4[b] < k4[a];
-                            const float ka = k4[a], kb = k4[b];
-                            const int ra = r4[a], rb = r4[b];
-                            k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
-                            r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
-                        };
-                        ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-                        const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
-                        if (sp + npush > kStackDepth) { overflow = true; break; }
-                        if (r4[3] >= 0) { stack[sp * sstride] = r4[3]; sp++; }
-                        if (r4[2] >= 0) { stack[sp * sstride] = r4[2]; sp++; }
-                        if (r4[1] >= 0) { stack[sp * sstride] = r4[1]; sp++; }
-                        if (r4[0] >= 0) {
-                            cur = r4[0];
-                        } else {
-                            if (sp == 0) break;
-                            sp--;
-                            cur = stack[sp * sstride];
+                            // interior slots, nearest first: sort (key, ref), push the others farthest first
+                            auto ce = [&](int a, int b) {
+                                const bool sw = k4[b] < k4[a];
+                                const float ka = k4[a], kb = k4[b];
+                                const int ra = r4[a], rb = r4[b];
+                                k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
+                                r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
+                            };
+                            ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+                            const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
+                            if (sp + npush > kStackDepth) { use2 = true; break; }
+                            if (r4[3] >= 0) { stack[sp * sstride] = r4[3]; sp++; }
+                            if (r4[2] >= 0) { stack[sp * sstride] = r4[2]; sp++; }
+                            if (r4[1] >= 0) { stack[sp * sstride] = r4[1]; sp++; }
+                            if (r4[0] >= 0) {
+                                cur = r4[0];
+                            } else {
+                                if (sp == 0) break;
+                                sp--;
+                                cur = stack[sp * sstride];
+                            }
                         }
                     }
-                }
-                if (overflow) walk2();
+                    if (use2) walk2();
 #else
-                walk2();
+                    walk2();
 #endif
+                }
+                if (!(ANY && cert)) break;
+                const float tw = gett(o2, d2, bp);
+                if (tw > 0) { out.obj = i; out.prim = bprim; out.t = tw; out.pad = 1; return out; }
+                allow_cert = false;     // winner behind the origin: walk the object again, exactly
             }
         }
         if (found) {
             float t = gett(o2, d2, bp);
+            if (ANY && t > 0 && t <= t_cert) { out.obj = i; out.prim = bprim; out.t = t; out.pad = 1; return out; }
             if (t < nearest && t > 0) {
                 nearest = t;
                 out.obj = i; out.prim = bprim; out.t = t;
@@ -1355,7 +1372,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(const SceneView sv, const Camer
 // added to the node colour here (col + c or col + 0, as Scene::RecursiveShading's light loop
 // does); with several, the visibility is recorded and k_light_sum adds them in light order.
 template <bool EXHAUSTIVE, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_shadow(const SceneView sv,
+__global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const SceneView sv,
                                                                        ShadowRec* __restrict__ shadows,
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount,
@@ -1370,17 +1387,45 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_shadow(const Sce
         const ShadowRec sr = shadows[idx];
         const f3 o = mk(sr.o.x, sr.o.y, sr.o.z), d = mk(sr.d.x, sr.d.y, sr.d.z);
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
-        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
-                                                  s_stack + threadIdx.x, kTraceBlock, st);
         const int i = idx / sv.num_lights;
+        const NodeRec& nr = nodes[i];   // (p, lp: only for t_cert; re-read after the traversal)
+        const f3 p = mk(nr.px, nr.py, nr.pz);
+        const f3 lp = mk(sr.L.x, sr.L.y, sr.L.z);
+        // Certification bound (closest_hit ANY): for 0 < t <= t_cert the computed
+        // norm(p - (o + d t)) stays below the computed norm(p - L) (the point-light test of
+        // PointLight::IsShadow, src/Light.cpp:188-205): |p - hp| <= |p - o| + t|d| plus rounding
+        // of hp, of the difference and of the norm, all inside the 1e-5 relative margins.
+        // Directional / environment queries are blocked by any hit (t_cert = inf).
+        float t_cert = 0.0f;
+        if (!EXHAUSTIVE) {
+            if (sr.c.w == 1.0f) {
+                const float DL = norm(p - lp);
+                const float po = norm(p - o), dn = norm(d);
+                const float S = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(p.x))),
+                                      fmaxf(fabsf(p.y), fabsf(p.z)));
+                const float num = DL * (1.0f - 1e-5f) - 1e-5f * S - po * (1.0f + 1e-5f);
+                if (num > 0.0f && dn > 0.0f) t_cert = num / (dn * (1.0f + 2e-5f));
+                if (!(t_cert < FLT_MAX)) t_cert = 0.0f;
+            } else {
+                t_cert = INFINITY;
+            }
+        }
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, !EXHAUSTIVE && RTG_SHADOW_ANY>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
+                                                               s_stack + threadIdx.x, kTraceBlock, st, t_cert);
         bool blocked;
-        if (sr.c.w == 1.0f) {
+        if (h.pad == 1) {
+            blocked = true;         // certified by closest_hit (ANY)
+        } else if (sr.c.w == 1.0f) {
             blocked = false;
             if (h.obj >= 0) {
-                const NodeRec& nr = nodes[i];
-                f3 p = mk(nr.px, nr.py, nr.pz);
-                f3 hp = o + d * h.t;
-                blocked = norm(p - mk(sr.L.x, sr.L.y, sr.L.z)) > norm(p - hp);
+                // re-read (not kept live across the traversal: register pressure)
+                const float* q = reinterpret_cast<const float*>(shadows + idx);
+                auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
+                const f3 o_ = mk(ld(q + 0), ld(q + 1), ld(q + 2)), d_ = mk(ld(q + 4), ld(q + 5), ld(q + 6));
+                const f3 l_ = mk(ld(q + 12), ld(q + 13), ld(q + 14));
+                const f3 p_ = mk(ld(&nodes[i].px), ld(&nodes[i].py), ld(&nodes[i].pz));
+                f3 hp = o_ + d_ * h.t;
+                blocked = norm(p_ - l_) > norm(p_ - hp);
             }
         } else {
             blocked = h.obj >= 0;
