@@ -291,6 +291,9 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     float nearest = tmax;
     const float eps = sv.int_eps;
     for (int i = 0; i < sv.num_tops; i++) {
+#ifdef RTG_DBG_ONLYOBJ
+        if (i != RTG_DBG_ONLYOBJ) continue;
+#endif
         const TopObject& T = sv.tops[i];
         const Geometry& g = sv.geoms[T.geom];
         f3 o2, d2;
@@ -394,7 +397,9 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                                    g.root_max[1], g.root_max[2])) {
                     // Leaf children are resolved as soon as they are reached.
                     auto leaf = [&](int start, int count) {
+#ifndef RTG_DBG_NOLEAF
                         for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
+#endif
                     };
                     // BVH2 walk (ordered, pruned): the reference tree node by node.
                     auto walk2 = [&]() {

@@ -12,7 +12,10 @@ namespace rtg {
 
 constexpr int kMaxLights = 64;      // per-node shadow slots are statically strided
 constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
-constexpr int kTraceBlock = 256;
+#ifndef RTG_TRACE_BLOCK
+#define RTG_TRACE_BLOCK 64
+#endif
+constexpr int kTraceBlock = RTG_TRACE_BLOCK;   // threads per traversal block (LDS stack: 128 B per lane)
 constexpr int kShadeBlock = 512;
 
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:86-127):

@@ -17,6 +17,8 @@ elif name == "bunny5k":
     sc = scenegen.bunny5k(1920, 1080, spp=spp)
 else:
     sc = scenegen.cornell(1920, 1080, spp=spp)
+if len(sys.argv) > 3:
+    sc.max_depth = int(sys.argv[3])     # e.g. 0: primary rays only (fixed trace input across variants)
 t0 = time.time()
 r = rtg.Renderer(sc, 0)
 print("create", round(time.time() - t0, 2), "s", flush=True)
