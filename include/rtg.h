@@ -204,6 +204,7 @@ typedef struct rtg_render_opts {
     int32_t max_batch_rays;  /* 0 = auto */
     int32_t collect_stats;   /* 1 = count BVH node visits / triangle tests (slower) */
     int32_t collect_timing;  /* 1 = HIP-event time every closest-hit / shadow launch */
+    int32_t streams;         /* passes in flight on separate HIP streams (0 = library default, 3) */
 } rtg_render_opts;
 
 typedef struct rtg_render_stats {

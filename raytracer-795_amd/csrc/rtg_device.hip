@@ -26,6 +26,9 @@ namespace rtg {
 #ifndef RTG_SHADOW_ATTR  // 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
+#ifndef RTG_PACKET        // 1: wave-packet walk of the 4-wide tree (scalar node loads, one stack per wave)
+#define RTG_PACKET 0
+#endif
 #ifndef RTG_SHADOW_ANY    // 1: certified early exit for blocked shadow queries (closest_hit ANY).  Off: on
 #define RTG_SHADOW_ANY 0  // dragon1m it saves 5% of the steps but costs 12 VGPRs (35.3 vs 32.6 ms)
 #endif
@@ -262,7 +265,9 @@ DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d
     d2 = xform(T.inv, d, 0.0f);
 }
 
-struct Stats { unsigned nodes, tris, steps; };
+// steps: node steps of this lane; iters: loop iterations its wave ran for it (packet walk:
+// one per node the packet visits; per-lane walk: = steps, the wave runs max over lanes)
+struct Stats { unsigned nodes, tris, steps, iters; };
 
 // ------------------------------------------------------------------ closest hit
 // BVHMethods::FindIntersection (src/Helper.cpp:72-134) with the per-object nearest
@@ -284,7 +289,7 @@ struct Stats { unsigned nodes, tris, steps; };
 // without certification (exact closest-hit semantics).
 template <bool EXHAUSTIVE, bool STATS, bool ANY = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride,
-                       Stats& st, float t_cert = 0.0f) {
+                       int* wst_node, unsigned long long* wst_mask, Stats& st, float t_cert = 0.0f) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
@@ -457,6 +462,144 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     // pushes per level) restarts the object on the BVH2 walk, whose depth bound
                     // fits; candidates already found stay valid.
                     bool use2 = EXHAUSTIVE || !fast;
+#if RTG_PACKET
+                    // Packet walk: the wave traverses the collapsed tree together.  Rays of one wave
+                    // are the samples of one pixel (or of an 8x8 tile at 1 spp), so they visit nearly
+                    // the same nodes: the node index and its 128-B record are wave-uniform (scalar
+                    // loads into SGPRs), the stack is one per wave (LDS), and every lane applies its
+                    // own exact box predicate and parameter window -- a child is pushed with the mask
+                    // of the lanes that reach it, a leaf is tested by the lanes that reach it.  Each
+                    // lane therefore tests exactly the leaves the per-ray walk would reach (minus
+                    // window-pruned ones), and the result is order independent.
+                    {
+                        const unsigned long long pk = __ballot(!use2);
+                        if (pk) {
+                            const int lane = __lane_id();
+                            int psp = 0;
+                            int cur = __builtin_amdgcn_readfirstlane(g.node4_base);
+                            unsigned long long m = pk;
+                            while (true) {
+                                const bool in = (m >> lane) & 1ull;
+                                if (STATS) st.iters++;
+                                if (STATS && in) { st.nodes += 4; st.steps++; }
+                                const Node4 nd = sv.nodes4[cur];
+                                const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
+                                const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
+                                const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
+                                const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
+                                const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
+                                const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
+                                const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
+                                const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
+                                float key[4];
+                                int okm = 0, surem = 0, gate_mask = 0;
+#pragma unroll
+                                for (int j = 0; j < 4; j++) {
+                                    const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
+                                    const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
+                                    const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
+                                    const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                                    const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                                    const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                                    const float lo = le - e - padt, hi = sl + e + padt;
+                                    key[j] = lo;
+                                    const bool valid = inf[j] >= 0;
+                                    const bool isleaf = (inf[j] & kSlotCount) != 0;
+                                    const bool win = !(hi < lo || hi < tlo || lo > thi);
+                                    const bool miss = sl < le - e;
+                                    const bool sure = sl >= le + e;
+                                    const bool ok = in & valid & win & (isleaf | !miss);
+                                    okm |= ok << j;
+                                    surem |= sure << j;
+                                    gate_mask |= (ok & !isleaf & !sure) << j;
+                                }
+                                while (gate_mask) {          // exact tests of uncertain interior slots (rare)
+                                    const int j = __builtin_ctz(gate_mask);
+                                    gate_mask &= gate_mask - 1;
+                                    const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
+                                    const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
+                                    const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
+                                    const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
+                                    const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
+                                    const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
+                                    if (box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2)) surem |= 1 << j;
+                                    else okm &= ~(1 << j);
+                                }
+#pragma unroll
+                                for (int q = 0; q < 4; q += 2) {   // collapsed-child gates (pair union box)
+                                    const int g0 = inf[q], g1 = inf[q + 1];
+                                    const bool gated = ((g0 >= 0) & ((g0 & kSlotGate) != 0)) | ((g1 >= 0) & ((g1 & kSlotGate) != 0));
+                                    const int lm = (((g0 & kSlotCount) != 0) & (g0 >= 0)) | ((((g1 & kSlotCount) != 0) & (g1 >= 0)) << 1);
+                                    const int pm = 3 << q;
+                                    if (gated && (okm & (lm << q)) && !(surem & pm)) {
+                                        const bool b0 = g0 >= 0, b1 = g1 >= 0;
+                                        const float ux = b0 && b1 ? fminf(lx[q], lx[q + 1]) : (b0 ? lx[q] : lx[q + 1]);
+                                        const float uy = b0 && b1 ? fminf(ly[q], ly[q + 1]) : (b0 ? ly[q] : ly[q + 1]);
+                                        const float uz = b0 && b1 ? fminf(lz[q], lz[q + 1]) : (b0 ? lz[q] : lz[q + 1]);
+                                        const float vx = b0 && b1 ? fmaxf(hx[q], hx[q + 1]) : (b0 ? hx[q] : hx[q + 1]);
+                                        const float vy = b0 && b1 ? fmaxf(hy[q], hy[q + 1]) : (b0 ? hy[q] : hy[q + 1]);
+                                        const float vz = b0 && b1 ? fmaxf(hz[q], hz[q + 1]) : (b0 ? hz[q] : hz[q + 1]);
+                                        if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) okm &= ~pm;
+                                    }
+                                }
+                                // leaf slots: the lanes that reach them (and whose window still admits
+                                // them) test the primitives; the triangle records are wave-uniform
+#pragma unroll
+                                for (int j = 0; j < 4; j++) {
+                                    const int cnt = inf[j] & kSlotCount;
+                                    if (inf[j] < 0 || cnt == 0) continue;
+                                    const bool me = ((okm >> j) & 1) && !(key[j] > thi);
+                                    if (!__ballot(me)) continue;
+                                    const int start = rf[j];
+                                    for (int k = start; k < start + cnt; k++) {
+                                        const TriGeom tg = sv.tris[k];
+                                        if (me) test_prim(tg, k, start);
+                                    }
+                                }
+                                // interior slots: masks of the lanes that reach them (window-pruned),
+                                // ordered by the entry key of their first lane, pushed far first
+                                float k4[4];
+                                int r4[4];
+                                unsigned long long m4[4];
+#pragma unroll
+                                for (int j = 0; j < 4; j++) {
+                                    const bool interior = inf[j] >= 0 && (inf[j] & kSlotCount) == 0;
+                                    const bool me = ((okm >> j) & 1) && !(key[j] > thi);
+                                    const unsigned long long mj = interior ? __ballot(me) : 0ull;
+                                    m4[j] = mj;
+                                    r4[j] = rf[j];
+                                    k4[j] = mj ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                     __builtin_bit_cast(int, key[j]), (int)__builtin_ctzll(mj)))
+                                               : INFINITY;
+                                }
+                                auto ce = [&](int a, int b) {
+                                    const bool sw = k4[b] < k4[a] || (m4[a] == 0ull && m4[b] != 0ull);
+                                    const float ka = k4[a], kb = k4[b];
+                                    const int ra = r4[a], rb = r4[b];
+                                    const unsigned long long ma = m4[a], mb = m4[b];
+                                    k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
+                                    r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
+                                    m4[a] = sw ? mb : ma; m4[b] = sw ? ma : mb;
+                                };
+                                ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+#pragma unroll
+                                for (int j = 3; j >= 1; j--)
+                                    if (m4[j]) { wst_node[psp] = r4[j]; wst_mask[psp] = m4[j]; psp++; }
+                                if (m4[0]) {
+                                    cur = r4[0];
+                                    m = m4[0];
+                                } else {
+                                    if (psp == 0) break;
+                                    psp--;
+                                    cur = __builtin_amdgcn_readfirstlane(wst_node[psp]);
+                                    m = wst_mask[psp];
+                                    m = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
+                                        (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
+                                }
+                            }
+                        }
+                    }
+#else
                     if (!use2) {
                         int sp = 0;
                         int cur = g.node4_base;
@@ -573,6 +716,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                             }
                         }
                     }
+#endif
                     if (use2) walk2();
 #else
                     walk2();
@@ -1142,17 +1286,20 @@ template <bool EXHAUSTIVE, bool STATS>
 __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayRec* __restrict__ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
+    __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
+    __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Stats st = {0, 0, 0};
+    Stats st = {0, 0, 0, 0};
     if (i < n) {
         RayRec r = rays[i];
         HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, mk(r.o_t.x, r.o_t.y, r.o_t.z), mk(r.d.x, r.d.y, r.d.z), r.o_t.w,
-                                                  r.d.w, s_stack + threadIdx.x, kTraceBlock, st);
+                                                  r.d.w, s_stack + threadIdx.x, kTraceBlock, s_wnode[threadIdx.x >> 6],
+                                                  s_wmask[threadIdx.x >> 6], st);
         hits[i] = h;
     }
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
-        unsigned mx = st.steps;
+        unsigned mx = RTG_PACKET ? st.iters : st.steps;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
@@ -1384,9 +1531,11 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        NodeRec* __restrict__ nodes,
                                                                        unsigned* nan_queries, Counters* ctr) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
+    __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
+    __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
-    Stats st = {0, 0, 0};
+    Stats st = {0, 0, 0, 0};
     if (j < (int)*scount) {
         const int idx = slist[j];
         const ShadowRec sr = shadows[idx];
@@ -1416,7 +1565,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             }
         }
         HitRec h = closest_hit<EXHAUSTIVE, STATS, !EXHAUSTIVE && RTG_SHADOW_ANY>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
-                                                               s_stack + threadIdx.x, kTraceBlock, st, t_cert);
+                                                               s_stack + threadIdx.x, kTraceBlock, s_wnode[threadIdx.x >> 6],
+                                                               s_wmask[threadIdx.x >> 6], st, t_cert);
         bool blocked;
         if (h.pad == 1) {
             blocked = true;         // certified by closest_hit (ANY)
@@ -1449,7 +1599,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     if (nm && (threadIdx.x & 63) == 0) atomicAdd(nan_queries, (unsigned)__popcll(nm));
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
-        unsigned mx = st.steps;
+        unsigned mx = RTG_PACKET ? st.iters : st.steps;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);

@@ -8,11 +8,13 @@
 // rtg_render() drives the per-level kernels of rtg_device.hip.
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <new>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -363,6 +365,42 @@ int upload(DBuf& b, const std::vector<T>& v) {
 
 struct Level {
     DBuf rays, meta, hits, nodes, shadows, slist;
+    void release() { rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release(); }
+};
+
+// One in-flight pass: its own stream, level buffers and queue counters, so that while the
+// host waits for one pass's level count the GPU runs the other passes' kernels (the tails of
+// the per-level launches overlap instead of draining the device).
+struct Lane {
+    hipStream_t st = nullptr;
+    hipEvent_t ev_count = nullptr;          // recorded after the level count copy
+    hipEvent_t ev_t[4] = {};                // trace start/end, shadow start/end (collect_timing)
+    unsigned long long* h_count = nullptr;  // pinned host slot
+    DBuf qcnt;                              // 64 x u64 per pass (level -> next rays | shadow entries << 32)
+    std::vector<Level> levels;
+    // current pass
+    std::vector<int> passes;                // indices into the frame's pass list (this lane's, in order)
+    size_t next_pass = 0;
+    bool busy = false;
+    int pass = -1, level = 0;
+    std::vector<int> counts;
+    int create() {
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&ev_count, hipEventDisableTiming));
+        for (hipEvent_t& e : ev_t) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipHostMalloc((void**)&h_count, sizeof(unsigned long long), hipHostMallocDefault));
+        return RTG_OK;
+    }
+    void destroy() {
+        for (Level& l : levels) l.release();
+        qcnt.release();
+        if (h_count) (void)hipHostFree(h_count);
+        for (hipEvent_t e : ev_t) if (e) (void)hipEventDestroy(e);
+        if (ev_count) (void)hipEventDestroy(ev_count);
+        if (st) (void)hipStreamDestroy(st);
+        h_count = nullptr; ev_count = nullptr; st = nullptr;
+        for (hipEvent_t& e : ev_t) e = nullptr;
+    }
 };
 
 }  // namespace
@@ -378,9 +416,10 @@ struct rtg_scene {
     DBuf d_tops, d_geoms, d_nodes, d_nodes4, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
         d_texels, d_lights, d_origprim;
     // render workspace
-    std::vector<Level> levels;
+    std::vector<Lane> lanes;
     DBuf d_acc, d_counters, d_stats;
     rtg_render_stats stats{};
+    int num_lanes = 3;                       // default passes in flight (env RTG_STREAMS overrides)
 };
 
 extern "C" {
@@ -460,7 +499,8 @@ static void scene_free(rtg_scene* s) {
                     &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights, &s->d_origprim,
                     &s->d_acc, &s->d_counters, &s->d_stats};
     for (DBuf* b : bufs) b->release();
-    for (Level& l : s->levels) { l.rays.release(); l.meta.release(); l.hits.release(); l.nodes.release(); l.shadows.release(); l.slist.release(); }
+    for (Lane& l : s->lanes) l.destroy();
+    s->lanes.clear();
 }
 
 int32_t rtg_scene_destroy(rtg_scene* s) {
@@ -812,6 +852,7 @@ int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene**
     rtg_scene* s = new (std::nothrow) rtg_scene();
     if (!s) return fail(RTG_ERR_OOM, "host allocation");
     s->device = device;
+    if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
     rc = build_scene(s, desc);
     if (rc) {
         scene_free(s);
@@ -871,7 +912,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     if (npix_ll > (1LL << 30)) return fail(RTG_ERR_UNSUPPORTED, "image too large");
     int npix = (int)npix_ll;
     int total = cam->num_samples;
-    long long max_batch = o.max_batch_rays > 0 ? o.max_batch_rays : (4LL << 20);
+    long long max_batch = o.max_batch_rays > 0 ? o.max_batch_rays : (8LL << 20);
     // passes: all samples of a pixel range (chunks of samples only when spp exceeds the batch)
     const int ns_chunk = (int)std::max<long long>(1, std::min<long long>(total, max_batch));
     const int np_pass = (int)std::max<long long>(1, std::min<long long>(npix, max_batch / ns_chunk));
@@ -880,98 +921,165 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
 
     int rc;
     if ((rc = s->d_acc.grow(sizeof(float) * 3 * std::max<size_t>(npix, 1)))) return rc;
-    // d_cnt[0]: NaN shadow queries; qcnt[level] (64-bit, from d_cnt + 64): next-level rays (low
-    // word) and shadow-query list length (high word) of each level of the current pass
-    if ((rc = s->d_counters.grow(sizeof(unsigned) * 64 + sizeof(unsigned long long) * 64))) return rc;
+    // d_cnt[0]: NaN shadow queries (all passes)
+    if ((rc = s->d_counters.grow(sizeof(unsigned) * 64))) return rc;
     if ((rc = s->d_stats.grow(sizeof(Counters)))) return rc;
     unsigned* d_cnt = s->d_counters.as<unsigned>();
     Counters* d_stats = s->d_stats.as<Counters>();
     HIP_TRY(hipMemsetAsync(s->d_counters.p, 0, sizeof(unsigned) * 64, st));
-    unsigned long long* qcnt = reinterpret_cast<unsigned long long*>(d_cnt + 64);
-    uint64_t shadow_listed = 0;
     HIP_TRY(hipMemsetAsync(s->d_stats.p, 0, sizeof(Counters), st));
+    uint64_t shadow_listed = 0;
 
     struct Events {                     // RAII: released on every return path
-        hipEvent_t e[6] = {};
+        hipEvent_t e[3] = {};
         ~Events() { for (hipEvent_t x : e) if (x) (void)hipEventDestroy(x); }
     } ev;
     for (hipEvent_t& x : ev.e) HIP_TRY(hipEventCreate(&x));
-    hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1], ejoin = ev.e[2];
     HIP_TRY(hipEventRecord(e0, st));
     const bool timing = o.collect_timing != 0;
     Counters* sctr = o.collect_stats ? d_stats : nullptr;
 
-    rtg_render_stats stt{};
-    std::vector<int> counts;
-    const int max_levels = std::max(0, s->sv.max_depth) + 1;
-    for (int s0 = 0; s0 < total && npix > 0; s0 += ns_chunk)
-    for (int p0 = 0; p0 < npix; p0 += np_pass) {
-        PassDev ps;
-        ps.s0 = s0; ps.ns = std::min(ns_chunk, total - s0);
-        ps.p0 = p0; ps.npass = std::min(np_pass, npix - p0);
-        ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned;
-        const int n0 = ps.ns * ps.npass;
-        HIP_TRY(hipMemsetAsync(qcnt, 0, sizeof(unsigned long long) * 64, st));
-        counts.assign(1, n0);
-        if ((int)s->levels.size() < 1) s->levels.resize(1);
-        Level& L0 = s->levels[0];
-        if ((rc = L0.rays.grow(sizeof(RayRec) * (size_t)n0)) || (rc = L0.meta.grow(sizeof(RayMeta) * (size_t)n0)))
-            return rc;
-        launch_raygen(s->sv, cd, ps, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(), n0, st);
-        stt.primary_rays += (uint64_t)n0;
-        int level = 0;
-        for (;; level++) {
-            int n = counts[level];
-            if ((int)s->levels.size() < level + 2) s->levels.resize(level + 2);
-            Level& Lc = s->levels[level];
-            Level& Ln = s->levels[level + 1];
-            if ((rc = Lc.hits.grow(sizeof(HitRec) * (size_t)n)) || (rc = Lc.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
-                (rc = Lc.shadows.grow(sizeof(ShadowRec) * (size_t)n * std::max(nL, 1))) ||
-                (rc = Lc.slist.grow(sizeof(int) * (size_t)n * std::max(nL, 1))))
-                return rc;
-            bool may_spawn = level + 1 < max_levels;
-            size_t cap = may_spawn ? 2 * (size_t)n : 1;
-            if ((rc = Ln.rays.grow(sizeof(RayRec) * cap)) || (rc = Ln.meta.grow(sizeof(RayMeta) * cap))) return rc;
-            if (timing) HIP_TRY(hipEventRecord(ev.e[2], st));
-            launch_trace(s->sv, Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, st);
-            if (timing) HIP_TRY(hipEventRecord(ev.e[3], st));
-            launch_shade(s->sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(),
-                         Lc.hits.as<HitRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
-                         Ln.rays.as<RayRec>(), Ln.meta.as<RayMeta>(), qcnt + level, n, st);
-            if (timing) HIP_TRY(hipEventRecord(ev.e[4], st));
-            launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
-                          reinterpret_cast<const unsigned*>(qcnt + level) + 1,   // high word (little endian)
-                          Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, st);
-            if (timing) HIP_TRY(hipEventRecord(ev.e[5], st));
-            HIP_TRY(hipGetLastError());
-            unsigned long long q = 0;
-            HIP_TRY(hipMemcpyAsync(&q, qcnt + level, sizeof(q), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            const unsigned next = (unsigned)q;
-            shadow_listed += q >> 32;
-            if (timing) {
-                float a = 0.0f, b = 0.0f;
-                HIP_TRY(hipEventElapsedTime(&a, ev.e[2], ev.e[3]));
-                stt.trace_ms += a;
-                stt.trace_launches++;
-                if (nL > 0) {
-                    HIP_TRY(hipEventElapsedTime(&b, ev.e[4], ev.e[5]));
-                    stt.shadow_ms += b;
-                    stt.shadow_launches++;
-                }
-            }
-            if (next > cap) return fail(RTG_ERR_HIP, "secondary queue overflow");
-            if (next == 0 || !may_spawn) break;
-            counts.push_back((int)next);
-            stt.secondary_rays += next;
-            if (level + 1 >= 62) return fail(RTG_ERR_UNSUPPORTED, "recursion deeper than 62 levels");
+    // the frame's passes: pixel ranges (outer) x sample chunks (inner); all chunks of one pixel
+    // range go to the same lane, in order (MultiSample's in-order sum, src/Scene.cpp:519-540)
+    std::vector<PassDev> plist;
+    for (int p0 = 0; p0 < npix; p0 += np_pass)
+        for (int s0 = 0; s0 < total; s0 += ns_chunk) {
+            PassDev ps;
+            ps.s0 = s0; ps.ns = std::min(ns_chunk, total - s0);
+            ps.p0 = p0; ps.npass = std::min(np_pass, npix - p0);
+            ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned;
+            plist.push_back(ps);
         }
+    const int nranges = npix > 0 ? (npix + np_pass - 1) / np_pass : 1;
+    const int want_lanes = std::max(1, std::min(o.streams > 0 ? std::min(o.streams, 8) : s->num_lanes, nranges));
+    while ((int)s->lanes.size() < want_lanes) {
+        s->lanes.emplace_back();
+        if ((rc = s->lanes.back().create())) { s->lanes.back().destroy(); s->lanes.pop_back(); return rc; }
+    }
+    const int L = want_lanes;
+    for (int k = 0; k < L; k++) {
+        Lane& ln = s->lanes[k];
+        ln.passes.clear(); ln.next_pass = 0; ln.busy = false;
+        HIP_TRY(hipStreamWaitEvent(ln.st, e0, 0));
+    }
+    for (size_t k = 0; k < plist.size(); k++) {
+        const int prange = plist[k].p0 / np_pass;
+        s->lanes[prange % L].passes.push_back((int)k);
+    }
+
+    rtg_render_stats stt{};
+    const int max_levels = std::max(0, s->sv.max_depth) + 1;
+    // enqueue trace / shade / shadow of the lane's current level and the count read-back
+    auto enqueue_level = [&](Lane& ln) -> int {
+        const PassDev& ps = plist[ln.pass];
+        const int level = ln.level;
+        const int n = ln.counts[level];
+        if ((int)ln.levels.size() < level + 2) ln.levels.resize(level + 2);
+        Level& Lc = ln.levels[level];
+        Level& Ln = ln.levels[level + 1];
+        int rc2;
+        if ((rc2 = Lc.hits.grow(sizeof(HitRec) * (size_t)n)) || (rc2 = Lc.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
+            (rc2 = Lc.shadows.grow(sizeof(ShadowRec) * (size_t)n * std::max(nL, 1))) ||
+            (rc2 = Lc.slist.grow(sizeof(int) * (size_t)n * std::max(nL, 1))))
+            return rc2;
+        const bool may_spawn = level + 1 < max_levels;
+        const size_t cap = may_spawn ? 2 * (size_t)n : 1;
+        if ((rc2 = Ln.rays.grow(sizeof(RayRec) * cap)) || (rc2 = Ln.meta.grow(sizeof(RayMeta) * cap))) return rc2;
+        unsigned long long* qc = ln.qcnt.as<unsigned long long>() + level;
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
+        launch_trace(s->sv, Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st);
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
+        launch_shade(s->sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
+                     Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), Ln.rays.as<RayRec>(),
+                     Ln.meta.as<RayMeta>(), qc, n, ln.st);
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
+        launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
+                      reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
+                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st);
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
+        HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
+        return RTG_OK;
+    };
+    auto start_pass = [&](Lane& ln) -> int {
+        ln.pass = ln.passes[ln.next_pass++];
+        const PassDev& ps = plist[ln.pass];
+        const int n0 = ps.ns * ps.npass;
+        int rc2;
+        if ((rc2 = ln.qcnt.grow(sizeof(unsigned long long) * 64))) return rc2;
+        HIP_TRY(hipMemsetAsync(ln.qcnt.p, 0, sizeof(unsigned long long) * 64, ln.st));
+        ln.counts.assign(1, n0);
+        ln.level = 0;
+        if ((int)ln.levels.size() < 1) ln.levels.resize(1);
+        Level& L0 = ln.levels[0];
+        if ((rc2 = L0.rays.grow(sizeof(RayRec) * (size_t)n0)) || (rc2 = L0.meta.grow(sizeof(RayMeta) * (size_t)n0)))
+            return rc2;
+        launch_raygen(s->sv, cd, ps, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(), n0, ln.st);
+        stt.primary_rays += (uint64_t)n0;
+        ln.busy = true;
+        return enqueue_level(ln);
+    };
+    auto finish_pass = [&](Lane& ln) {
+        const PassDev& ps = plist[ln.pass];
+        const int level = ln.level;
         stt.max_level = std::max(stt.max_level, level);
         for (int l = level - 1; l >= 0; l--)
-            launch_resolve(s->sv, s->levels[l].nodes.as<NodeRec>(), s->levels[l + 1].nodes.as<NodeRec>(), counts[l], st);
-        int mode = (total == 1) ? 2 : (s0 == 0 ? 1 : 0);
-        launch_accumulate(s->levels[0].nodes.as<NodeRec>(), s->d_acc.as<float>(), ps, cam->nx, mode, st);
+            launch_resolve(s->sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(), ln.counts[l],
+                           ln.st);
+        const int mode = (total == 1) ? 2 : (ps.s0 == 0 ? 1 : 0);
+        launch_accumulate(ln.levels[0].nodes.as<NodeRec>(), s->d_acc.as<float>(), ps, cam->nx, mode, ln.st);
         stt.passes++;
+        ln.busy = false;
+    };
+    std::deque<int> waiting;           // lanes with a level in flight, in enqueue order
+    for (int k = 0; k < L; k++)
+        if (!s->lanes[k].passes.empty() && npix > 0) {
+            if ((rc = start_pass(s->lanes[k]))) return rc;
+            waiting.push_back(k);
+        }
+    while (!waiting.empty()) {
+        const int k = waiting.front();
+        waiting.pop_front();
+        Lane& ln = s->lanes[k];
+        HIP_TRY(hipEventSynchronize(ln.ev_count));
+        const unsigned long long q = *ln.h_count;
+        const unsigned next = (unsigned)q;
+        shadow_listed += q >> 32;
+        if (timing) {
+            float a = 0.0f, b = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&a, ln.ev_t[0], ln.ev_t[1]));
+            stt.trace_ms += a;
+            stt.trace_launches++;
+            if (nL > 0) {
+                HIP_TRY(hipEventElapsedTime(&b, ln.ev_t[2], ln.ev_t[3]));
+                stt.shadow_ms += b;
+                stt.shadow_launches++;
+            }
+        }
+        const int n = ln.counts[ln.level];
+        const bool may_spawn = ln.level + 1 < max_levels;
+        const size_t cap = may_spawn ? 2 * (size_t)n : 1;
+        if (next > cap) return fail(RTG_ERR_HIP, "secondary queue overflow");
+        if (next > 0 && may_spawn) {
+            if (ln.level + 1 >= 62) return fail(RTG_ERR_UNSUPPORTED, "recursion deeper than 62 levels");
+            ln.counts.push_back((int)next);
+            stt.secondary_rays += next;
+            ln.level++;
+            if ((rc = enqueue_level(ln))) return rc;
+            waiting.push_back(k);
+            continue;
+        }
+        finish_pass(ln);
+        if (ln.next_pass < ln.passes.size()) {
+            if ((rc = start_pass(ln))) return rc;
+            waiting.push_back(k);
+        }
+    }
+    for (int k = 0; k < L; k++) {
+        HIP_TRY(hipEventRecord(ejoin, s->lanes[k].st));
+        HIP_TRY(hipStreamWaitEvent(st, ejoin, 0));
     }
     launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, cam->ny, off, stride, total, st);
     HIP_TRY(hipGetLastError());

@@ -11,7 +11,8 @@
 namespace rtg {
 
 constexpr int kMaxLights = 64;      // per-node shadow slots are statically strided
-constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
+constexpr int kStackDepth = 32;
+constexpr int kPacketStack = 64;    // wave stack of the packet walk: <= 3 pushes per 4-wide level, <= 16 levels     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
 #ifndef RTG_TRACE_BLOCK
 #define RTG_TRACE_BLOCK 64
 #endif

@@ -52,7 +52,7 @@ class Renderer:
 
     @staticmethod
     def opts(seed=DEFAULT_SEED, row_offset=0, row_stride=1, traversal=0, max_batch_rays=0, collect_stats=0,
-             collect_timing=0):
+             collect_timing=0, streams=0):
         o = A.RenderOpts()
         o.seed = seed
         o.row_offset, o.row_stride = row_offset, row_stride
@@ -60,6 +60,7 @@ class Renderer:
         o.max_batch_rays = max_batch_rays
         o.collect_stats = collect_stats
         o.collect_timing = collect_timing
+        o.streams = streams
         return o
 
     def render(self, camera: Camera | int = 0, **kw) -> np.ndarray:

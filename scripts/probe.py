@@ -23,7 +23,9 @@ t0 = time.time()
 r = rtg.Renderer(sc, 0)
 print("create", round(time.time() - t0, 2), "s", flush=True)
 r.render(0)
+base = {"max_batch_rays": int(os.environ.get("RTG_BATCH", "0"))}
 for kw in ({"collect_stats": 1}, {"collect_timing": 1}, {}):
+    kw = {**base, **kw}
     t0 = time.time()
     r.render(0, **kw)
     st = r.stats()
