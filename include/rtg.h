@@ -256,6 +256,26 @@ int32_t rtg_device_count(void);
    the host-side structures (matrices, normals, BVH) for introspection; such a scene
    cannot render or trace (RTG_ERR_NO_DEVICE). */
 int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene** out);
+
+/* BVH builder selection for rtg_scene_create_ex.  All builders produce the reference's tree
+   (src/BVH.cpp:64-135) bit for bit; they differ only in where the work runs. */
+typedef enum rtg_bvh_builder {
+    RTG_BVH_AUTO = 0,   /* GPU for meshes of >= 4096 finite triangles on a device scene, else host */
+    RTG_BVH_HOST = 1,   /* recursive host build */
+    RTG_BVH_GPU = 2     /* level-synchronous GPU build (falls back to host for non-finite input) */
+} rtg_bvh_builder;
+typedef struct rtg_build_opts {
+    int32_t bvh_builder;     /* rtg_bvh_builder */
+} rtg_build_opts;
+/* rtg_scene_create with build options (NULL = defaults). */
+int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rtg_build_opts* opts,
+                            rtg_scene** out);
+typedef struct rtg_build_stats {
+    double bvh_build_ms;     /* wall time of all per-object BVH constructions */
+    int32_t bvh_gpu_objects; /* objects whose BVH was built on the GPU */
+    int32_t num_objects;
+} rtg_build_stats;
+int32_t rtg_scene_build_stats(const rtg_scene* scene, rtg_build_stats* out);
 int32_t rtg_scene_destroy(rtg_scene* scene);
 
 /* Render one camera; rgb_out is caller-owned host memory of ny*nx*3 floats ([y][x][c]). */

@@ -1,0 +1,440 @@
+// rtg_bvh_gpu.hip — the reference's per-object BVH construction on the GPU.
+//
+// Reproduces BVH::ConstructionHelper / FindMedian / ComputeBoundingBox (src/BVH.cpp:64-135,
+// 268-303) bit for bit -- the same primitive permutation, the same tree, the same node boxes --
+// level by level instead of recursively:
+//
+//   * split: the median of the segment's centres along axis depth % 3 (even count: the mean of
+//     the two middle values, computed as (lower + upper) * 0.5f).  One radix sort per level of
+//     64-bit keys (segment id << 32 | order-preserving float bits) yields every segment's order
+//     statistics at once.
+//   * partition: the reference's in-place loop `if (c[i] < split) swap(p[s++], p[i])` (a Lomuto
+//     partition) is evaluated in closed form.  With k = #less and lessPrefix(i) = #less in
+//     [0, i): the less elements land at lessPrefix(i) in order; the element ending at position
+//     j >= k is resolve(j), where resolve(j) = e_j if e_j is not less, else
+//     resolve(lessPrefix(j)) (the swap moves the oldest element of the ">= block" to the scan
+//     position).  lessPrefix(j) < j, so the chains are resolved by pointer jumping.
+//   * boxes: min / max of the primitive boxes over the node's range in the order the reference
+//     sees it; ties between equal values (+0 / -0) keep the earliest element, as the reference's
+//     `a <= b ? a : b` fold does.  Non-finite inputs are rejected (the host builder handles them).
+//   * leaves: one primitive, or depth 30 (possibly empty); empty ranges below depth 30 are null.
+//
+// Node numbering here is breadth-first; the host converts to the reference's pre-order.
+#include <float.h>
+#include <limits.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <string>
+#include <vector>
+
+#include "rtg_internal.h"
+
+namespace rtg {
+namespace {
+
+constexpr int kMaxDepth = 30;      // src/BVH.cpp:67
+constexpr int kBigNode = 512;      // box reduction: one block per node from this length on
+
+__device__ __forceinline__ uint32_t ord_bits(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_bits(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+struct Seg {       // one interior node of the current level
+    int start, end, node, off;   // off: position of its keys in the sorted array
+};
+
+__global__ void k_segid(int n, const Seg* __restrict__ segs, int S, int* __restrict__ segid) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int lo = 0, hi = S - 1, r = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (segs[mid].start <= i) { r = mid; lo = mid + 1; } else { hi = mid - 1; }
+    }
+    segid[i] = (r >= 0 && i < segs[r].end) ? r : S;
+}
+
+__global__ void k_keys(int n, int axis, const int* __restrict__ segid, int S, const int* __restrict__ perm,
+                       const float* __restrict__ c3, unsigned long long* __restrict__ keys) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int sid = segid[i];
+    unsigned long long k = (unsigned long long)S << 32;
+    if (sid < S) k = ((unsigned long long)sid << 32) | ord_bits(c3[3 * perm[i] + axis]);
+    keys[i] = k;
+}
+
+__global__ void k_split(const Seg* __restrict__ segs, int S, const unsigned long long* __restrict__ sorted,
+                        float* __restrict__ split) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const Seg g = segs[s];
+    const int len = g.end - g.start, mi = len / 2;
+    float v = unord_bits((uint32_t)sorted[g.off + mi]);                 // FindMedian, src/BVH.cpp:117-135
+    if (len % 2 == 0) {
+        const float lower = unord_bits((uint32_t)sorted[g.off + mi - 1]);
+        v = (lower + v) * 0.5f;
+    }
+    split[s] = v;
+}
+
+__global__ void k_less(int n, int axis, const int* __restrict__ segid, int S, const int* __restrict__ perm,
+                       const float* __restrict__ c3, const float* __restrict__ split, int* __restrict__ less) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    int l = 0;
+    if (i < n) {
+        const int sid = segid[i];
+        if (sid < S) l = c3[3 * perm[i] + axis] < split[sid];
+    }
+    less[i] = l;      // less[n] = 0: the exclusive scan then has n + 1 entries
+}
+
+__global__ void k_ptr_init(int n, const int* __restrict__ segid, int S, const Seg* __restrict__ segs,
+                           const int* __restrict__ G, const int* __restrict__ less, int* __restrict__ ptr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int sid = segid[i];
+    int p = i;
+    if (sid < S && less[i]) {
+        const int st = segs[sid].start;
+        p = st + (G[i] - G[st]);           // resolve(i) = resolve(lessPrefix(i))
+    }
+    ptr[i] = p;
+}
+
+// In-place pointer jumping: every write replaces ptr[i] by one of its ancestors, so concurrent
+// updates are safe and every chain ends at a non-less element (lessPrefix(j) < j).
+__global__ void k_jump(int n, int* ptr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int p = ptr[i];
+    while (true) {
+        const int q = ptr[p];
+        if (q == p) break;
+        const int r = ptr[q];
+        if (r == q) { p = q; break; }
+        p = r;
+        ptr[i] = p;
+    }
+    ptr[i] = p;
+}
+
+__global__ void k_scatter(int n, const int* __restrict__ segid, int S, const Seg* __restrict__ segs,
+                          const int* __restrict__ G, const int* __restrict__ less, const int* __restrict__ ptr,
+                          const int* __restrict__ perm, int* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int sid = segid[i];
+    if (sid >= S) { out[i] = perm[i]; return; }
+    const Seg g = segs[sid];
+    const int k = G[g.end] - G[g.start];
+    if (less[i]) out[g.start + (G[i] - G[g.start])] = perm[i];
+    if (i >= g.start + k) out[i] = perm[ptr[i]];
+}
+
+// Children of every segment: counts of nodes and of interior (next-level) segments.
+__device__ __forceinline__ int child_kind(int len, int depth) {   // 0 null, 1 leaf, 2 interior
+    if (len == 1 || depth >= kMaxDepth) return 1;                 // src/BVH.cpp:67-76
+    if (len == 0) return 0;                                       // :77
+    return 2;
+}
+__global__ void k_child_count(const Seg* __restrict__ segs, int S, int depth1, const int* __restrict__ G,
+                              int* __restrict__ nnodes, int* __restrict__ nint) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > S) return;
+    int a = 0, b = 0;
+    if (s < S) {
+        const Seg g = segs[s];
+        const int k = G[g.end] - G[g.start];
+        const int kl = child_kind(k, depth1), kr = child_kind(g.end - g.start - k, depth1);
+        a = (kl != 0) + (kr != 0);
+        b = (kl == 2) + (kr == 2);
+    }
+    nnodes[s] = a;     // entry S = 0 (exclusive scans of S + 1 entries give the totals)
+    nint[s] = b;
+}
+__global__ void k_child_emit(const Seg* __restrict__ segs, int S, int depth1, const int* __restrict__ G,
+                             const int* __restrict__ node_off, const int* __restrict__ int_off, int node_base,
+                             int4* __restrict__ nodes, Seg* __restrict__ next, int* __restrict__ big,
+                             int* __restrict__ nbig) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const Seg g = segs[s];
+    const int k = G[g.end] - G[g.start];
+    const int r0[2] = {g.start, g.start + k}, r1[2] = {g.start + k, g.end};
+    int id = node_base + node_off[s], nx = int_off[s];
+    int child[2] = {-1, -1};
+    for (int q = 0; q < 2; q++) {
+        const int len = r1[q] - r0[q];
+        const int kind = child_kind(len, depth1);
+        if (kind == 0) continue;
+        child[q] = id;
+        nodes[id] = make_int4(-1, -1, r0[q], r1[q]);
+        if (len >= kBigNode) big[atomicAdd(nbig, 1)] = id;
+        if (kind == 2) { Seg c; c.start = r0[q]; c.end = r1[q]; c.node = id; c.off = 0; next[nx++] = c; }
+        id++;
+    }
+    nodes[g.node].x = child[0];
+    nodes[g.node].y = child[1];
+}
+
+// Segment key offsets: exclusive sum of lengths (written into Seg.off)
+__global__ void k_seg_len(const Seg* __restrict__ segs, int S, int* __restrict__ len) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < S) len[s] = segs[s].end - segs[s].start;
+}
+__global__ void k_seg_off(Seg* __restrict__ segs, int S, const int* __restrict__ off) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < S) segs[s].off = off[s];
+}
+
+// ComputeBoundingBox (src/BVH.cpp:268-303): min/max with ties -> earliest element.
+struct MinMax {
+    float v[6];     // min xyz, max xyz
+    int at[6];      // position that supplied the value (-1: the FLT_MAX / -FLT_MAX start)
+};
+__device__ __forceinline__ void mm_init(MinMax& m) {
+    for (int z = 0; z < 3; z++) { m.v[z] = FLT_MAX; m.v[3 + z] = -FLT_MAX; m.at[z] = m.at[3 + z] = -1; }
+}
+__device__ __forceinline__ void mm_push(MinMax& m, int pos, const float* lo, const float* hi) {   // in order
+    for (int z = 0; z < 3; z++) {
+        if (!(m.v[z] <= lo[z])) { m.v[z] = lo[z]; m.at[z] = pos; }
+        if (!(m.v[3 + z] >= hi[z])) { m.v[3 + z] = hi[z]; m.at[3 + z] = pos; }
+    }
+}
+__device__ __forceinline__ void mm_merge(MinMax& a, const MinMax& b) {   // order-independent (value, position)
+    for (int z = 0; z < 6; z++) {
+        const bool take = (z < 3) ? (b.v[z] < a.v[z] || (b.v[z] == a.v[z] && b.at[z] < a.at[z]))
+                                  : (b.v[z] > a.v[z] || (b.v[z] == a.v[z] && b.at[z] < a.at[z]));
+        if (take) { a.v[z] = b.v[z]; a.at[z] = b.at[z]; }
+    }
+}
+__global__ void k_box_small(const int4* __restrict__ nodes, int first, int count, const int* __restrict__ perm,
+                            const float* __restrict__ lo3, const float* __restrict__ hi3, float* __restrict__ box) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const int id = first + t;
+    const int4 nd = nodes[id];
+    if (nd.w - nd.z >= kBigNode) return;
+    MinMax m;
+    mm_init(m);
+    for (int p = nd.z; p < nd.w; p++) {
+        const int f = perm[p];
+        mm_push(m, p, lo3 + 3 * f, hi3 + 3 * f);
+    }
+    for (int z = 0; z < 6; z++) box[6 * (size_t)id + z] = m.v[z];
+}
+__global__ void __launch_bounds__(256) k_box_big(const int* __restrict__ big, const int* __restrict__ nbig,
+                                                 const int4* __restrict__ nodes,
+                                                 const int* __restrict__ perm, const float* __restrict__ lo3,
+                                                 const float* __restrict__ hi3, float* __restrict__ box) {
+    __shared__ MinMax sm[256];
+    if ((int)blockIdx.x >= *nbig) return;       // grid sized by an upper bound
+    const int id = big[blockIdx.x];
+    const int4 nd = nodes[id];
+    const int len = nd.w - nd.z;
+    const int per = (len + 255) / 256;
+    const int a = nd.z + threadIdx.x * per, b = min(nd.w, a + per);   // contiguous chunk per thread
+    MinMax m;
+    mm_init(m);
+    for (int p = a; p < b; p++) {
+        const int f = perm[p];
+        mm_push(m, p, lo3 + 3 * f, hi3 + 3 * f);
+    }
+    // the chunk's start values carry at = -1 only if the chunk is empty; make them lose ties
+    for (int z = 0; z < 6; z++) if (m.at[z] < 0) m.at[z] = INT_MAX;
+    sm[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            MinMax x = sm[threadIdx.x];
+            mm_merge(x, sm[threadIdx.x + w]);
+            sm[threadIdx.x] = x;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        MinMax r;
+        mm_init(r);              // the fold starts from FLT_MAX / -FLT_MAX (earliest of all)
+        MinMax x = sm[0];
+        for (int z = 0; z < 6; z++) {
+            const bool take = (z < 3) ? (x.v[z] < r.v[z]) : (x.v[z] > r.v[z]);
+            if (take) r.v[z] = x.v[z];
+        }
+        for (int z = 0; z < 6; z++) box[6 * (size_t)id + z] = r.v[z];
+    }
+}
+
+__global__ void k_iota(int n, int* p) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = i;
+}
+
+template <class T>
+struct DevArr {
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t grow(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, sizeof(T) * (n + 16));
+        if (e == hipSuccess) cap = n + 16;
+        return e;
+    }
+    ~DevArr() { if (p) (void)hipFree(p); }
+};
+
+inline int nb(long long n, int b) { return (int)((n + b - 1) / b); }
+
+}  // namespace
+
+#define BVH_TRY(expr)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            err = std::string(#expr) + ": " + hipGetErrorString(e_);           \
+            return -1;                                                         \
+        }                                                                      \
+    } while (0)
+
+int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, int n, GpuBvh& out, std::string& err,
+                  hipStream_t st) {
+    out = GpuBvh();
+    if (n <= 0) { out.root = -1; return 0; }
+    DevArr<float> c3, lo3, hi3, box;
+    DevArr<int> perm, perm2, segid, less, G, ptr, lens, offs, nn, ni, nnoff, nioff, big, cnt;
+    DevArr<int4> nodes;
+    DevArr<unsigned long long> keys, sorted;
+    DevArr<Seg> segs, next;
+    DevArr<float> split;
+    DevArr<unsigned char> tmp;
+    BVH_TRY(c3.grow(3 * (size_t)n)); BVH_TRY(lo3.grow(3 * (size_t)n)); BVH_TRY(hi3.grow(3 * (size_t)n));
+    BVH_TRY(hipMemcpyAsync(c3.p, centers, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
+    BVH_TRY(hipMemcpyAsync(lo3.p, bmin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
+    BVH_TRY(hipMemcpyAsync(hi3.p, bmax, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
+    BVH_TRY(perm.grow(n)); BVH_TRY(perm2.grow(n)); BVH_TRY(segid.grow(n)); BVH_TRY(less.grow(n + 1));
+    BVH_TRY(G.grow(n + 1)); BVH_TRY(ptr.grow(n)); BVH_TRY(keys.grow(n)); BVH_TRY(sorted.grow(n));
+    BVH_TRY(big.grow(2 * (size_t)n + 64)); BVH_TRY(cnt.grow(4));
+    // per-segment arrays: a level has at most n / 2 interior segments
+    const size_t scap = (size_t)n / 2 + 2;
+    BVH_TRY(split.grow(scap)); BVH_TRY(lens.grow(scap)); BVH_TRY(offs.grow(scap)); BVH_TRY(nn.grow(scap));
+    BVH_TRY(ni.grow(scap)); BVH_TRY(nnoff.grow(scap)); BVH_TRY(nioff.grow(scap));
+    BVH_TRY(segs.grow(scap)); BVH_TRY(next.grow(scap));
+    size_t node_cap = 2 * (size_t)n + 64;
+    BVH_TRY(nodes.grow(node_cap)); BVH_TRY(box.grow(6 * node_cap));
+    hipLaunchKernelGGL(k_iota, dim3(nb(n, 256)), dim3(256), 0, st, n, perm.p);
+
+    // root: construct(0, n, 0, 0)
+    int num_nodes = 1;
+    const int4 root = make_int4(-1, -1, 0, n);
+    BVH_TRY(hipMemcpyAsync(nodes.p, &root, sizeof(int4), hipMemcpyHostToDevice, st));
+    {
+        const int rb[2] = {0, 1};     // big list {root}, count 1
+        BVH_TRY(hipMemcpyAsync(big.p, &rb[0], sizeof(int), hipMemcpyHostToDevice, st));
+        BVH_TRY(hipMemcpyAsync(cnt.p, &rb[1], sizeof(int), hipMemcpyHostToDevice, st));
+        if (n >= kBigNode) hipLaunchKernelGGL(k_box_big, dim3(1), dim3(256), 0, st, big.p, cnt.p, nodes.p, perm.p, lo3.p, hi3.p, box.p);
+        else hipLaunchKernelGGL(k_box_small, dim3(1), dim3(64), 0, st, nodes.p, 0, 1, perm.p, lo3.p, hi3.p, box.p);
+    }
+    int S = 0;
+    if (n >= 2) {
+        Seg s0; s0.start = 0; s0.end = n; s0.node = 0; s0.off = 0;
+        BVH_TRY(hipMemcpyAsync(segs.p, &s0, sizeof(Seg), hipMemcpyHostToDevice, st));
+        S = 1;
+    }
+    size_t tmp_bytes = 0;
+    auto ensure_tmp = [&](size_t need) -> hipError_t { if (need > tmp_bytes) { tmp_bytes = need; return tmp.grow(need); } return hipSuccess; };
+    for (int depth = 0; S > 0; depth++) {
+        const int axis = depth % 3;           // splitType 0,1,2,0,... (src/BVH.cpp:70-72)
+        // key offsets of the segments in the sorted array
+        hipLaunchKernelGGL(k_seg_len, dim3(nb(S, 256)), dim3(256), 0, st, segs.p, S, lens.p);
+        size_t need = 0;
+        BVH_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, need, lens.p, offs.p, S, st));
+        BVH_TRY(ensure_tmp(need));
+        BVH_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, need, lens.p, offs.p, S, st));
+        hipLaunchKernelGGL(k_seg_off, dim3(nb(S, 256)), dim3(256), 0, st, segs.p, S, offs.p);
+        // order statistics: sort (segment, centre) keys
+        hipLaunchKernelGGL(k_segid, dim3(nb(n, 256)), dim3(256), 0, st, n, segs.p, S, segid.p);
+        hipLaunchKernelGGL(k_keys, dim3(nb(n, 256)), dim3(256), 0, st, n, axis, segid.p, S, perm.p, c3.p, keys.p);
+        const int sbits = 32 - __builtin_clz((unsigned)S);      // S itself (the sentinel) must fit
+        need = 0;
+        BVH_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, need, keys.p, sorted.p, n, 0, 32 + sbits, st));
+        BVH_TRY(ensure_tmp(need));
+        BVH_TRY(hipcub::DeviceRadixSort::SortKeys(tmp.p, need, keys.p, sorted.p, n, 0, 32 + sbits, st));
+        hipLaunchKernelGGL(k_split, dim3(nb(S, 256)), dim3(256), 0, st, segs.p, S, sorted.p, split.p);
+        // partition
+        hipLaunchKernelGGL(k_less, dim3(nb(n + 1, 256)), dim3(256), 0, st, n, axis, segid.p, S, perm.p, c3.p, split.p, less.p);
+        need = 0;
+        BVH_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, need, less.p, G.p, n + 1, st));
+        BVH_TRY(ensure_tmp(need));
+        BVH_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, need, less.p, G.p, n + 1, st));
+        hipLaunchKernelGGL(k_ptr_init, dim3(nb(n, 256)), dim3(256), 0, st, n, segid.p, S, segs.p, G.p, less.p, ptr.p);
+        hipLaunchKernelGGL(k_jump, dim3(nb(n, 256)), dim3(256), 0, st, n, ptr.p);
+        hipLaunchKernelGGL(k_scatter, dim3(nb(n, 256)), dim3(256), 0, st, n, segid.p, S, segs.p, G.p, less.p, ptr.p,
+                           perm.p, perm2.p);
+        std::swap(perm.p, perm2.p);
+        std::swap(perm.cap, perm2.cap);
+        // children
+        hipLaunchKernelGGL(k_child_count, dim3(nb(S + 1, 256)), dim3(256), 0, st, segs.p, S, depth + 1, G.p, nn.p, ni.p);
+        need = 0;
+        BVH_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, need, nn.p, nnoff.p, S + 1, st));
+        BVH_TRY(ensure_tmp(need));
+        BVH_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, need, nn.p, nnoff.p, S + 1, st));
+        BVH_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, need, ni.p, nioff.p, S + 1, st));
+        int tot[2] = {0, 0};
+        BVH_TRY(hipMemcpyAsync(&tot[0], nnoff.p + S, sizeof(int), hipMemcpyDeviceToHost, st));
+        BVH_TRY(hipMemcpyAsync(&tot[1], nioff.p + S, sizeof(int), hipMemcpyDeviceToHost, st));
+        BVH_TRY(hipStreamSynchronize(st));
+        const int new_nodes = tot[0], S_next = tot[1];
+        if ((size_t)(num_nodes + new_nodes) > node_cap) {       // grow the node arrays, keeping contents
+            size_t cap2 = std::max(node_cap * 2, (size_t)(num_nodes + new_nodes) + 64);
+            int4* n2 = nullptr; float* b2 = nullptr;
+            BVH_TRY(hipMalloc(&n2, sizeof(int4) * cap2));
+            BVH_TRY(hipMalloc(&b2, sizeof(float) * 6 * cap2));
+            BVH_TRY(hipMemcpyAsync(n2, nodes.p, sizeof(int4) * num_nodes, hipMemcpyDeviceToDevice, st));
+            BVH_TRY(hipMemcpyAsync(b2, box.p, sizeof(float) * 6 * num_nodes, hipMemcpyDeviceToDevice, st));
+            BVH_TRY(hipStreamSynchronize(st));
+            (void)hipFree(nodes.p); (void)hipFree(box.p);
+            nodes.p = n2; nodes.cap = cap2; box.p = b2; box.cap = 6 * cap2;
+            node_cap = cap2;
+            BVH_TRY(big.grow(cap2));
+        }
+        int zero = 0;
+        BVH_TRY(hipMemcpyAsync(cnt.p, &zero, sizeof(int), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_child_emit, dim3(nb(S, 256)), dim3(256), 0, st, segs.p, S, depth + 1, G.p, nnoff.p, nioff.p,
+                           num_nodes, nodes.p, next.p, big.p, cnt.p);
+        // boxes of the new nodes over their ranges in the partitioned order (big ones: one block
+        // each; their count is bounded by n / kBigNode, the exact count stays on the device)
+        if (new_nodes > 0) {
+            hipLaunchKernelGGL(k_box_small, dim3(nb(new_nodes, 256)), dim3(256), 0, st, nodes.p, num_nodes, new_nodes,
+                               perm.p, lo3.p, hi3.p, box.p);
+            const int max_big = std::min(new_nodes, n / kBigNode + 2);
+            if (n >= kBigNode)
+                hipLaunchKernelGGL(k_box_big, dim3(max_big), dim3(256), 0, st, big.p, cnt.p, nodes.p, perm.p, lo3.p, hi3.p,
+                                   box.p);
+        }
+        BVH_TRY(hipGetLastError());
+        num_nodes += new_nodes;
+        std::swap(segs.p, next.p);
+        std::swap(segs.cap, next.cap);
+        S = S_next;
+    }
+    out.perm.resize(n);
+    out.nodes.resize(num_nodes);
+    out.box.resize(6 * (size_t)num_nodes);
+    BVH_TRY(hipMemcpyAsync(out.perm.data(), perm.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+    BVH_TRY(hipMemcpyAsync(out.nodes.data(), nodes.p, sizeof(int4) * num_nodes, hipMemcpyDeviceToHost, st));
+    BVH_TRY(hipMemcpyAsync(out.box.data(), box.p, sizeof(float) * 6 * num_nodes, hipMemcpyDeviceToHost, st));
+    BVH_TRY(hipStreamSynchronize(st));
+    out.root = 0;
+    return 0;
+}
+
+}  // namespace rtg

@@ -8,10 +8,13 @@
 // rtg_render() drives the per-level kernels of rtg_device.hip.
 #include <float.h>
 #include <math.h>
+#include <cmath>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <string>
 #include <deque>
@@ -340,7 +343,7 @@ struct DBuf {
     size_t bytes = 0;
     int grow(size_t need) {
         if (need <= bytes) return RTG_OK;
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr; bytes = 0;
         size_t want = need + need / 4 + 256;
         if (hipMalloc(&p, want) != hipSuccess) {
@@ -351,7 +354,7 @@ struct DBuf {
         return RTG_OK;
     }
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
-    void release() { if (p) hipFree(p); p = nullptr; bytes = 0; }
+    void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
 };
 
 template <class T>
@@ -420,6 +423,9 @@ struct rtg_scene {
     DBuf d_acc, d_counters, d_stats;
     rtg_render_stats stats{};
     int num_lanes = 3;                       // default passes in flight (env RTG_STREAMS overrides)
+    int bvh_builder = RTG_BVH_AUTO;
+    double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
+    int bvh_gpu_objects = 0;                 // objects whose BVH the GPU built
 };
 
 extern "C" {
@@ -595,8 +601,53 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         ob.perm.resize(np);
         for (int k = 0; k < np; k++) ob.perm[k] = k;
         BuildCtx B{centers.data(), bmin.data(), bmax.data(), &ob.perm, &ob.nodes, {}};
-        ob.nodes.reserve(2 * (size_t)np + 1);
-        ob.root = construct(B, 0, np, 0, 0);
+        auto tb0 = std::chrono::steady_clock::now();
+        bool use_gpu = s->device >= 0 && o.type != RTG_OBJ_SPHERE &&
+                       (s->bvh_builder == RTG_BVH_GPU || (s->bvh_builder == RTG_BVH_AUTO && np >= 4096));
+        if (use_gpu) {     // non-finite centres / boxes: the GPU build does not model NaN folds
+            for (int k = 0; k < np && use_gpu; k++)
+                use_gpu = std::isfinite(centers[k].x) && std::isfinite(centers[k].y) && std::isfinite(centers[k].z) &&
+                          std::isfinite(bmin[k].x) && std::isfinite(bmin[k].y) && std::isfinite(bmin[k].z) &&
+                          std::isfinite(bmax[k].x) && std::isfinite(bmax[k].y) && std::isfinite(bmax[k].z);
+        }
+        if (use_gpu) {
+            GpuBvh gb;
+            std::string err;
+            if (gpu_build_bvh(&centers[0].x, &bmin[0].x, &bmax[0].x, np, gb, err, nullptr))
+                return fail(RTG_ERR_HIP, "GPU BVH build: " + err);
+            ob.perm = std::move(gb.perm);
+            // breadth-first -> the reference's pre-order numbering (node, left subtree, right subtree)
+            const int nn = (int)gb.nodes.size();
+            std::vector<int> pre(nn, -1), stk;
+            ob.nodes.clear();
+            ob.nodes.reserve(nn);
+            if (nn > 0) stk.push_back(0);
+            while (!stk.empty()) {
+                const int id = stk.back();
+                stk.pop_back();
+                pre[id] = (int)ob.nodes.size();
+                HNode h;
+                h.left = gb.nodes[id].x; h.right = gb.nodes[id].y;     // fixed below
+                h.start = gb.nodes[id].z; h.end = gb.nodes[id].w;
+                for (int z = 0; z < 3; z++) { h.mn[z] = gb.box[6 * (size_t)id + z]; h.mx[z] = gb.box[6 * (size_t)id + 3 + z]; }
+                ob.nodes.push_back(h);
+                if (gb.nodes[id].y >= 0) stk.push_back(gb.nodes[id].y);
+                if (gb.nodes[id].x >= 0) stk.push_back(gb.nodes[id].x);
+            }
+            for (HNode& h : ob.nodes) {
+                if (h.left >= 0) h.left = pre[h.left];
+                if (h.right >= 0) h.right = pre[h.right];
+            }
+            ob.root = nn > 0 ? 0 : -1;
+            s->bvh_gpu_objects++;
+        } else {
+            ob.nodes.reserve(2 * (size_t)np + 1);
+            ob.root = construct(B, 0, np, 0, 0);
+        }
+        const double bms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
+        s->bvh_build_ms += bms;
+        if (getenv("RTG_BUILD_TIMING"))
+            fprintf(stderr, "[rtg] object %d: %d prims, BVH %s %.1f ms\n", i, np, use_gpu ? "gpu" : "host", bms);
 
         Geometry& g = geoms[i];
         memset(&g, 0, sizeof g);
@@ -837,7 +888,13 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
 }
 
 int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene** out) {
+    return rtg_scene_create_ex(desc, device, nullptr, out);
+}
+
+int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rtg_build_opts* opts, rtg_scene** out) {
     if (!out) return fail(RTG_ERR_INVALID, "null out pointer");
+    if (opts && (opts->bvh_builder < RTG_BVH_AUTO || opts->bvh_builder > RTG_BVH_GPU))
+        return fail(RTG_ERR_INVALID, "bvh_builder");
     *out = nullptr;
     int rc = validate(desc);
     if (rc) return rc;
@@ -853,6 +910,7 @@ int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene**
     if (!s) return fail(RTG_ERR_OOM, "host allocation");
     s->device = device;
     if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
+    s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
     rc = build_scene(s, desc);
     if (rc) {
         scene_free(s);
@@ -1127,8 +1185,16 @@ int32_t rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_op
         hipError_t e = hipMemcpy(rgb_out, d_out, bytes, hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = fail(RTG_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
     }
-    hipFree(d_out);
+    (void)hipFree(d_out);
     return rc;
+}
+
+int32_t rtg_scene_build_stats(const rtg_scene* s, rtg_build_stats* out) {
+    if (!s || !out) return fail(RTG_ERR_INVALID, "null argument");
+    out->bvh_build_ms = s->bvh_build_ms;
+    out->bvh_gpu_objects = s->bvh_gpu_objects;
+    out->num_objects = s->num_objects;
+    return RTG_OK;
 }
 
 int32_t rtg_last_render_stats(const rtg_scene* s, rtg_render_stats* out) {

@@ -4,6 +4,9 @@
 #pragma once
 #include <stdint.h>
 
+#include <string>
+#include <vector>
+
 #include <hip/hip_runtime.h>
 
 #include "../../include/rtg.h"
@@ -221,5 +224,17 @@ void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offse
                      hipStream_t st);
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st);
+
+// GPU BVH construction (rtg_bvh_gpu.hip): the reference median-split tree of one object.
+// nodes: breadth-first {left, right, start, end} (children -1: none); box: 6 floats per node
+// (min xyz, max xyz); perm: BVH position -> original primitive.  Inputs must be finite.
+struct GpuBvh {
+    std::vector<int> perm;
+    std::vector<int4> nodes;
+    std::vector<float> box;
+    int root = -1;
+};
+int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, int n, GpuBvh& out, std::string& err,
+                  hipStream_t st);
 
 }  // namespace rtg

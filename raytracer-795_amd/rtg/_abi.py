@@ -118,6 +118,17 @@ class Ray(C.Structure):
     _fields_ = [("origin", F3), ("direction", F3), ("time", C.c_float)]
 
 
+class BuildOpts(C.Structure):
+    _fields_ = [("bvh_builder", C.c_int32)]
+
+
+class BuildStats(C.Structure):
+    _fields_ = [("bvh_build_ms", C.c_double), ("bvh_gpu_objects", C.c_int32), ("num_objects", C.c_int32)]
+
+
+RTG_BVH_AUTO, RTG_BVH_HOST, RTG_BVH_GPU = 0, 1, 2
+
+
 class Hit(C.Structure):
     _fields_ = [("full", C.c_int32), ("object", C.c_int32), ("prim", C.c_int32), ("material", C.c_int32),
                 ("t", C.c_float), ("point", F3), ("normal", F3)]
@@ -129,6 +140,9 @@ EXPORTS = {
     "rtg_last_error": (C.c_char_p, []),
     "rtg_device_count": (C.c_int32, []),
     "rtg_scene_create": (C.c_int32, [C.POINTER(SceneDesc), C.c_int32, C.POINTER(C.c_void_p)]),
+    "rtg_scene_create_ex": (C.c_int32, [C.POINTER(SceneDesc), C.c_int32, C.POINTER(BuildOpts),
+                                         C.POINTER(C.c_void_p)]),
+    "rtg_scene_build_stats": (C.c_int32, [C.c_void_p, C.POINTER(BuildStats)]),
     "rtg_scene_destroy": (C.c_int32, [C.c_void_p]),
     "rtg_render": (C.c_int32, [C.c_void_p, C.POINTER(CameraDesc), C.POINTER(RenderOpts), PF]),
     "rtg_render_device": (C.c_int32, [C.c_void_p, C.POINTER(CameraDesc), C.POINTER(RenderOpts), C.c_void_p,

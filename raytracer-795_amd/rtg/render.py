@@ -24,12 +24,13 @@ DEFAULT_SEED = 0x5EED2026
 
 
 class Renderer:
-    def __init__(self, scene: Scene, device: int = 0):
+    def __init__(self, scene: Scene, device: int = 0, bvh_builder: int = A.RTG_BVH_AUTO):
         self.lib = A.load_library()
         self.scene = scene
         desc, self._keep = scene.to_desc()
         h = C.c_void_p()
-        A.check(self.lib.rtg_scene_create(C.byref(desc), int(device), C.byref(h)), self.lib)
+        bo = A.BuildOpts(bvh_builder)
+        A.check(self.lib.rtg_scene_create_ex(C.byref(desc), int(device), C.byref(bo), C.byref(h)), self.lib)
         self.handle = h
         self.device = device
 
@@ -95,6 +96,11 @@ class Renderer:
         hits = (A.Hit * max(n, 1))()
         A.check(self.lib.rtg_trace_closest(self.handle, rays, n, hits, traversal), self.lib)
         return hits_to_dict(hits, n)
+
+    def build_stats(self) -> dict:
+        b = A.BuildStats()
+        A.check(self.lib.rtg_scene_build_stats(self.handle, C.byref(b)), self.lib)
+        return {"bvh_build_ms": b.bvh_build_ms, "bvh_gpu_objects": b.bvh_gpu_objects, "num_objects": b.num_objects}
 
     def bvh(self, obj: int):
         return _bvh(self.lib.rtg_scene_object_bvh, self.handle, obj)

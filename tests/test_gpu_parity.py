@@ -122,8 +122,22 @@ def test_render_is_deterministic(gpu):
         a = r.render(0)
         b = r.render(0)
         c = r.render(0, max_batch_rays=1000)          # different pass batching, same sample order
+        others = [r.render(0, max_batch_rays=1000, streams=k) for k in (1, 2, 8)]   # passes in flight
     assert np.array_equal(a.view(np.int32), b.view(np.int32))
     assert np.array_equal(a.view(np.int32), c.view(np.int32))
+    for x in others:
+        assert np.array_equal(a.view(np.int32), x.view(np.int32))
+
+
+def test_sample_chunks_accumulate_in_order(gpu):
+    """spp above the ray batch: sample chunks of one pixel range run as successive passes on
+    one stream, so MultiSample's in-order sum (src/Scene.cpp:519-540) is kept bit for bit."""
+    sc = scenegen.cornell(24, 18, spp=8)
+    with rtg.Renderer(sc, device=gpu) as r:
+        a = r.render(0)
+        for k in (1, 3):
+            b = r.render(0, max_batch_rays=3, streams=k)   # ns_chunk = 3: chunks 0-2, 3-5, 6-7
+            assert np.array_equal(a.view(np.int32), b.view(np.int32))
 
 
 def test_ray_counts_match_oracle(gpu):
