@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 1
+#define RTG_ABI_VERSION 2
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -104,6 +104,12 @@ typedef struct rtg_object_desc {
     int32_t face_first;      /* range in rtg_scene_desc.faces (triples of 1-based vertex indices,
                                 vertexOffset already added: src/Parser.h:1112-1139) */
     int32_t face_count;
+    /* object light (hw7 <LightSphere> / <LightMesh>, pages/Page7.md:7-13; no reference code):
+       is_light = 1 makes the object an emitter of `radiance` from both sides.  Only the path
+       tracer (rtg_camera_desc.integrator) treats it as a light; the reference integrator
+       shades it like any other object. */
+    int32_t is_light;
+    float radiance[3];
 } rtg_object_desc;
 
 typedef struct rtg_instance_desc {
@@ -194,7 +200,21 @@ typedef struct rtg_camera_desc {     /* src/Camera.h:351-399; FovY/GazePoint alr
     float focus_distance;
     float aperture_size;
     int32_t left_handed;
+    /* hw7 <Renderer> / <RendererParams> (pages/Page7.md:15-33, 41-45; no reference code) */
+    int32_t integrator;              /* rtg_integrator */
+    int32_t pt_flags;                /* rtg_pt_flags (path tracing only) */
 } rtg_camera_desc;
+
+typedef enum rtg_integrator {
+    RTG_INTEGRATOR_REFERENCE = 0,    /* Scene::RecursiveShading (Whitted / distribution ray tracing) */
+    RTG_INTEGRATOR_PATH = 1          /* hw7 path tracer */
+} rtg_integrator;
+typedef enum rtg_pt_flags {
+    RTG_PT_IMPORTANCE = 1,           /* cosine-weighted hemisphere sampling (else uniform) */
+    RTG_PT_NEE = 2,                  /* next event estimation towards object lights */
+    RTG_PT_RUSSIAN_ROULETTE = 4      /* cosine-based termination, no MaxRecursionDepth cap */
+} rtg_pt_flags;
+#define RTG_PT_MAX_BOUNCES 32        /* hard cap on path length with Russian roulette */
 
 typedef struct rtg_render_opts {
     uint64_t seed;           /* Philox key for all stochastic draws (reference: random_device) */

@@ -244,7 +244,7 @@ static mat4 m_inverse_transpose(const mat4* M) {
 }
 
 /* ------------------------------------------------------------------ Philox RNG */
-enum { RNG_CAMERA = 1, RNG_ROUGH = 2, RNG_AREA = 3, RNG_ENV = 4 };
+enum { RNG_CAMERA = 1, RNG_ROUGH = 2, RNG_AREA = 3, RNG_ENV = 4, RNG_PT_BOUNCE = 5, RNG_PT_EMIT = 6 };
 
 static inline void philox_round(uint32_t c[4], const uint32_t k[2]) {
     uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
@@ -355,8 +355,20 @@ struct orc_scene {
     int nmat; rtg_material_desc* mats;
     int ntex; Tex* texs;
     int nlight; Lgt* lights;
+    /* hw7 object lights (path tracer only): emitters in object order */
+    int nemit; struct Emit* emits;
+    v3* etris;                /* world-space triangles of mesh emitters, 3 vertices each */
+    float* ecdf;              /* running float sum of their areas, per emitter range */
     uint64_t counts[3];
 };
+typedef struct Emit {
+    int obj;                  /* object index */
+    int sphere;
+    v3 Le;
+    float area;               /* mesh: total world area (last cdf entry) */
+    int tri_first, tri_count;
+    v3 center; float radius;  /* sphere: world centre, radius * |model column 0| */
+} Emit;
 
 /* per-thread render context */
 typedef struct {
@@ -1211,6 +1223,196 @@ static v3 background(const struct orc_scene* s, int row, int col, int nx, int ny
     return tex_color(&s->texs[s->bgTexture], u, v);
 }
 
+/* ------------------------------------------------------------------ hw7 path tracer
+ * No reference code exists (pages/Page7.md describes it in prose only).
+ * This is the integrator DESIGN.md §8 specifies; librtg.so's wavefront must match it bit
+ * for bit.  Per sample: throughput T, radiance L; at each vertex L += T (x) v where v is
+ *   - the emitter radiance on an object-light hit (counted at the camera vertex, without
+ *     NEE, or after a specular bounce — Page7.md:135-141), which ends the path;
+ *   - else Scene::BasicShading (ambient + every light in order, shadowed) plus, with NEE,
+ *     one sample of every object light (Page7.md:143-147 distance-checked shadow test);
+ * then the path continues by one sampled direction (diffuse: uniform / cosine hemisphere,
+ * mirror / conductor: reflection, dielectric: reflect or refract chosen by Fresnel).
+ * Russian roulette continues with probability |n . w_next| (Page7.md:41-45) and lifts the
+ * MaxRecursionDepth cap (RTG_PT_MAX_BOUNCES bounds the path instead). */
+static int is_emitter(const struct orc_scene* s, const RetVal* r, const Emit** out) {
+    if (r->obj < 0 || r->obj >= s->nobj) return 0;
+    for (int k = 0; k < s->nemit; k++)
+        if (s->emits[k].obj == r->obj) { *out = &s->emits[k]; return 1; }
+    return 0;
+}
+
+/* light response used everywhere: the material's BRDF (Light::BRDF) or the reference's
+   non-BRDF Blinn-Phong diffuse + specular terms, for incident radiance LC */
+static v3 surface_response(v3 LC, v3 wo, v3 wi, const RetVal* ret, const rtg_material_desc* m) {
+    if (m->brdf != RTG_BRDF_NONE) return brdf(wi, wo, ret, LC, m);
+    float alpha = fmax0(vdot(ret->normal, wi));
+    return vadd(diffuse_term(LC, ret, m, alpha), specular_term(LC, wo, wi, ret, m));
+}
+
+/* NEE: one sample of emitter k (light slot nlight + k) */
+static v3 emitter_shading(Ctx* cx, int k, const Ray* prime, const RetVal* ret, const rtg_material_desc* m,
+                          uint64_t path) {
+    struct orc_scene* s = cx->s;
+    const Emit* E = &s->emits[k];
+    const uint32_t li = (uint32_t)(s->nlight + k);
+    float xi[4];
+    rng4(cx->rng.seed, cx->rng.pixel, cx->rng.sample, path, RNG_PT_EMIT, li, 0, xi);
+    v3 p = ret->point, wo = vneg(prime->direction);
+    v3 q, wi, LC;
+    float dist;
+    if (E->sphere) {
+        /* uniform in the cone the sphere subtends; from inside, uniform over all directions */
+        v3 dv = vsub(E->center, p);
+        float dd = vnorm(dv);
+        int inside = !(dd > E->radius);
+        float cosmax = -1.0f;
+        if (!inside) {
+            float sin2 = (E->radius * E->radius) / (dd * dd);
+            cosmax = sqrtf(fmax0(1.0f - sin2));
+        }
+        float cosT = 1.0f - xi[0] * (1.0f - cosmax);
+        float sinT = sqrtf(fmax0(1.0f - cosT * cosT));
+        float phi = (float)(2 * PI_D) * xi[1];
+        v3 dn = dd > 0.0f ? vdivs(dv, dd) : V(0, 1, 0);
+        v3 u = ortho_u(dn), w = vcross(dn, u);
+        wi = vnormalized(vadd(vadd(vmul(u, sinT * f_cos(phi)), vmul(w, sinT * f_sin(phi))), vmul(dn, cosT)));
+        v3 oc = vsub(p, E->center);
+        float b = vdot(wi, oc);
+        float disc = b * b - (vsqn(oc) - E->radius * E->radius);
+        float t = inside ? -b + sqrtf(fmax0(disc)) : -b - sqrtf(fmax0(disc));
+        q = vadd(p, vmul(wi, t));
+        dist = vnorm(vsub(p, q));
+        LC = vmul(E->Le, (float)(2 * PI_D) * (1.0f - cosmax));
+    } else {
+        const float* cdf = s->ecdf + E->tri_first;
+        float target = xi[0] * E->area;
+        int lo = 0, hi = E->tri_count - 1;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (target < cdf[mid]) hi = mid; else lo = mid + 1;
+        }
+        const v3* T = s->etris + 3 * (size_t)(E->tri_first + lo);
+        float sq = sqrtf(xi[1]);
+        q = vadd(vadd(vmul(T[0], 1.0f - sq), vmul(T[1], sq * (1.0f - xi[2]))), vmul(T[2], sq * xi[2]));
+        v3 nl = vnormalized(vcross(vsub(T[1], T[0]), vsub(T[2], T[0])));
+        v3 dv = vsub(q, p);
+        dist = vnorm(dv);
+        wi = vdivs(dv, dist);
+        float cosl = fabsf(vdot(wi, nl));
+        LC = vmul(E->Le, (cosl * E->area) / (dist * dist));
+    }
+    Ray ray = R(vadd(p, vmul(ret->normal, s->shadowEps)), wi, prime->time);
+    RetVal nr = trace(cx, &ray, 2);
+    if (nr.full && vnorm(vsub(p, nr.point)) < dist - (s->shadowEps + 1e-4f * dist)) return V(0, 0, 0);
+    return surface_response(LC, wo, wi, ret, m);
+}
+
+static v3 pt_sample(Ctx* cx, Ray ray, int flags, v3 bg) {
+    struct orc_scene* s = cx->s;
+    v3 L = V(0, 0, 0), T = V(1, 1, 1);
+    int spec = 1, medium = 0, depth = s->maxDepth;
+    for (int b = 0;; b++) {
+        const uint64_t path = (uint64_t)b + 1;
+        RetVal ret = trace(cx, &ray, b == 0 ? 0 : 1);
+        if (!ret.full) {
+            if (b == 0) L = vadd(L, vcw(T, bg));
+            break;
+        }
+        if (medium) {                                   /* Beer's law over the segment inside */
+            v3 sig = mv(MAT(s, medium)->absorption_coeff);
+            float bd = vnorm(vsub(ret.point, ray.origin));
+            T = vcw(T, V(f_exp(-sig.x * bd), f_exp(-sig.y * bd), f_exp(-sig.z * bd)));
+        }
+        const Emit* E;
+        if (is_emitter(s, &ret, &E)) {
+            if (b == 0 || !(flags & RTG_PT_NEE) || spec) L = vadd(L, vcw(T, E->Le));
+            break;
+        }
+        if (b == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) { L = vadd(L, vcw(T, ret.textureColor)); break; }
+        const rtg_material_desc* m = MAT(s, ret.matIndex);
+        /* dielectric geometry (Scene::DielectricRefraction :188-249) */
+        int entering = 1, isTir = 0;
+        float F = 0.0f;
+        v3 tdir = V(0, 0, 0), torg = V(0, 0, 0);
+        if (m->type == RTG_MAT_DIELECTRIC) {
+            float dp = vdot(ray.direction, ret.normal);
+            float nt = m->refraction_index;
+            float snell, n_t, n_i;
+            v3 normal;
+            if (dp < 0) { snell = 1.0f / nt; normal = ret.normal; n_t = nt; n_i = 1; entering = 1; }
+            else { snell = nt; normal = vneg(ret.normal); n_t = 1; n_i = nt; entering = 0; }
+            float cosTheta = -vdot(ray.direction, normal);
+            v3 leftPart = vmul(vadd(ray.direction, vmul(normal, cosTheta)), snell);
+            float srp = (float)(1 - pow((double)snell, 2) * (1 - pow((double)cosTheta, 2)));
+            isTir = srp < 0;
+            srp = sqrtf(srp);
+            tdir = vnormalized(vsub(leftPart, vmul(normal, srp)));
+            torg = vsub(ret.point, vmul(normal, s->shadowEps));
+            float cos_t = -vdot(tdir, normal);
+            float cos_i = -vdot(ray.direction, normal);
+            float rPar = (n_t * cos_i - n_i * cos_t) / (n_t * cos_i + n_i * cos_t);
+            float rPer = (n_i * cos_i - n_t * cos_t) / (n_i * cos_i + n_t * cos_t);
+            F = (float)(0.5f * (pow((double)rPar, 2) + pow((double)rPer, 2)));
+        }
+        if (entering) {
+            v3 v = basic_shading(cx, &ray, &ret, m, path);
+            if (flags & RTG_PT_NEE)
+                for (int k = 0; k < s->nemit; k++) v = vadd(v, emitter_shading(cx, k, &ray, &ret, m, path));
+            L = vadd(L, vcw(T, v));
+        }
+        int cont = (flags & RTG_PT_RUSSIAN_ROULETTE) ? (b + 1 < RTG_PT_MAX_BOUNCES) : (depth > 0);
+        if (!cont) break;
+        float xi[4];
+        rng4(cx->rng.seed, cx->rng.pixel, cx->rng.sample, path, RNG_PT_BOUNCE, 0, 0, xi);
+        v3 w = V(1, 1, 1);
+        Ray next;
+        int nspec = 1, nmedium = medium;
+        if (m->type == RTG_MAT_NORMAL) {
+            v3 n = ret.normal, u = ortho_u(n), bt = vcross(n, u);
+            float phi = (float)(2 * PI_D) * xi[0];
+            float cosT = (flags & RTG_PT_IMPORTANCE) ? sqrtf(1.0f - xi[1]) : xi[1];
+            float sinT = sqrtf(fmax0(1.0f - cosT * cosT));
+            v3 wi = vnormalized(vadd(vadd(vmul(u, sinT * f_cos(phi)), vmul(n, cosT)), vmul(bt, sinT * f_sin(phi))));
+            v3 fc = surface_response(V(1, 1, 1), vneg(ray.direction), wi, &ret, m);
+            if (flags & RTG_PT_IMPORTANCE) w = cosT > 0.0f ? vmul(fc, (float)PI_D / cosT) : V(0, 0, 0);
+            else w = vmul(fc, (float)(2 * PI_D));
+            next = R(vadd(ret.point, vmul(n, s->shadowEps)), wi, ray.time);
+            nspec = 0;
+        } else if (m->type == RTG_MAT_DIELECTRIC && !isTir && !(xi[3] < F)) {
+            next = R(torg, tdir, ray.time);
+            nmedium = entering ? ret.matIndex : 0;
+        } else {
+            /* mirror / conductor / dielectric reflection: Scene::MirrorReflectance :163-186 */
+            v3 wo = vneg(ray.direction);
+            float n_wo = vdot(ret.normal, wo);
+            v3 wr = vadd(vneg(wo), vmul(vmul(ret.normal, 2), n_wo));
+            wr = vdivs(wr, vnorm(wr));
+            if (m->is_rough) {
+                v3 u = ortho_u(wr), v = vcross(wr, u);
+                float xr[4];
+                rng4(cx->rng.seed, cx->rng.pixel, cx->rng.sample, path, RNG_ROUGH, 0, 0, xr);
+                float uChi = xr[0] - 0.5f, vChi = xr[1] - 0.5f;
+                wr = vnormalized(vadd(wr, vmul(vadd(vmul(u, uChi), vmul(v, vChi)), m->roughness)));
+            }
+            next = R(vadd(ret.point, vmul(ret.normal, s->shadowEps)), wr, ray.time);
+            if (m->type == RTG_MAT_MIRROR) w = mv(m->mirror);
+            else if (m->type == RTG_MAT_CONDUCTOR)
+                w = vmul(mv(m->mirror), conductor_fresnel(m->refraction_index, m->absorption_index, ray.direction, ret.normal));
+        }
+        if (visnan(next.origin) || visnan(next.direction)) break;
+        if (flags & RTG_PT_RUSSIAN_ROULETTE) {
+            float qc = fabsf(vdot(ret.normal, next.direction));
+            if (!(xi[2] < qc)) break;
+            w = vdivs(w, qc);
+        }
+        T = vcw(T, w);
+        if (T.x == 0.0f && T.y == 0.0f && T.z == 0.0f) break;
+        ray = next; spec = nspec; medium = nmedium; depth--;
+    }
+    return L;
+}
+
 /* ------------------------------------------------------------------ camera (src/Camera.cpp) */
 typedef struct {
     v3 pos, gaze, up, right;
@@ -1310,6 +1512,7 @@ void orc_scene_destroy(orc_scene* s) {
     free(s->mats);
     for (int i = 0; i < s->ntex; i++) free(s->texs[i].texels);
     free(s->texs); free(s->lights);
+    free(s->emits); free(s->etris); free(s->ecdf);
     free(s);
 }
 
@@ -1401,6 +1604,44 @@ int orc_scene_create(const rtg_scene_desc* d, orc_scene** out) {
         in->inv = m_inverse(&in->model);
         in->invT = m_inverse_transpose(&in->model);
     }
+    /* hw7 object lights (no reference code): world-space emitter geometry,
+       sampled at time 0 (motion blur of emitters is ignored by the light sampler) */
+    {
+        int ntri = 0;
+        for (int i = 0; i < s->nobj; i++)
+            if (d->objects[i].is_light) { s->nemit++; if (d->objects[i].type != RTG_OBJ_SPHERE) ntri += s->objs[i].nprims; }
+        s->emits = (Emit*)calloc(s->nemit ? s->nemit : 1, sizeof(Emit));
+        s->etris = (v3*)malloc(sizeof(v3) * 3 * (size_t)(ntri ? ntri : 1));
+        s->ecdf = (float*)malloc(sizeof(float) * (size_t)(ntri ? ntri : 1));
+        int e = 0, t = 0;
+        for (int i = 0; i < s->nobj; i++) {
+            const rtg_object_desc* od = &d->objects[i];
+            if (!od->is_light) continue;
+            Obj* o = &s->objs[i];
+            Emit* E = &s->emits[e++];
+            E->obj = i;
+            E->Le = mv(od->radiance);
+            E->sphere = od->type == RTG_OBJ_SPHERE;
+            if (E->sphere) {
+                E->center = m_xform(&o->model, s->vertices[od->center - 1], 1.0f);
+                E->radius = od->radius * vnorm(V(o->model.c[0][0], o->model.c[0][1], o->model.c[0][2]));
+                continue;
+            }
+            E->tri_first = t;
+            E->tri_count = o->nprims;
+            float acc = 0.0f;
+            for (int k = 0; k < o->nprims; k++, t++) {      /* original (parse) face order */
+                const int* vi = o->pv + 3 * k;
+                v3 a = m_xform(&o->model, s->vertices[vi[0] - 1], 1.0f);
+                v3 b = m_xform(&o->model, s->vertices[vi[1] - 1], 1.0f);
+                v3 c = m_xform(&o->model, s->vertices[vi[2] - 1], 1.0f);
+                s->etris[3 * t] = a; s->etris[3 * t + 1] = b; s->etris[3 * t + 2] = c;
+                acc = acc + 0.5f * vnorm(vcross(vsub(b, a), vsub(c, a)));
+                s->ecdf[t] = acc;
+            }
+            E->area = acc;
+        }
+    }
     /* smooth vertex normals, src/Scene.cpp:433-449, Shape.cpp:378-406 */
     s->vnormals = (v3*)calloc(s->nv ? s->nv : 1, sizeof(v3));
     for (int i = 0; i < s->nobj; i++) {
@@ -1451,6 +1692,8 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
     if (row_end <= 0 || row_end > ny) row_end = ny;
     if (row_begin < 0) row_begin = 0;
     uint64_t np = 0, nsec = 0, nsh = 0;
+    const int pathT = cd->integrator == RTG_INTEGRATOR_PATH;
+    if (pathT && pobj) for (int k = 0; k < nx * ny; k++) { pobj[k] = -1; pprim[k] = -1; pt[k] = 0; }
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
@@ -1470,6 +1713,10 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
                     float xi[4];
                     rng4(seed, pixel, (uint32_t)i, 1, RNG_CAMERA, 0, 0, xi);
                     Ray r = cam_sample(&cam, lb, i, xi);
+                    if (pathT) {
+                        color = vadd(color, pt_sample(&cx, r, cd->pt_flags, background(s, y, x, nx, ny, &r)));
+                        continue;
+                    }
                     RetVal nr = trace(&cx, &r, 0);
                     if (i == 0 && pobj) { pobj[pixel] = nr.full ? nr.obj : -1; pprim[pixel] = nr.full ? nr.prim : -1; pt[pixel] = nr.full ? nr.t : 0; }
                     if (nr.full) color = vadd(color, shading(&cx, &r, &nr));
@@ -1479,6 +1726,12 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
             } else {                                      /* Scene::SingleSample :496-515 (row=x, col=y) */
                 cx.rng.sample = 0;
                 Ray r = cam_primary(&cam, x, y);
+                if (pathT) {
+                    color = pt_sample(&cx, r, cd->pt_flags, background(s, x, y, nx, ny, &r));
+                    float* o = rgb + (size_t)pixel * 3;
+                    o[0] = color.x; o[1] = color.y; o[2] = color.z;
+                    continue;
+                }
                 RetVal nr = trace(&cx, &r, 0);
                 if (pobj) { pobj[pixel] = nr.full ? nr.obj : -1; pprim[pixel] = nr.full ? nr.prim : -1; pt[pixel] = nr.full ? nr.t : 0; }
                 if (nr.full) color = shading(&cx, &r, &nr);

@@ -94,7 +94,7 @@ DEV f3 xform(const float* m, f3 v, float w) {
 }
 
 // ------------------------------------------------------------------ Philox4x32-10
-enum { RNG_CAMERA = 1, RNG_ROUGH = 2, RNG_AREA = 3, RNG_ENV = 4 };
+enum { RNG_CAMERA = 1, RNG_ROUGH = 2, RNG_AREA = 3, RNG_ENV = 4, RNG_PT_BOUNCE = 5, RNG_PT_EMIT = 6 };
 DEV void rng4(uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, uint32_t purpose, uint32_t light,
               uint32_t iter, float out[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ (uint32_t)(path >> 32);
@@ -1170,8 +1170,60 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         c = phong_or_brdf<FULL>(env_radiance(sv, L, direction), wo, direction, ret, m);
         break;
     }
+    case kLightEmitMesh:                                        // hw7 object lights: NEE sample
+    case kLightEmitSphere: {                                    // (oracle emitter_shading)
+        float xi[4];
+        rng4(seed, pixel, sample, path, RNG_PT_EMIT, (uint32_t)li, 0, xi);
+        const f3 p = ret.point;
+        f3 LC;
+        if (L.type == kLightEmitSphere) {                       // uniform in the subtended cone
+            const f3 C = ld3(L.pos);
+            const float Rw = L.size;
+            const f3 dv = C - p;
+            const float dd = norm(dv);
+            const bool inside = !(dd > Rw);                     // inside: all directions
+            float cosmax = -1.0f;
+            if (!inside) {
+                const float sin2 = (Rw * Rw) / (dd * dd);
+                cosmax = sqrtf(fmax0(1.0f - sin2));
+            }
+            const float cosT = 1.0f - xi[0] * (1.0f - cosmax);
+            const float sinT = sqrtf(fmax0(1.0f - cosT * cosT));
+            const float phi = (float)(2 * PI_D) * xi[1];
+            const f3 dn = dd > 0.0f ? dv / dd : mk(0, 1, 0);
+            const f3 u = ortho_u(dn), w = cross(dn, u);
+            dir = normalized((u * (sinT * f_cos(phi)) + w * (sinT * f_sin(phi))) + dn * cosT);
+            const f3 oc = p - C;
+            const float b = dot(dir, oc);
+            const float disc = b * b - (sqn(oc) - Rw * Rw);
+            const float t = inside ? -b + sqrtf(fmax0(disc)) : -b - sqrtf(fmax0(disc));
+            lp = p + dir * t;
+            LC = ld3(L.inten) * ((float)(2 * PI_D) * (1.0f - cosmax));
+        } else {                                                // area-weighted triangle, uniform point
+            const float* cdf = sv.emit_cdf + L.tri_first;
+            const float target = xi[0] * L.coverage;
+            int lo = 0, hi = L.tri_count - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (target < cdf[mid]) hi = mid; else lo = mid + 1;
+            }
+            const float* T = sv.emit_tris + 9 * (size_t)(L.tri_first + lo);
+            const f3 a = ld3(T), b = ld3(T + 3), cc = ld3(T + 6);
+            const float sq = sqrtf(xi[1]);
+            lp = (a * (1.0f - sq) + b * (sq * (1.0f - xi[2]))) + cc * (sq * xi[2]);
+            const f3 nl = normalized(cross(b - a, cc - a));
+            const f3 dv = lp - p;
+            const float dd = norm(dv);
+            dir = dv / dd;
+            const float cosl = fabsf(dot(dir, nl));
+            LC = ld3(L.inten) * ((cosl * L.coverage) / (dd * dd));
+        }
+        mode = 3.0f;
+        c = phong_or_brdf<FULL>(LC, wo, dir, ret, m);
+        break;
     }
-    if (mode == 1.0f) {
+    }
+    if (mode == 1.0f || mode == 3.0f) {
         // hits with gett() beyond |p-L| + eps can never satisfy the blocking test
         float dl = norm(ret.point - lp);
         float oabs = fmaxf(fmaxf(fabsf(origin.x), fabsf(origin.y)), fabsf(origin.z));
@@ -1519,6 +1571,233 @@ __global__ void __launch_bounds__(BLOCK) k_shade(const SceneView sv, const Camer
     }
 }
 
+// ------------------------------------------------------------------ hw7 path tracer
+// One shading step of oracle/rtg_oracle.c pt_sample() per ray (no reference code exists:
+// pages/Page7.md describes the integrator in prose; DESIGN.md §8 fixes it).  Writes the
+// vertex contribution v into nodes[i] (k_shadow / k_light_sum add the lights, k_pt_gather
+// adds T (x) v to the sample's radiance), the Beer-attenuated throughput into paths[i], and
+// at most one continuation ray.
+struct DielSplit {
+    bool entering, tir;
+    float F;
+    f3 tdir, torg;
+};
+DEV DielSplit dielectric_split(const SceneView& sv, f3 d, const Ret& ret, const MaterialDev& m) {   // :188-259
+    DielSplit r;
+    float dp = dot(d, ret.normal);
+    float nt = m.refraction_index;
+    float snell, n_t, n_i;
+    f3 normal;
+    if (dp < 0) { snell = 1.0f / nt; normal = ret.normal; n_t = nt; n_i = 1; r.entering = true; }
+    else { snell = nt; normal = -ret.normal; n_t = 1; n_i = nt; r.entering = false; }
+    float cosTheta = -dot(d, normal);
+    f3 leftPart = (d + normal * cosTheta) * snell;
+    float srp = (float)(1 - sq_d(snell) * (1 - sq_d(cosTheta)));
+    r.tir = srp < 0;
+    srp = sqrtf(srp);
+    r.tdir = normalized(leftPart - normal * srp);
+    r.torg = ret.point - normal * sv.shadow_eps;
+    float cos_t = -dot(r.tdir, normal);
+    float cos_i = -dot(d, normal);
+    float rPar = (n_t * cos_i - n_i * cos_t) / (n_t * cos_i + n_i * cos_t);
+    float rPer = (n_i * cos_i - n_t * cos_t) / (n_i * cos_i + n_t * cos_t);
+    r.F = (float)(0.5f * (sq_d(rPar) + sq_d(rPer)));
+    return r;
+}
+
+constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour to the sample
+
+template <bool FULL, bool SPOT>
+__global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+                                                  uint64_t seed, const RayRec* __restrict__ rays,
+                                                  const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
+                                                  PathRec* __restrict__ paths, NodeRec* __restrict__ nodes,
+                                                  ShadowRec* __restrict__ shadows, int* __restrict__ slist,
+                                                  RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
+                                                  PathRec* __restrict__ next_paths, unsigned long long* qcount, int n) {
+    constexpr int BLOCK = 256;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool has = false;
+    RayRec cr;
+    RayMeta cm;
+    PathRec cp;
+    NodeRec nd;
+    unsigned long long smask = 0;
+    if (i < n) {
+        const RayRec r = rays[i];
+        const RayMeta mt = meta[i];
+        const HitRec h = hits[i];
+        const f3 o = mk(r.o_t.x, r.o_t.y, r.o_t.z), d = mk(r.d.x, r.d.y, r.d.z);
+        const float time = r.o_t.w;
+        uint32_t pixel, sample;
+        int x, y;
+        slot_pixel(cam, ps, mt.slot, pixel, sample, x, y);
+        const uint64_t path = (uint64_t)level + 1;
+        const int flags = sv.pt_flags;
+        f3 T = mk(1, 1, 1);
+        int spec = 1, medium = 0;
+        if (level > 0) {
+            const PathRec pr = paths[i];
+            T = mk(pr.tr, pr.tg, pr.tb);
+            spec = pr.flags & 1;
+            medium = pr.flags >> 8;
+        }
+        nd.px = nd.py = nd.pz = 0.0f;
+        nd.cr = nd.cg = nd.cb = 0.0f;
+        nd.F = 0.0f;
+        nd.child0 = nd.child1 = -1;
+        nd.material = 0;
+        nd.slot = mt.slot;
+        int kind = NK_FINAL;
+        if (h.obj < 0) {
+            if (level == 0) {     // primary miss: the reference's background rules
+                f3 bg = !FULL ? ld3(sv.background)
+                      : (cam.total > 1) ? background(sv, cam, y, x, d) : background(sv, cam, x, y, d);
+                nd.cr = bg.x; nd.cg = bg.y; nd.cb = bg.z;
+                kind |= kContrib;
+            }
+        } else {
+            const Ret ret = hit_record<FULL>(sv, o, d, time, h);
+            nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
+            nd.material = ret.matIndex;
+            if (medium) {                                              // Beer's law inside
+                const MaterialDev& mm = sv.materials[medium - 1];
+                const float bd = norm(ret.point - o);
+                T = cw(T, mk(f_exp(-mm.absorption[0] * bd), f_exp(-mm.absorption[1] * bd),
+                             f_exp(-mm.absorption[2] * bd)));
+            }
+            const int em = sv.top_emit[h.obj];
+            if (em >= 0) {                                             // object light: emit, stop
+                if (level == 0 || !(flags & RTG_PT_NEE) || spec) {
+                    const LightDev& L = sv.lights[em];
+                    nd.cr = L.inten[0]; nd.cg = L.inten[1]; nd.cb = L.inten[2];
+                    kind |= kContrib;
+                }
+            } else if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {
+                nd.cr = ret.tc.x; nd.cg = ret.tc.y; nd.cb = ret.tc.z;
+                kind |= kContrib;
+            } else {
+                const MaterialDev m = sv.materials[ret.matIndex - 1];
+                DielSplit ds;
+                ds.entering = true; ds.tir = false; ds.F = 0.0f;
+                if (m.type == RTG_MAT_DIELECTRIC) ds = dielectric_split(sv, d, ret, m);
+                if (ds.entering) {                                     // BasicShading + NEE
+                    kind |= kContrib | 0x100;
+                    const f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
+                    nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
+                    for (int li = 0; li < sv.num_lights; li++) {
+                        ShadowRec sr;
+                        light_sample<FULL, SPOT>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
+                        shadows[(size_t)i * sv.num_lights + li] = sr;
+                        if (sr.c.w != 0.0f) smask |= 1ull << li;
+                        else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
+                    }
+                }
+                const bool cont = (flags & RTG_PT_RUSSIAN_ROULETTE) ? (level + 1 < RTG_PT_MAX_BOUNCES) : (mt.depth > 0);
+                if (cont) {
+                    float xi[4];
+                    rng4(seed, pixel, sample, path, RNG_PT_BOUNCE, 0, 0, xi);
+                    f3 w = mk(1, 1, 1), no, ndir;
+                    int nspec = 1, nmedium = medium;
+                    if (m.type == RTG_MAT_NORMAL) {                    // hemisphere sample
+                        const f3 nn = ret.normal, u = ortho_u(nn), bt = cross(nn, u);
+                        const float phi = (float)(2 * PI_D) * xi[0];
+                        const float cosT = (flags & RTG_PT_IMPORTANCE) ? sqrtf(1.0f - xi[1]) : xi[1];
+                        const float sinT = sqrtf(fmax0(1.0f - cosT * cosT));
+                        const f3 wi = normalized((u * (sinT * f_cos(phi)) + nn * cosT) + bt * (sinT * f_sin(phi)));
+                        const f3 fc = phong_or_brdf<FULL>(mk(1, 1, 1), -d, wi, ret, m);
+                        if (flags & RTG_PT_IMPORTANCE) w = cosT > 0.0f ? fc * ((float)PI_D / cosT) : mk(0, 0, 0);
+                        else w = fc * (float)(2 * PI_D);
+                        no = ret.point + nn * sv.shadow_eps;
+                        ndir = wi;
+                        nspec = 0;
+                    } else if (m.type == RTG_MAT_DIELECTRIC && !ds.tir && !(xi[3] < ds.F)) {   // refract
+                        no = ds.torg;
+                        ndir = ds.tdir;
+                        nmedium = ds.entering ? ret.matIndex : 0;
+                    } else {                                           // reflect
+                        mirror_ray(sv, d, ret, m, seed, pixel, sample, path, no, ndir);
+                        if (m.type == RTG_MAT_MIRROR) w = ld3(m.mirror);
+                        else if (m.type == RTG_MAT_CONDUCTOR)
+                            w = ld3(m.mirror) * conductor_fresnel(m.refraction_index, m.absorption_index, d, ret.normal);
+                    }
+                    bool ok = !(isnan3(no) || isnan3(ndir));
+                    if (ok && (flags & RTG_PT_RUSSIAN_ROULETTE)) {
+                        const float qc = fabsf(dot(ret.normal, ndir));
+                        ok = xi[2] < qc;
+                        if (ok) w = w / qc;
+                    }
+                    if (ok) {
+                        const f3 Tn = cw(T, w);
+                        if (!(Tn.x == 0.0f && Tn.y == 0.0f && Tn.z == 0.0f)) {
+                            has = true;
+                            cr = make_ray(no, ndir, time);
+                            cm.slot = mt.slot; cm.path_lo = (unsigned)(path + 1); cm.path_hi = 0u; cm.depth = mt.depth - 1;
+                            cp.tr = Tn.x; cp.tg = Tn.y; cp.tb = Tn.z; cp.flags = nspec | (nmedium << 8);
+                        }
+                    }
+                }
+            }
+        }
+        nd.kind = kind;
+        PathRec pw;
+        pw.tr = T.x; pw.tg = T.y; pw.tb = T.z; pw.flags = spec | (medium << 8);
+        paths[i] = pw;
+    }
+    // compaction: one continuation per lane, shadow list light-major per wave (as k_shade)
+    __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64];
+    __shared__ unsigned long long s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long lt = __lanemask_lt();
+    const unsigned long long m1 = __ballot(has);
+    const unsigned coff = __popcll(m1 & lt);
+    unsigned stot = 0;
+    for (int li = 0; li < sv.num_lights; li++) stot += __popcll(__ballot((smask >> li) & 1ull));
+    if (lane == 0) { s_wc[wv] = __popcll(m1); s_ws[wv] = stot; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned c = 0, sh = 0;
+        for (int k = 0; k < BLOCK / 64; k++) {
+            const unsigned a = s_wc[k], b = s_ws[k];
+            s_wc[k] = c; s_ws[k] = sh;
+            c += a; sh += b;
+        }
+        s_base = (c | sh) ? atomicAdd(qcount, ((unsigned long long)sh << 32) | c) : 0ull;
+    }
+    __syncthreads();
+    const int idx = (int)((unsigned)s_base + s_wc[wv] + coff);
+    if (i < n) {
+        if (has) { next_rays[idx] = cr; next_meta[idx] = cm; next_paths[idx] = cp; nd.child1 = idx; }
+        nodes[i] = nd;
+    }
+    unsigned sb = (unsigned)(s_base >> 32) + s_ws[wv];
+    for (int li = 0; li < sv.num_lights; li++) {
+        const bool need = (smask >> li) & 1ull;
+        const unsigned long long m = __ballot(need);
+        if (need) slist[sb + __popcll(m & lt)] = i * sv.num_lights + li;
+        sb += __popcll(m);
+    }
+}
+
+// L[slot] += T (x) v of every contributing vertex, one level at a time (stream order keeps
+// the oracle's per-sample summation order).  Level 0 starts the sum: L = (0,0,0) [+ T (x) v].
+__global__ void __launch_bounds__(256) k_pt_gather(const NodeRec* __restrict__ nodes, const PathRec* __restrict__ paths,
+                                                   NodeRec* __restrict__ level0, int level, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NodeRec nd = nodes[i];
+    const bool c = (nd.kind & kContrib) != 0;
+    if (level == 0) {
+        f3 L = mk(0, 0, 0);
+        if (c) L = L + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), mk(nd.cr, nd.cg, nd.cb));
+        level0[i].cr = L.x; level0[i].cg = L.y; level0[i].cb = L.z;
+    } else if (c) {
+        NodeRec& z = level0[nd.slot];
+        const f3 L = mk(z.cr, z.cg, z.cb) + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), mk(nd.cr, nd.cg, nd.cb));
+        z.cr = L.x; z.cg = L.y; z.cb = L.z;
+    }
+}
+
 // Shadow queries + in-order light sum of Scene::BasicShading (src/Scene.cpp:374-398).
 // One thread per traced shadow query (compacted by k_shade).  With one light the result is
 // added to the node colour here (col + c or col + 0, as Scene::RecursiveShading's light loop
@@ -1560,7 +1839,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 const float num = DL * (1.0f - 1e-5f) - 1e-5f * S - po * (1.0f + 1e-5f);
                 if (num > 0.0f && dn > 0.0f) t_cert = num / (dn * (1.0f + 2e-5f));
                 if (!(t_cert < FLT_MAX)) t_cert = 0.0f;
-            } else {
+            } else if (sr.c.w == 2.0f) {
                 t_cert = INFINITY;
             }
         }
@@ -1570,7 +1849,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         bool blocked;
         if (h.pad == 1) {
             blocked = true;         // certified by closest_hit (ANY)
-        } else if (sr.c.w == 1.0f) {
+        } else if (sr.c.w == 1.0f || sr.c.w == 3.0f) {
             blocked = false;
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
@@ -1580,7 +1859,12 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 const f3 l_ = mk(ld(q + 12), ld(q + 13), ld(q + 14));
                 const f3 p_ = mk(ld(&nodes[i].px), ld(&nodes[i].py), ld(&nodes[i].pz));
                 f3 hp = o_ + d_ * h.t;
-                blocked = norm(p_ - l_) > norm(p_ - hp);
+                if (sr.c.w == 1.0f) {
+                    blocked = norm(p_ - l_) > norm(p_ - hp);
+                } else {   // object light (hw7, Page7.md:143-147): an occluder nearer than the sample
+                    const float dl = norm(p_ - l_);
+                    blocked = norm(p_ - hp) < dl - (sv.shadow_eps + 1e-4f * dl);
+                }
             }
         } else {
             blocked = h.obj >= 0;
@@ -1781,6 +2065,26 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
     if (sv.num_lights > 1)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, shadows, nodes, n);
+}
+void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
+                     const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
+                     ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta, PathRec* next_paths,
+                     unsigned long long* qcount, int n, hipStream_t st) {
+    if (n <= 0) return;
+    dim3 g(nblk(n, 256)), b(256);
+    if (sv.full)
+        hipLaunchKernelGGL((k_pt_shade<true, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, nodes,
+                           shadows, slist, next_rays, next_meta, next_paths, qcount, n);
+    else if (sv.spot)
+        hipLaunchKernelGGL((k_pt_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, nodes,
+                           shadows, slist, next_rays, next_meta, next_paths, qcount, n);
+    else
+        hipLaunchKernelGGL((k_pt_shade<false, false>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths,
+                           nodes, shadows, slist, next_rays, next_meta, next_paths, qcount, n);
+}
+void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, NodeRec* level0, int level, int n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, nodes, paths, level0, level, n);
 }
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st) {
     if (n <= 0) return;

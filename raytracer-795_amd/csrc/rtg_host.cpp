@@ -59,6 +59,11 @@ inline V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x *
 inline float comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 
 struct Mat4 { float c[4][4]; };   // glm column-major
+inline V3 xform_point(const Mat4& m, V3 v, float w) {   // glm mat4 * vec4: (c0x + c1y) + (c2z + c3w)
+    float r[3];
+    for (int i = 0; i < 3; i++) r[i] = (m.c[0][i] * v.x + m.c[1][i] * v.y) + (m.c[2][i] * v.z + m.c[3][i] * w);
+    return v3(r[0], r[1], r[2]);
+}
 Mat4 identity() {
     Mat4 m;
     memset(&m, 0, sizeof m);
@@ -367,8 +372,11 @@ int upload(DBuf& b, const std::vector<T>& v) {
 }
 
 struct Level {
-    DBuf rays, meta, hits, nodes, shadows, slist;
-    void release() { rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release(); }
+    DBuf rays, meta, hits, nodes, shadows, slist, paths;
+    void release() {
+        rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release();
+        paths.release();
+    }
 };
 
 // One in-flight pass: its own stream, level buffers and queue counters, so that while the
@@ -417,7 +425,8 @@ struct rtg_scene {
     std::vector<int> orig_prim;              // absolute BVH position -> original prim index
     SceneView sv{};
     DBuf d_tops, d_geoms, d_nodes, d_nodes4, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
-        d_texels, d_lights, d_origprim;
+        d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf;
+    int num_emit = 0;                        // hw7 object lights
     // render workspace
     std::vector<Lane> lanes;
     DBuf d_acc, d_counters, d_stats;
@@ -503,7 +512,7 @@ static int validate(const rtg_scene_desc* d) {
 static void scene_free(rtg_scene* s) {
     DBuf* bufs[] = {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices, &s->d_vnormals,
                     &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights, &s->d_origprim,
-                    &s->d_acc, &s->d_counters, &s->d_stats};
+                    &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_acc, &s->d_counters, &s->d_stats};
     for (DBuf* b : bufs) b->release();
     for (Lane& l : s->lanes) l.destroy();
     s->lanes.clear();
@@ -842,6 +851,45 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         }
     }
 
+    // hw7 object lights (path tracer NEE): appended after the scene's lights, in object order.
+    // World-space geometry sampled at time 0, exactly as oracle/rtg_oracle.c builds it.
+    std::vector<int> top_emit(d->num_objects + d->num_instances, -1);
+    std::vector<float> etris, ecdf;
+    s->num_emit = 0;
+    for (int i = 0; i < d->num_objects; i++) {
+        const rtg_object_desc& o = d->objects[i];
+        if (!o.is_light) continue;
+        if (d->num_lights + s->num_emit + 1 > kMaxLights) return fail(RTG_ERR_UNSUPPORTED, "more than 64 lights + object lights");
+        LightDev L;
+        memset(&L, 0, sizeof L);
+        memcpy(L.inten, o.radiance, 12);
+        const Mat4& M = model[i];
+        if (o.type == RTG_OBJ_SPHERE) {
+            L.type = kLightEmitSphere;
+            V3 c = xform_point(M, verts[o.center - 1], 1.0f);
+            L.pos[0] = c.x; L.pos[1] = c.y; L.pos[2] = c.z;
+            L.size = o.radius * vnorm(v3(M.c[0][0], M.c[0][1], M.c[0][2]));
+        } else {
+            L.type = kLightEmitMesh;
+            const std::vector<int>& pv = op[i].v;
+            L.tri_first = (int)ecdf.size();
+            L.tri_count = (int)(pv.size() / 3);
+            float acc = 0.0f;
+            for (size_t k = 0; k + 2 < pv.size(); k += 3) {       // parse order
+                V3 a = xform_point(M, verts[pv[k] - 1], 1.0f), b = xform_point(M, verts[pv[k + 1] - 1], 1.0f),
+                   c = xform_point(M, verts[pv[k + 2] - 1], 1.0f);
+                const float t9[9] = {a.x, a.y, a.z, b.x, b.y, b.z, c.x, c.y, c.z};
+                etris.insert(etris.end(), t9, t9 + 9);
+                acc = acc + 0.5f * vnorm(cross(b - a, c - a));
+                ecdf.push_back(acc);
+            }
+            L.coverage = acc;
+        }
+        top_emit[i] = d->num_lights + s->num_emit;
+        lights.push_back(L);
+        s->num_emit++;
+    }
+
     if (s->device < 0) return RTG_OK;   // host-only build (introspection / CPU tests)
     std::vector<float> vflat(d->vertices, d->vertices + 3 * (size_t)nv);
     std::vector<float> tcflat;
@@ -852,7 +900,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         (rc = upload(s->d_tris, tris)) || (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_vertices, vflat)) ||
         (rc = upload(s->d_vnormals, s->vnormals)) || (rc = upload(s->d_texcoords, tcflat)) ||
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
-        (rc = upload(s->d_lights, lights)) || (rc = upload(s->d_origprim, s->orig_prim)))
+        (rc = upload(s->d_lights, lights)) || (rc = upload(s->d_origprim, s->orig_prim)) ||
+        (rc = upload(s->d_topemit, top_emit)) || (rc = upload(s->d_etris, etris)) || (rc = upload(s->d_ecdf, ecdf)))
         return rc;
 
     SceneView& sv = s->sv;
@@ -870,6 +919,11 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.textures = s->d_textures.as<TextureDev>(); sv.num_textures = d->num_textures;
     sv.texels = s->d_texels.as<float>();
     sv.lights = s->d_lights.as<LightDev>(); sv.num_lights = d->num_lights;
+    sv.top_emit = s->d_topemit.as<int>();
+    sv.emit_tris = s->d_etris.as<float>();
+    sv.emit_cdf = s->d_ecdf.as<float>();
+    sv.num_emit = s->num_emit;
+    sv.pt_flags = 0;
     sv.max_depth = d->max_recursion_depth;
     sv.shadow_eps = d->shadow_ray_eps;
     sv.int_eps = d->intersection_test_eps;
@@ -975,7 +1029,15 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     const int ns_chunk = (int)std::max<long long>(1, std::min<long long>(total, max_batch));
     const int np_pass = (int)std::max<long long>(1, std::min<long long>(npix, max_batch / ns_chunk));
     int exhaustive = o.traversal == 1;
-    const int nL = s->sv.num_lights;
+    if (cam->integrator != RTG_INTEGRATOR_REFERENCE && cam->integrator != RTG_INTEGRATOR_PATH)
+        return fail(RTG_ERR_INVALID, "unknown integrator");
+    const bool pt = cam->integrator == RTG_INTEGRATOR_PATH;
+    SceneView sv = s->sv;                    // per-render view: the path tracer's light loop
+    if (pt) {
+        sv.pt_flags = cam->pt_flags;
+        if (cam->pt_flags & RTG_PT_NEE) sv.num_lights += s->num_emit;
+    }
+    const int nL = sv.num_lights;
 
     int rc;
     if ((rc = s->d_acc.grow(sizeof(float) * 3 * std::max<size_t>(npix, 1)))) return rc;
@@ -1027,7 +1089,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     }
 
     rtg_render_stats stt{};
-    const int max_levels = std::max(0, s->sv.max_depth) + 1;
+    const int max_levels = (pt && (cam->pt_flags & RTG_PT_RUSSIAN_ROULETTE)) ? RTG_PT_MAX_BOUNCES
+                                                                             : std::max(0, s->sv.max_depth) + 1;
     // enqueue trace / shade / shadow of the lane's current level and the count read-back
     auto enqueue_level = [&](Lane& ln) -> int {
         const PassDev& ps = plist[ln.pass];
@@ -1044,18 +1107,29 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const bool may_spawn = level + 1 < max_levels;
         const size_t cap = may_spawn ? 2 * (size_t)n : 1;
         if ((rc2 = Ln.rays.grow(sizeof(RayRec) * cap)) || (rc2 = Ln.meta.grow(sizeof(RayMeta) * cap))) return rc2;
+        if (pt && ((rc2 = Lc.paths.grow(sizeof(PathRec) * (size_t)n)) || (rc2 = Ln.paths.grow(sizeof(PathRec) * cap))))
+            return rc2;
         unsigned long long* qc = ln.qcnt.as<unsigned long long>() + level;
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
-        launch_trace(s->sv, Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st);
+        launch_trace(sv, Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
-        launch_shade(s->sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
-                     Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), Ln.rays.as<RayRec>(),
-                     Ln.meta.as<RayMeta>(), qc, n, ln.st);
+        if (pt)
+            launch_pt_shade(sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
+                            Lc.paths.as<PathRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
+                            Ln.rays.as<RayRec>(), Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st);
+        else
+            launch_shade(sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
+                         Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), Ln.rays.as<RayRec>(),
+                         Ln.meta.as<RayMeta>(), qc, n, ln.st);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
-        launch_shadow(s->sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
+        launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
                       Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
+        // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
+        if (pt)
+            launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), ln.levels[0].nodes.as<NodeRec>(), level, n,
+                             ln.st);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
         HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
@@ -1074,7 +1148,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         Level& L0 = ln.levels[0];
         if ((rc2 = L0.rays.grow(sizeof(RayRec) * (size_t)n0)) || (rc2 = L0.meta.grow(sizeof(RayMeta) * (size_t)n0)))
             return rc2;
-        launch_raygen(s->sv, cd, ps, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(), n0, ln.st);
+        launch_raygen(sv, cd, ps, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(), n0, ln.st);
         stt.primary_rays += (uint64_t)n0;
         ln.busy = true;
         return enqueue_level(ln);
@@ -1083,8 +1157,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const PassDev& ps = plist[ln.pass];
         const int level = ln.level;
         stt.max_level = std::max(stt.max_level, level);
-        for (int l = level - 1; l >= 0; l--)
-            launch_resolve(s->sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(), ln.counts[l],
+        for (int l = level - 1; l >= 0 && !pt; l--)
+            launch_resolve(sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(), ln.counts[l],
                            ln.st);
         const int mode = (total == 1) ? 2 : (ps.s0 == 0 ? 1 : 0);
         launch_accumulate(ln.levels[0].nodes.as<NodeRec>(), s->d_acc.as<float>(), ps, cam->nx, mode, ln.st);

@@ -91,6 +91,12 @@ struct TriGeom {
     float4 p2;  // (a-c).z, orig_index (bits), leaf length (int bits, first prim of each leaf), 0
 };
 
+// Internal light types of hw7 object lights (appended after the scene's lights; only the
+// path tracer's NEE loop reaches them).  inten = radiance; mesh: coverage = total world area,
+// tri_first/tri_count = range in SceneView::emit_tris / emit_cdf; sphere: pos = world centre,
+// size = world radius.
+constexpr int kLightEmitMesh = 16;
+constexpr int kLightEmitSphere = 17;
 struct LightDev {
     int type;
     float pos[3], dir[3], inten[3];
@@ -98,6 +104,7 @@ struct LightDev {
     float normal[3], u[3], v[3];
     int tex;
     float cos_fall, cos_cov;   // host-computed cos() of fall/coverage (same convention)
+    int tri_first, tri_count;  // mesh emitters
 };
 
 struct TextureDev {
@@ -137,6 +144,19 @@ struct SceneView {
     int bg_texture, env_light;
     int full;                      // 0: no textures / BRDFs / area or environment lights
     int spot;                      // any spot light (its double-precision cone math is compiled in)
+    // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
+    // lights into num_lights)
+    const int* top_emit;           // per top-level entry: emitter light index, -1 if not a light
+    const float* emit_tris;        // 9 floats per world-space emitter triangle (parse order)
+    const float* emit_cdf;         // running float sum of the triangle areas per emitter
+    int num_emit;
+    int pt_flags;
+};
+
+// Path state of one path-tracing ray (per level, next to RayRec / RayMeta).
+struct PathRec {       // 16 B
+    float tr, tg, tb;  // throughput (after the Beer attenuation of the segment, once shaded)
+    int flags;         // bit 0: previous bounce specular; bits 8..: medium material (1-based, 0 none)
 };
 
 // One batch ("pass") of the frame: pixels [p0, p0 + npass) of the tiled pixel order (8x8
@@ -217,6 +237,11 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
                   unsigned long long* qcount, int n, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
                    int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st);
+void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
+                     const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
+                     ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta, PathRec* next_paths,
+                     unsigned long long* qcount, int n, hipStream_t st);
+void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, NodeRec* level0, int level, int n, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
 void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);

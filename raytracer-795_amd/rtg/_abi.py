@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 1
+RTG_ABI_VERSION = 2
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -26,6 +26,9 @@ INTERP_NN, INTERP_BILINEAR = 0, 1
 TEX_IMAGE, TEX_PERLIN = 0, 1
 NC_ABSVAL, NC_LINEAR, NC_NONE = 0, 1, 2
 LIGHT_POINT, LIGHT_AREA, LIGHT_DIRECTIONAL, LIGHT_SPOT, LIGHT_ENVIRONMENT = 0, 1, 2, 3, 4
+INTEGRATOR_REFERENCE, INTEGRATOR_PATH = 0, 1
+PT_IMPORTANCE, PT_NEE, PT_RUSSIAN_ROULETTE = 1, 2, 4
+PT_MAX_BOUNCES = 32
 
 F3 = C.c_float * 3
 I2 = C.c_int32 * 2
@@ -43,7 +46,8 @@ class ObjectDesc(C.Structure):
                 ("textures", I2), ("texture_offset", C.c_int32), ("smooth", C.c_int32),
                 ("xform_first", C.c_int32), ("xform_count", C.c_int32), ("blur", F3),
                 ("center", C.c_int32), ("radius", C.c_float), ("v", I3),
-                ("face_first", C.c_int32), ("face_count", C.c_int32)]
+                ("face_first", C.c_int32), ("face_count", C.c_int32),
+                ("is_light", C.c_int32), ("radiance", F3)]
 
 
 class InstanceDesc(C.Structure):
@@ -95,7 +99,8 @@ class CameraDesc(C.Structure):
                 ("left", C.c_float), ("right", C.c_float), ("bottom", C.c_float), ("top", C.c_float),
                 ("near_distance", C.c_float), ("nx", C.c_int32), ("ny", C.c_int32),
                 ("num_samples", C.c_int32), ("is_dof", C.c_int32), ("focus_distance", C.c_float),
-                ("aperture_size", C.c_float), ("left_handed", C.c_int32)]
+                ("aperture_size", C.c_float), ("left_handed", C.c_int32),
+                ("integrator", C.c_int32), ("pt_flags", C.c_int32)]
 
 
 class RenderOpts(C.Structure):

@@ -58,6 +58,8 @@ class Camera:                       # src/Camera.h, src/Parser.h:52-164
     aperture_size: float = 0.0
     is_dof: bool = False
     left_handed: bool = False
+    integrator: int = A.INTEGRATOR_REFERENCE     # hw7 <Renderer>PathTracing</Renderer>
+    pt_flags: int = 0                            # hw7 <RendererParams> (A.PT_*)
     # XML-only conveniences kept for write_xml round trips
     gaze_point: np.ndarray | None = None
     fov_y: float | None = None
@@ -75,6 +77,8 @@ class Camera:                       # src/Camera.h, src/Parser.h:52-164
         d.focus_distance = float(f32(self.focus_distance))
         d.aperture_size = float(f32(self.aperture_size))
         d.left_handed = int(bool(self.left_handed))
+        d.integrator = int(self.integrator)
+        d.pt_flags = int(self.pt_flags)
         return d
 
 
@@ -138,6 +142,8 @@ class Object:                       # src/Shape.h (Sphere / Triangle / Mesh)
     faces: np.ndarray | None = None                 # (F,3) int32, 1-based, offsets applied
     ply_file: str | None = None                     # write_xml: emit faces as a PLY
     xml_vertex_offset: int = 0
+    is_light: bool = False                          # hw7 <LightSphere> / <LightMesh>
+    radiance: tuple = (0.0, 0.0, 0.0)
 
 
 @dataclass
@@ -240,6 +246,8 @@ class Scene:
             od.v = A.I3(*o.v)
             od.face_first = face_first[i]
             od.face_count = 0 if o.faces is None else int(np.asarray(o.faces).reshape(-1, 3).shape[0])
+            od.is_light = int(bool(o.is_light))
+            od.radiance = A.F3(*map(float, np.asarray(o.radiance, f32)))
         keep.append(objs)
         insts = (A.InstanceDesc * max(1, len(self.instances)))()
         for i, it in enumerate(self.instances):
@@ -544,6 +552,16 @@ def parse_xml(xml_path: str) -> Scene:
             y = f32(f32(math.tan(float(fovr))) * f32(cam.near_distance))
             x = f32(aspect * y)
             cam.near_plane = (float(-x), float(x), float(-y), float(y))
+        # hw7 (pages/Page7.md; the reference parser has no such tags): <Renderer>PathTracing</Renderer>
+        # and <RendererParams>ImportanceSampling NextEventEstimation RussianRoulette</RendererParams>
+        ren = _text(ce, "Renderer")
+        if ren is not None and ren.strip().lower().startswith("pathtracing"):
+            cam.integrator = A.INTEGRATOR_PATH
+        rp = _text(ce, "RendererParams")
+        if rp is not None:
+            for tok in rp.split():
+                cam.pt_flags |= {"importancesampling": A.PT_IMPORTANCE, "nexteventestimation": A.PT_NEE,
+                                 "russianroulette": A.PT_RUSSIAN_ROULETTE}.get(tok.strip().lower(), 0)
         sc.cameras.append(cam)
     # ParseBRDF (:166-302)
     brdfs = []   # (type, id, exponent)
@@ -708,21 +726,31 @@ def parse_xml(xml_path: str) -> Scene:
         if mb is not None:
             o.blur = tuple(_f3(mb))
 
-    for el in oe.findall("Sphere"):
-        o = Object(type=A.OBJ_SPHERE)
-        common(el, o)
-        o.center = _query_int(_text(el, "Center"), 1)
-        o.radius = _query_float(_text(el, "Radius"), 1.0)
-        sc.objects.append(o)
+    # object lights (hw7): <LightSphere> after the spheres, <LightMesh> after the meshes
+    def light(el, o):
+        o.is_light = True
+        o.radiance = tuple(_f3(_text(el, "Radiance")))
+
+    for tag in ("Sphere", "LightSphere"):
+        for el in oe.findall(tag):
+            o = Object(type=A.OBJ_SPHERE)
+            common(el, o)
+            o.center = _query_int(_text(el, "Center"), 1)
+            o.radius = _query_float(_text(el, "Radius"), 1.0)
+            if tag == "LightSphere":
+                light(el, o)
+            sc.objects.append(o)
     for el in oe.findall("Triangle"):
         o = Object(type=A.OBJ_TRIANGLE)
         common(el, o)
         o.v = tuple(int(v) for v in _text(el, "Indices").split()[:3])
         sc.objects.append(o)
     mesh_start = len(sc.objects)
-    for el in oe.findall("Mesh"):
+    for el in oe.findall("Mesh") + oe.findall("LightMesh"):
         o = Object(type=A.OBJ_MESH)
         common(el, o)
+        if el.tag == "LightMesh":
+            light(el, o)
         o.smooth = _attr_prefix(el, "shadingMode", "smooth")
         fe = el.find("Faces")
         ply = None
@@ -850,6 +878,12 @@ def write_xml(sc: Scene, xml_path: str, images: dict | None = None) -> str:
             out.append(f"<FocusDistance>{_fmt(c.focus_distance)}</FocusDistance>")
             out.append(f"<ApertureSize>{_fmt(c.aperture_size)}</ApertureSize>")
         out.append(f"<ImageName>{c.image_name}</ImageName>")
+        if c.integrator == A.INTEGRATOR_PATH:
+            out.append("<Renderer>PathTracing</Renderer>")
+            toks = [n for f, n in ((A.PT_IMPORTANCE, "ImportanceSampling"), (A.PT_NEE, "NextEventEstimation"),
+                                   (A.PT_RUSSIAN_ROULETTE, "RussianRoulette")) if c.pt_flags & f]
+            if toks:
+                out.append(f"<RendererParams>{' '.join(toks)}</RendererParams>")
         out.append("</Camera>")
     out.append("</Cameras>")
     # BRDFs referenced by materials
@@ -965,24 +999,31 @@ def write_xml(sc: Scene, xml_path: str, images: dict | None = None) -> str:
             lines.append(f"<MotionBlur>{_fmts(o.blur)}</MotionBlur>")
         return lines
 
-    for o in sc.objects:
-        if o.type == A.OBJ_SPHERE:
-            out.append(f'<Sphere id="{o.id}">')
-            out.extend(common(o, "Sphere"))
-            out.append(f"<Center>{o.center}</Center><Radius>{_fmt(o.radius)}</Radius>")
-            out.append("</Sphere>")
+    def radiance(o):
+        return [f"<Radiance>{_fmts(o.radiance)}</Radiance>"] if o.is_light else []
+
+    for lt in (False, True):
+        for o in sc.objects:
+            if o.type == A.OBJ_SPHERE and bool(o.is_light) == lt:
+                tag = "LightSphere" if lt else "Sphere"
+                out.append(f'<{tag} id="{o.id}">')
+                out.extend(common(o, tag))
+                out.append(f"<Center>{o.center}</Center><Radius>{_fmt(o.radius)}</Radius>")
+                out.extend(radiance(o))
+                out.append(f"</{tag}>")
     for o in sc.objects:
         if o.type == A.OBJ_TRIANGLE:
             out.append(f'<Triangle id="{o.id}">')
             out.extend(common(o, "Triangle"))
             out.append(f"<Indices>{o.v[0]} {o.v[1]} {o.v[2]}</Indices>")
             out.append("</Triangle>")
-    for o in sc.objects:
-        if o.type != A.OBJ_MESH:
-            continue
+    meshes = [o for o in sc.objects if o.type == A.OBJ_MESH]
+    for o in [o for o in meshes if not o.is_light] + [o for o in meshes if o.is_light]:
         sm = ' shadingMode="smooth"' if o.smooth else ""
-        out.append(f'<Mesh id="{o.id}"{sm}>')
-        out.extend(common(o, "Mesh"))
+        tag = "LightMesh" if o.is_light else "Mesh"
+        out.append(f'<{tag} id="{o.id}"{sm}>')
+        out.extend(common(o, tag))
+        out.extend(radiance(o))
         f = np.asarray(o.faces, np.int64).reshape(-1, 3)
         if o.ply_file:
             lo, hi = int(f.min()), int(f.max())
@@ -993,7 +1034,7 @@ def write_xml(sc: Scene, xml_path: str, images: dict | None = None) -> str:
             out.append(f'<Faces textureOffset="{to}">')
             out.extend(f"{a} {b} {c}" for a, b, c in f)
             out.append("</Faces>")
-        out.append("</Mesh>")
+        out.append(f"</{tag}>")
     for it in sc.instances:
         base = sc.objects[it.base_object]
         rt = ' resetTransform="true"' if it.reset_transform else ""

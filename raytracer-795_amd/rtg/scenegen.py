@@ -228,10 +228,66 @@ def cornell(nx=1920, ny=1080, spp=64, dof=True, level=2) -> Scene:
     return sc
 
 
-def cornell_pt(nx=1920, ny=1080, spp=256) -> Scene:
-    """C5: C4 geometry at 256 spp (distribution ray tracing; no path-tracer oracle exists)."""
-    sc = cornell(nx, ny, spp=spp, dof=False)
-    sc.cameras[0].image_name = "cornell_pt.png"
+PT_ALL = A.PT_IMPORTANCE | A.PT_NEE | A.PT_RUSSIAN_ROULETTE
+
+
+def cornell_pt(nx=1920, ny=1080, spp=256, flags=PT_ALL, max_depth=6, light_sphere=True, level=2) -> Scene:
+    """C5 (hw7 cornellbox path tracing, pages/Page7.md): cornell box with a ceiling LightMesh and a
+    LightSphere, normalised-BRDF walls, a glossy instanced icosphere, glass and mirror spheres,
+    path traced with `flags` (A.PT_*)."""
+    sc = Scene(max_depth=max_depth, background=(0, 0, 0), ambient=(0, 0, 0))
+    sc.cameras.append(_cam((0, 5, 13.5), (0, 0, -1), (0, 1, 0), nx, ny, fov_deg=45, spp=spp, name="cornell_pt.exr",
+                           integrator=A.INTEGRATOR_PATH, pt_flags=flags))
+    z3 = (0.0, 0.0, 0.0)
+    sc.materials += [
+        Material(brdf=A.BRDF_MBPN, phong_exp=1, ambient=z3, diffuse=(0.75, 0.75, 0.75), specular=z3),
+        Material(brdf=A.BRDF_MBPN, phong_exp=1, ambient=z3, diffuse=(0.75, 0.1, 0.1), specular=z3),
+        Material(brdf=A.BRDF_MBPN, phong_exp=1, ambient=z3, diffuse=(0.1, 0.75, 0.1), specular=z3),
+        Material(brdf=A.BRDF_MBPN, phong_exp=40, ambient=z3, diffuse=(0.2, 0.3, 0.7), specular=(0.4, 0.4, 0.4)),
+        Material(type=A.MAT_MIRROR, ambient=z3, diffuse=z3, specular=z3, mirror=(0.9, 0.9, 0.9)),
+        Material(type=A.MAT_DIELECTRIC, ambient=z3, diffuse=z3, specular=z3, refraction_index=1.5,
+                 absorption_coeff=(0.02, 0.05, 0.1)),
+    ]
+    w = _add_vertices(sc, [(-5, 0, 5), (5, 0, 5), (5, 0, -5), (-5, 0, -5),
+                           (-5, 10, 5), (5, 10, 5), (5, 10, -5), (-5, 10, -5)])
+    q = lambda a, b, c, d: [[a, b, c], [a, c, d]]
+    walls_white = np.array(q(w, w + 1, w + 2, w + 3) + q(w + 4, w + 7, w + 6, w + 5) + q(w + 3, w + 2, w + 6, w + 7),
+                           np.int32)
+    red = np.array(q(w, w + 3, w + 7, w + 4), np.int32)
+    green = np.array(q(w + 1, w + 5, w + 6, w + 2), np.int32)
+    lq = _add_vertices(sc, [(-1.25, 9.98, 1.25), (1.25, 9.98, 1.25), (1.25, 9.98, -1.25), (-1.25, 9.98, -1.25)])
+    iv, ifc = icosphere(level)
+    ib = _add_vertices(sc, iv)
+    sph = _add_vertices(sc, [(2.2, 1.3, 1.2), (-2.4, 1.5, 2.0), (-3.2, 8.2, -2.5)])
+    sc.translations += [(-1.2, 1.4, -2.0)]
+    sc.scalings += [(1.4, 1.4, 1.4)]
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=1, material=6, center=sph, radius=1.3))
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=2, material=5, center=sph + 1, radius=1.0))
+    if light_sphere:
+        sc.objects.append(Object(type=A.OBJ_SPHERE, id=3, material=1, center=sph + 2, radius=0.4, is_light=True,
+                                 radiance=(160.0, 120.0, 80.0)))
+    sc.objects.append(Object(type=A.OBJ_MESH, id=1, material=1, faces=walls_white))
+    sc.objects.append(Object(type=A.OBJ_MESH, id=2, material=2, faces=red))
+    sc.objects.append(Object(type=A.OBJ_MESH, id=3, material=3, faces=green))
+    sc.objects.append(Object(type=A.OBJ_MESH, id=4, material=4, faces=(ifc + ib).astype(np.int32), smooth=True,
+                             xforms=[(A.XF_TRANSLATION, 1), (A.XF_SCALING, 1)]))
+    sc.objects.append(Object(type=A.OBJ_MESH, id=5, material=1, faces=np.array(q(lq + 3, lq + 2, lq + 1, lq), np.int32),
+                             is_light=True, radiance=(600.0, 560.0, 500.0)))
+    return sc
+
+
+def furnace(nx=8, ny=6, spp=64, flags=A.PT_IMPORTANCE, kd=0.6, Le=(10.0, 20.0, 40.0), radius=50.0) -> Scene:
+    """Analytic case: a convex diffuse sphere (normalised Lambertian kd/pi) inside a LightSphere of
+    radiance Le.  Every visible point sees only the light, so its radiance is exactly kd * Le."""
+    sc = Scene(max_depth=1, background=(0, 0, 0), ambient=(0, 0, 0))
+    sc.cameras.append(_cam((0, 0, 4), (0, 0, -1), (0, 1, 0), nx, ny, fov_deg=20, spp=spp, name="furnace.exr",
+                           integrator=A.INTEGRATOR_PATH, pt_flags=flags))
+    sc.materials.append(Material(brdf=A.BRDF_MBPN, phong_exp=1, ambient=(0, 0, 0), diffuse=(kd, kd, kd),
+                                 specular=(0, 0, 0)))
+    c = _add_vertices(sc, [(0, 0, 0)])
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=1, material=1, center=c, radius=1.0))
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=2, material=1, center=c, radius=radius, is_light=True,
+                             radiance=Le))
     return sc
 
 
