@@ -64,6 +64,25 @@ def cpu_baseline(scene, rows: int, threads: int) -> dict:
                       f"({rows * cam.nx} px, {nrays} rays, {dt:.1f} s, literal visit-both-children BVH)"}
 
 
+# BASELINE.json configs -> (rtg.scenegen factory, default spp, config.workload text, data text)
+WORKLOADS = {
+    "dragon1m": ("dragon1m", 64,
+                 "C3 dragon1m: 1,000,004-triangle BVH + mirror & dielectric spheres, point light, Whitted depth 6",
+                 "synthetic (scenegen.dragon1m, seed 20261015)"),
+    "bunny": ("bunny5k", 1,
+              "C2 bunny5k: 5,120-triangle displaced icosphere, mirror floor, glass sphere, Whitted depth 6",
+              "synthetic (scenegen.bunny5k)"),
+    "cornell": ("cornell", 64,
+                "C4 cornell_dynamic: instancing (resetTransform on/off), motion blur, area light, DoF, "
+                "rough mirror, conductor; distribution ray tracing depth 4",
+                "synthetic (scenegen.cornell)"),
+    "cornell_pt": ("cornell_pt", 256,
+                   "C5 cornell_pt (hw7): path tracing with importance sampling + NEE + Russian roulette, "
+                   "LightMesh + LightSphere, BRDF walls, glass / mirror spheres",
+                   "synthetic (scenegen.cornell_pt)"),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -71,7 +90,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--spp", type=int, default=0, help="0 = the workload's spp (64; cornell_pt 256)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="dragon1m",
+                    help="dragon1m = the BASELINE metric line (C3); the others are the configs' own scenes")
     ap.add_argument("--cpu-rows", type=int, default=540)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -91,10 +112,11 @@ def main():
         torch.cuda.set_device(local)
 
     import rtg
-    from rtg import scenegen
 
     t0 = time.perf_counter()
-    scene = scenegen.dragon1m(args.width, args.height, spp=args.spp)
+    from rtg import scenegen
+    make, spp_default, wl_text, data_text = WORKLOADS[args.workload]
+    scene = getattr(scenegen, make)(args.width, args.height, spp=args.spp or spp_default)
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
     t0 = time.perf_counter()
     r = rtg.Renderer(scene, device=local)
@@ -153,7 +175,7 @@ def main():
     bytes_per_launch = bytes_per_ray * trace_rays / max(trace_launches, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("rtg::k_trace<false, false>"),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("rtg::k_trace<false, false>") if args.workload == "dragon1m" else None,
             "traffic_unit": "bytes/launch (PMC, profiles/traffic_current.json)",
             "kernel": "k_trace<false,false> (closest hit, primary+secondary)",
             "avg_launch_ms": round(avg_launch_ms, 3), "launches": trace_launches,
@@ -169,9 +191,8 @@ def main():
         line = {"metric": METRIC, "value": round(value, 2), "unit": "Mray/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2),
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-                "data": "synthetic (scenegen.dragon1m, seed 20261015)",
-                "config": {"workload": "C3 dragon1m: 1,000,004-triangle BVH + mirror & dielectric spheres, "
-                                       "point light, Whitted depth 6",
+                "data": data_text,
+                "config": {"workload": wl_text,
                            "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
                            "parallelism": f"row-interleaved pixel shards x{world} + RCCL reduce"},
                 "rays_per_frame": rays // max(args.steps, 1),
