@@ -1089,7 +1089,7 @@ DEV f3 env_radiance(const SceneView& sv, const LightDev& L, f3 dir) {   // Light
 }
 
 // Unshadowed contribution of light li plus the shadow query it needs.
-template <bool FULL = true, bool SPOT = true>
+template <bool FULL = true, bool SPOT = true, bool BRDF = FULL>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
                       uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
     const LightDev& L = sv.lights[li];
@@ -1107,13 +1107,13 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         mode = 1.0f;
         float dist = norm(ret.point - pos);
         f3 LC = ld3(L.inten) / (dist * dist);
-        c = phong_or_brdf<FULL>(LC, wo, normalized(pos - ret.point), ret, m);
+        c = phong_or_brdf<BRDF>(LC, wo, normalized(pos - ret.point), ret, m);
         break;
     }
     case RTG_LIGHT_DIRECTIONAL: {                               // :447-459
         dir = -ld3(L.dir);
         mode = 2.0f;
-        c = phong_or_brdf<FULL>(ld3(L.inten), wo, dir, ret, m);
+        c = phong_or_brdf<BRDF>(ld3(L.inten), wo, dir, ret, m);
         break;
     }
     case RTG_LIGHT_SPOT: if constexpr (FULL || SPOT) {          // :547-574
@@ -1127,7 +1127,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
             mode = 1.0f;
             float dist = norm(ret.point - pos);
             f3 LC = ld3(L.inten) / (dist * dist);
-            c = phong_or_brdf<FULL>(LC, wo, normalized(pos - ret.point), ret, m);
+            c = phong_or_brdf<BRDF>(LC, wo, normalized(pos - ret.point), ret, m);
             if (!(angle < L.fall)) {
                 float fo = (float)pow((cos((double)angle) - (double)L.cos_cov) / (double)(L.cos_fall - L.cos_cov), 4.0);
                 c = c * fo;
@@ -1149,7 +1149,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         float dSq = norm(pms);
         dSq = dSq * dSq;
         f3 LC = ld3(L.inten) * ((L.size * L.size) * (cosTheta / dSq));
-        c = phong_or_brdf<FULL>(LC, wo, normalized(smp - ret.point), ret, m);
+        c = phong_or_brdf<BRDF>(LC, wo, normalized(smp - ret.point), ret, m);
         break;
     }
     case RTG_LIGHT_ENVIRONMENT: if constexpr (FULL) {          // :766-798
@@ -1167,7 +1167,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         }
         dir = direction;
         mode = 2.0f;
-        c = phong_or_brdf<FULL>(env_radiance(sv, L, direction), wo, direction, ret, m);
+        c = phong_or_brdf<BRDF>(env_radiance(sv, L, direction), wo, direction, ret, m);
         break;
     }
     case kLightEmitMesh:                                        // hw7 object lights: NEE sample
@@ -1219,7 +1219,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
             LC = ld3(L.inten) * ((cosl * L.coverage) / (dd * dd));
         }
         mode = 3.0f;
-        c = phong_or_brdf<FULL>(LC, wo, dir, ret, m);
+        c = phong_or_brdf<BRDF>(LC, wo, dir, ret, m);
         break;
     }
     }
@@ -1607,7 +1607,7 @@ DEV DielSplit dielectric_split(const SceneView& sv, f3 d, const Ret& ret, const 
 
 constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour to the sample
 
-template <bool FULL, bool SPOT>
+template <bool FULL, bool SPOT, bool BRDF>
 __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                   uint64_t seed, const RayRec* __restrict__ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
@@ -1687,7 +1687,7 @@ __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const Came
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
-                        light_sample<FULL, SPOT>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
+                        light_sample<FULL, SPOT, BRDF>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         shadows[(size_t)i * sv.num_lights + li] = sr;
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
@@ -1705,7 +1705,7 @@ __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const Came
                         const float cosT = (flags & RTG_PT_IMPORTANCE) ? sqrtf(1.0f - xi[1]) : xi[1];
                         const float sinT = sqrtf(fmax0(1.0f - cosT * cosT));
                         const f3 wi = normalized((u * (sinT * f_cos(phi)) + nn * cosT) + bt * (sinT * f_sin(phi)));
-                        const f3 fc = phong_or_brdf<FULL>(mk(1, 1, 1), -d, wi, ret, m);
+                        const f3 fc = phong_or_brdf<BRDF>(mk(1, 1, 1), -d, wi, ret, m);
                         if (flags & RTG_PT_IMPORTANCE) w = cosT > 0.0f ? fc * ((float)PI_D / cosT) : mk(0, 0, 0);
                         else w = fc * (float)(2 * PI_D);
                         no = ret.point + nn * sv.shadow_eps;
@@ -1781,19 +1781,29 @@ __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const Came
 
 // L[slot] += T (x) v of every contributing vertex, one level at a time (stream order keeps
 // the oracle's per-sample summation order).  Level 0 starts the sum: L = (0,0,0) [+ T (x) v].
+// With several lights the in-order light sum of k_light_sum is folded in here.
 __global__ void __launch_bounds__(256) k_pt_gather(const NodeRec* __restrict__ nodes, const PathRec* __restrict__ paths,
+                                                   const ShadowRec* __restrict__ shadows, int nL,
                                                    NodeRec* __restrict__ level0, int level, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const NodeRec nd = nodes[i];
     const bool c = (nd.kind & kContrib) != 0;
+    f3 v = mk(nd.cr, nd.cg, nd.cb);
+    if (nL > 1 && (nd.kind & 0x100)) {          // Scene::RecursiveShading's col = ((amb + L0) + L1) + ...
+        for (int li = 0; li < nL; li++) {
+            const float4 sc = shadows[(size_t)i * nL + li].c;
+            const float lit = shadows[(size_t)i * nL + li].L.w;
+            v = v + ((sc.w != 0.0f && lit == 1.0f) ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));
+        }
+    }
     if (level == 0) {
         f3 L = mk(0, 0, 0);
-        if (c) L = L + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), mk(nd.cr, nd.cg, nd.cb));
+        if (c) L = L + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), v);
         level0[i].cr = L.x; level0[i].cg = L.y; level0[i].cb = L.z;
     } else if (c) {
         NodeRec& z = level0[nd.slot];
-        const f3 L = mk(z.cr, z.cg, z.cb) + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), mk(nd.cr, nd.cg, nd.cb));
+        const f3 L = mk(z.cr, z.cg, z.cb) + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), v);
         z.cr = L.x; z.cg = L.y; z.cb = L.z;
     }
 }
@@ -2056,14 +2066,14 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
                            shadows, slist, next_rays, next_meta, qcount, n);
 }
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st) {
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool light_sum) {
     if (n <= 0 || sv.num_lights == 0) return;
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
     if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
     else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
     else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
-    if (sv.num_lights > 1)
+    if (sv.num_lights > 1 && light_sum)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, shadows, nodes, n);
 }
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
@@ -2072,19 +2082,20 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
                      unsigned long long* qcount, int n, hipStream_t st) {
     if (n <= 0) return;
     dim3 g(nblk(n, 256)), b(256);
-    if (sv.full)
-        hipLaunchKernelGGL((k_pt_shade<true, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, nodes,
-                           shadows, slist, next_rays, next_meta, next_paths, qcount, n);
-    else if (sv.spot)
-        hipLaunchKernelGGL((k_pt_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, nodes,
-                           shadows, slist, next_rays, next_meta, next_paths, qcount, n);
-    else
-        hipLaunchKernelGGL((k_pt_shade<false, false>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths,
-                           nodes, shadows, slist, next_rays, next_meta, next_paths, qcount, n);
+#define RTG_PT_LAUNCH(F, S, B)                                                                                    \
+    hipLaunchKernelGGL((k_pt_shade<F, S, B>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, nodes, \
+                       shadows, slist, next_rays, next_meta, next_paths, qcount, n)
+    // textures / area / environment lights need the full variant; BRDFs alone do not
+    if (sv.full && !sv.brdf_only) RTG_PT_LAUNCH(true, true, true);
+    else if (sv.full) { if (sv.spot) RTG_PT_LAUNCH(false, true, true); else RTG_PT_LAUNCH(false, false, true); }
+    else if (sv.spot) RTG_PT_LAUNCH(false, true, false);
+    else RTG_PT_LAUNCH(false, false, false);
+#undef RTG_PT_LAUNCH
 }
-void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, NodeRec* level0, int level, int n, hipStream_t st) {
+void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
+                      int level, int n, hipStream_t st) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, nodes, paths, level0, level, n);
+    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, nodes, paths, shadows, nL, level0, level, n);
 }
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st) {
     if (n <= 0) return;

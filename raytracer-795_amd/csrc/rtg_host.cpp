@@ -933,9 +933,12 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.env_light = d->environment_light;
     // The simple shading variant compiles out texturing, BRDFs and area/environment lights.
     sv.full = d->num_textures > 0 || d->background_texture != -1 || d->environment_light != -1;
-    for (int i = 0; i < d->num_materials; i++) sv.full |= d->materials[i].brdf != RTG_BRDF_NONE;
     for (int i = 0; i < d->num_lights; i++)
         sv.full |= d->lights[i].type == RTG_LIGHT_AREA || d->lights[i].type == RTG_LIGHT_ENVIRONMENT;
+    int any_brdf = 0;
+    for (int i = 0; i < d->num_materials; i++) any_brdf |= d->materials[i].brdf != RTG_BRDF_NONE;
+    sv.brdf_only = !sv.full && any_brdf;
+    sv.full |= any_brdf;
     sv.spot = 0;
     for (int i = 0; i < d->num_lights; i++) sv.spot |= d->lights[i].type == RTG_LIGHT_SPOT;
     return RTG_OK;
@@ -1124,12 +1127,12 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
         launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
-                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st);
+                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt)
-            launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), ln.levels[0].nodes.as<NodeRec>(), level, n,
-                             ln.st);
+            launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), Lc.shadows.as<ShadowRec>(), nL,
+                             ln.levels[0].nodes.as<NodeRec>(), level, n, ln.st);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
         HIP_TRY(hipEventRecord(ln.ev_count, ln.st));

@@ -144,6 +144,7 @@ struct SceneView {
     int bg_texture, env_light;
     int full;                      // 0: no textures / BRDFs / area or environment lights
     int spot;                      // any spot light (its double-precision cone math is compiled in)
+    int brdf_only;                 // full only because of BRDFs (no textures / area / environment)
     // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
     // lights into num_lights)
     const int* top_emit;           // per top-level entry: emitter light index, -1 if not a light
@@ -236,12 +237,13 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
                   ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta,
                   unsigned long long* qcount, int n, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st);
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool light_sum = true);
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st);
-void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, NodeRec* level0, int level, int n, hipStream_t st);
+void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
+                      int level, int n, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
 void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);

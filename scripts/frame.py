@@ -8,7 +8,8 @@ import rtg  # noqa: E402
 from rtg import scenegen  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1
-sc = scenegen.dragon1m(1920, 1080, spp=64)
+w = os.environ.get("RTG_WORKLOAD", "dragon1m")      # any rtg.scenegen factory
+sc = getattr(scenegen, w)(1920, 1080, spp=int(os.environ.get("RTG_SPP", "256" if w == "cornell_pt" else "64")))
 r = rtg.Renderer(sc, 0)
 for _ in range(n):
     r.render(0)
