@@ -1027,7 +1027,13 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     if (npix_ll > (1LL << 30)) return fail(RTG_ERR_UNSUPPORTED, "image too large");
     int npix = (int)npix_ll;
     int total = cam->num_samples;
-    long long max_batch = o.max_batch_rays > 0 ? o.max_batch_rays : (8LL << 20);
+    // auto batch: 8M-ray passes, but at least one pass per stream in flight for small frames
+    // (a multi-GPU rank's row shard) so one pass's level tail overlaps another's work
+    // (1/8 of the 1080p64 dragon frame: 9.6 -> 9.0 ms with 5.5M-ray passes)
+    const int lanes_req = o.streams > 0 ? std::min(o.streams, 8) : s->num_lanes;
+    const long long frame_rays = (long long)npix * total;
+    long long max_batch = o.max_batch_rays > 0 ? o.max_batch_rays
+                        : std::min(8LL << 20, std::max(2LL << 20, frame_rays / std::max(1, lanes_req) + 1));
     // passes: all samples of a pixel range (chunks of samples only when spp exceeds the batch)
     const int ns_chunk = (int)std::max<long long>(1, std::min<long long>(total, max_batch));
     const int np_pass = (int)std::max<long long>(1, std::min<long long>(npix, max_batch / ns_chunk));
