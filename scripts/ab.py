@@ -1,0 +1,20 @@
+"""A/B of librtg variants (RTG_LIBRARY): median frame time at the default streams and the
+isolated trace / shadow kernel times (streams=1 timing frame).  usage: ab.py [workload]"""
+import json, os, statistics, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracer-795_amd"))
+import rtg
+from rtg import scenegen
+w = sys.argv[1] if len(sys.argv) > 1 else "dragon1m"
+sc = getattr(scenegen, w)(1920, 1080, spp=256 if w == "cornell_pt" else 64)
+r = rtg.Renderer(sc, 0)
+r.render(0)
+ms = []
+for _ in range(int(os.environ.get("AB_FRAMES", "5"))):
+    r.render(0)
+    ms.append(r.stats()["render_ms"])
+r.render(0, collect_timing=1, streams=1)
+st = r.stats()
+print(json.dumps({"lib": os.environ.get("RTG_LIBRARY", "librtg"), "workload": w, "frame_ms": round(statistics.median(ms), 2),
+                  "frames": [round(x, 2) for x in ms], "trace_ms": round(st["trace_ms"], 2),
+                  "shadow_ms": round(st["shadow_ms"], 2), "streams1_ms": round(st["render_ms"], 2)}), flush=True)
