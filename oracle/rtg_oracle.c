@@ -1302,10 +1302,12 @@ static v3 emitter_shading(Ctx* cx, int k, const Ray* prime, const RetVal* ret, c
         float cosl = fabsf(vdot(wi, nl));
         LC = vmul(E->Le, (cosl * E->area) / (dist * dist));
     }
+    v3 c = surface_response(LC, wo, wi, ret, m);
+    if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return V(0, 0, 0);   /* nothing to shadow: no ray */
     Ray ray = R(vadd(p, vmul(ret->normal, s->shadowEps)), wi, prime->time);
     RetVal nr = trace(cx, &ray, 2);
     if (nr.full && vnorm(vsub(p, nr.point)) < dist - (s->shadowEps + 1e-4f * dist)) return V(0, 0, 0);
-    return surface_response(LC, wo, wi, ret, m);
+    return c;
 }
 
 static v3 pt_sample(Ctx* cx, Ray ray, int flags, v3 bg) {

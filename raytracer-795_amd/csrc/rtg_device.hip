@@ -315,6 +315,19 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 }
             }
         } else {
+            // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
+            // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
+            // send every box to the exact division test instead.
+            const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
+            const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
+                              adz <= 1e30f;
+            const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
+            // the root box first: an object whose root the line misses costs no further setup
+            // (small scenes are dominated by the reference's linear loop over objects)
+            const bool root_ok = g.node_base < 0 ? g.root_leaf_count > 0
+                               : box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
+                                         g.root_max[1], g.root_max[2]);
+            if (!root_ok) continue;
             // distance bound from the best hit so far (see DESIGN.md "pruning")
             float boundD = FLT_MAX;
             const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
@@ -337,20 +350,13 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 const float pad = g.prune_pad;
                 float best_d = FLT_MAX;
                 int best_leaf = -1;
-                // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
-                // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
-                // send every box to the exact division test instead.
-                const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
-                const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
-                                  adz <= 1e30f;
-                const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
                 // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
                 // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
                 // skipped when its box, expanded by `pad`, meets the line only outside that window.
                 const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
                 const float tlo = -(fabsf(eps) + 1e-6f);
                 const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
-                const float inv_dn = 1.0f / dnorm;
+                const float inv_dn = __builtin_amdgcn_rcpf(dnorm);   // 1 ulp: inside the 2e-5 margins of thi
                 float thi = INFINITY;
                 if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
                 const float tm_global = thi;
@@ -398,8 +404,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 if (g.node_base < 0) {
                     for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
                         test_prim(sv.tris[k], k, g.root_leaf_start);
-                } else if (box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
-                                   g.root_max[1], g.root_max[2])) {
+                } else {                // root box already hit (root_ok)
                     // Leaf children are resolved as soon as they are reached.
                     auto leaf = [&](int start, int count) {
 #ifndef RTG_DBG_NOLEAF
@@ -1218,8 +1223,10 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
             const float cosl = fabsf(dot(dir, nl));
             LC = ld3(L.inten) * ((cosl * L.coverage) / (dd * dd));
         }
-        mode = 3.0f;
         c = phong_or_brdf<BRDF>(LC, wo, dir, ret, m);
+        // a sample that contributes exactly zero (light behind the surface) needs no shadow ray:
+        // blocked or not it adds 0 (oracle emitter_shading does the same)
+        mode = (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) ? 0.0f : 3.0f;
         break;
     }
     }
