@@ -117,3 +117,24 @@ def test_reference_integrator_ignores_object_lights(gpu):
     linf, _, nanm = _cmp(img, ref)
     assert nanm == 0
     assert linf < TOL
+
+
+@pytest.mark.parametrize("name,make", [
+    ("textured", lambda: scenegen.textured(32, 24, spp=2)),          # textures, BRDFs, spot + directional
+    ("cornell_area_dof", lambda: scenegen.cornell(32, 24, spp=4)),   # area light, instances, blur, DoF
+    ("multilight", lambda: scenegen.multilight(32, 24, spp=2)),      # spots, rough mirror, conductor, glass
+])
+@pytest.mark.parametrize("flags", [I | N | R, 0])
+def test_path_trace_full_variant_matches_oracle(gpu, name, make, flags):
+    """The reference scenes path traced (classical lights as BasicShading at every vertex):
+    the full k_pt_shade specialisation (textures / area light / every material type)."""
+    sc = make()
+    sc.cameras[0].integrator = A.INTEGRATOR_PATH
+    sc.cameras[0].pt_flags = flags
+    with rtg.Renderer(sc, device=gpu) as r:
+        img = r.render(0)
+    ref, _, _, _ = pyoracle.Oracle(sc).render(0)
+    linf, frac, nanm = _cmp(img, ref)
+    print(f"{name} flags={flags}: Linf={linf:.3g} differing={frac:.2e}")
+    assert nanm == 0
+    assert linf < TOL
