@@ -307,6 +307,24 @@ int32_t rtg_render_device(rtg_scene* scene, const rtg_camera_desc* cam,
                           const rtg_render_opts* opts, float* rgb_out_device, void* stream);
 int32_t rtg_last_render_stats(const rtg_scene* scene, rtg_render_stats* out);
 
+/* hw5 tone mapping (pages/Page5.md:47-53 describes a global operator; src/ has none): the
+   Photographic TMO of DESIGN.md §11, from a camera's <Tonemap> (<TMO>Photographic</TMO>
+   <TMOOptions>key burn%</TMOOptions> <Saturation> <Gamma>).  Output: 0..255 floats, [y][x][c]. */
+typedef enum rtg_tmo { RTG_TMO_PHOTOGRAPHIC = 0 } rtg_tmo;
+typedef struct rtg_tonemap_desc {
+    int32_t tmo;             /* rtg_tmo */
+    float key;               /* TMOOptions[0], e.g. 0.18 */
+    float burn_percent;      /* TMOOptions[1]: percentage of the brightest pixels that saturate */
+    float saturation;
+    float gamma;
+} rtg_tonemap_desc;
+/* hdr_rgb / ldr_rgb: host arrays of ny*nx*3 floats; the work runs on HIP device `device`. */
+int32_t rtg_tonemap(int32_t device, const float* hdr_rgb, int32_t nx, int32_t ny, const rtg_tonemap_desc* tm,
+                    float* ldr_rgb);
+/* Same on device arrays, enqueued on `stream` (hipStream_t); synchronous on return. */
+int32_t rtg_tonemap_device(int32_t device, const float* hdr_rgb_device, int32_t nx, int32_t ny,
+                           const rtg_tonemap_desc* tm, float* ldr_rgb_device, void* stream);
+
 /* Batch closest-hit query (BVHMethods::FindIntersection) over host arrays. */
 int32_t rtg_trace_closest(rtg_scene* scene, const rtg_ray* rays, int32_t n, rtg_hit* hits,
                           int32_t traversal);

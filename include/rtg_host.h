@@ -32,6 +32,8 @@ const rtg_scene_desc* rtgh_scene_desc(const rtgh_scene* scene);
 int32_t rtgh_num_cameras(const rtgh_scene* scene);
 /* Camera i; image_name receives the <ImageName> (truncated to cap-1 bytes). */
 int32_t rtgh_camera(const rtgh_scene* scene, int32_t i, rtg_camera_desc* out, char* image_name, int32_t cap);
+/* Camera i's hw5 <Tonemap> (Photographic TMO): 1 and *out filled if present, 0 if not. */
+int32_t rtgh_camera_tonemap(const rtgh_scene* scene, int32_t i, rtg_tonemap_desc* out);
 void rtgh_free(rtgh_scene* scene);
 
 /* rgb: ny*nx*3 floats [y][x][c] (Image::_data). */

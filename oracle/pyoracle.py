@@ -43,6 +43,8 @@ def load():
         lib.orc_object_matrices.restype = C.c_int
         lib.orc_vertex_normals.argtypes = [C.c_void_p, A.PF]
         lib.orc_vertex_normals.restype = C.c_int
+        lib.orc_tonemap.argtypes = [A.PF, C.c_int, C.c_int, C.POINTER(A.TonemapDesc), A.PF]
+        lib.orc_tonemap.restype = C.c_int
         lib.orc_rng_uniform.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
                                         C.c_uint32, C.c_int]
         lib.orc_rng_uniform.restype = C.c_float
@@ -140,3 +142,16 @@ def philox4x32_10(ctr, key):
     o = (C.c_uint32 * 4)()
     f(c, k, o)
     return list(o)
+
+
+def tonemap(hdr, key=0.18, burn=1.0, saturation=1.0, gamma=2.2):
+    """orc_tonemap: the CPU restatement of the Photographic TMO (0..255 floats)."""
+    lib = load()
+    a = np.ascontiguousarray(hdr, np.float32)
+    out = np.zeros_like(a)
+    tm = A.TonemapDesc(A.TMO_PHOTOGRAPHIC, key, burn, saturation, gamma)
+    rc = lib.orc_tonemap(a.ctypes.data_as(A.PF), a.shape[1], a.shape[0], C.byref(tm), out.ctypes.data_as(A.PF))
+    if rc != 0:
+        raise RuntimeError(f"orc_tonemap failed: {rc}")
+    return out
+

@@ -1806,3 +1806,53 @@ int orc_vertex_normals(const orc_scene* s, float* normals) {
     }
     return RTG_OK;
 }
+
+/* ------------------------------------------------------------------ hw5 tone mapping
+ * pages/Page5.md:47-53 describes a global operator; src/ has no code.  The Photographic TMO
+ * of DESIGN.md §11 (Reinhard et al. 2002, global), restated plainly: luminance, log-average in
+ * double (index order), scale, burn rank by sorting, Reinhard curve, saturation, gamma. */
+static float tm_lum(const float* c) {
+    float y = (0.2126f * c[0] + 0.7152f * c[1]) + 0.0722f * c[2];
+    return (isfinite(y) && y > 0.0f) ? y : 0.0f;
+}
+static int cmp_f(const void* a, const void* b) {
+    float x = *(const float*)a, y = *(const float*)b;
+    return (x > y) - (x < y);
+}
+int orc_tonemap(const float* hdr, int nx, int ny, const rtg_tonemap_desc* tm, float* out) {
+    if (!hdr || !out || !tm || nx < 1 || ny < 1) return RTG_ERR_INVALID;
+    size_t n = (size_t)nx * ny;
+    float* Y = (float*)malloc(sizeof(float) * n);
+    float* L = (float*)malloc(sizeof(float) * n);
+    double sum = 0.0;
+    for (size_t i = 0; i < n; i++) { Y[i] = tm_lum(hdr + 3 * i); sum += log(1e-5 + (double)Y[i]); }
+    double lw = exp(sum / (double)n);
+    float k = (float)((double)tm->key / lw);
+    for (size_t i = 0; i < n; i++) L[i] = k * Y[i];
+    qsort(L, n, sizeof(float), cmp_f);
+    size_t widx = n - 1;
+    if (tm->burn_percent > 0.0f) {
+        double f = 1.0 - (double)tm->burn_percent / 100.0;
+        if (f < 0.0) f = 0.0;
+        long long idx = (long long)floor((double)(n - 1) * f);
+        widx = idx < 0 ? 0 : (idx > (long long)n - 1 ? n - 1 : (size_t)idx);
+    }
+    float white = L[widx];
+    double ig = 1.0 / (double)tm->gamma;
+    for (size_t i = 0; i < n; i++) {
+        float y = Y[i], l = k * y;
+        float ld = white > 0.0f ? (l * (1.0f + l / (white * white))) / (1.0f + l) : l / (1.0f + l);
+        for (int c = 0; c < 3; c++) {
+            float v = 0.0f;
+            if (y > 0.0f) {
+                float ch = hdr[3 * i + c] > 0.0f ? hdr[3 * i + c] : 0.0f;
+                v = ld * (float)pow((double)(ch / y), (double)tm->saturation);
+            }
+            v = v > 0.0f ? (v < 1.0f ? v : 1.0f) : 0.0f;
+            out[3 * i + c] = 255.0f * (float)pow((double)v, ig);
+        }
+    }
+    free(Y); free(L);
+    return RTG_OK;
+}
+

@@ -41,6 +41,9 @@ int orc_object_bvh(const orc_scene* s, int object, int32_t* num_prims, int32_t* 
 int orc_object_matrices(const orc_scene* s, int top_object, float* inv16, float* invT16);
 int orc_vertex_normals(const orc_scene* s, float* normals);
 
+/* hw5 Photographic tone mapping: hdr/out ny*nx*3 floats, out 0..255. */
+int orc_tonemap(const float* hdr, int nx, int ny, const rtg_tonemap_desc* tm, float* out);
+
 /* Raw Philox4x32-10 block (checked against the Random123 known-answer vectors). */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* Philox4x32-10 uniform draw shared bit-for-bit with the device code (for tests). */

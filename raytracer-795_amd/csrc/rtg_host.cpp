@@ -1272,6 +1272,49 @@ int32_t rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_op
     return rc;
 }
 
+static int check_tonemap(int32_t device, int32_t nx, int32_t ny, const rtg_tonemap_desc* tm) {
+    if (!tm) return fail(RTG_ERR_INVALID, "null tonemap descriptor");
+    if (tm->tmo != RTG_TMO_PHOTOGRAPHIC) return fail(RTG_ERR_UNSUPPORTED, "tone-mapping operator");
+    if (!(tm->gamma > 0.0f) || !(tm->key > 0.0f) || !(tm->burn_percent >= 0.0f) || !(tm->burn_percent <= 100.0f))
+        return fail(RTG_ERR_INVALID, "tonemap parameters");
+    if (nx < 1 || ny < 1 || (long long)nx * ny > (1LL << 30)) return fail(RTG_ERR_INVALID, "tonemap image size");
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return fail(RTG_ERR_NO_DEVICE, "no such device");
+    return RTG_OK;
+}
+
+int32_t rtg_tonemap_device(int32_t device, const float* hdr, int32_t nx, int32_t ny, const rtg_tonemap_desc* tm,
+                           float* out, void* stream) {
+    if (!hdr || !out) return fail(RTG_ERR_INVALID, "null argument");
+    int rc = check_tonemap(device, nx, ny, tm);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(device));
+    std::string err;
+    if (tonemap_device(hdr, nx, ny, *tm, out, (hipStream_t)stream, err)) return fail(RTG_ERR_HIP, err);
+    return RTG_OK;
+}
+
+int32_t rtg_tonemap(int32_t device, const float* hdr, int32_t nx, int32_t ny, const rtg_tonemap_desc* tm, float* out) {
+    if (!hdr || !out) return fail(RTG_ERR_INVALID, "null argument");
+    int rc = check_tonemap(device, nx, ny, tm);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(device));
+    const size_t bytes = sizeof(float) * 3 * (size_t)nx * ny;
+    float *dh = nullptr, *dl = nullptr;
+    if (hipMalloc(&dh, bytes) != hipSuccess || hipMalloc(&dl, bytes) != hipSuccess) {
+        if (dh) (void)hipFree(dh);
+        return fail(RTG_ERR_OOM, "tonemap buffers");
+    }
+    std::string err;
+    rc = RTG_OK;
+    if (hipMemcpy(dh, hdr, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = fail(RTG_ERR_HIP, "tonemap upload");
+    else if (tonemap_device(dh, nx, ny, *tm, dl, nullptr, err)) rc = fail(RTG_ERR_HIP, err);
+    else if (hipMemcpy(out, dl, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RTG_ERR_HIP, "tonemap download");
+    (void)hipFree(dh);
+    (void)hipFree(dl);
+    return rc;
+}
+
 int32_t rtg_scene_build_stats(const rtg_scene* s, rtg_build_stats* out) {
     if (!s || !out) return fail(RTG_ERR_INVALID, "null argument");
     out->bvh_build_ms = s->bvh_build_ms;

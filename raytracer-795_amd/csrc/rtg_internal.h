@@ -252,6 +252,11 @@ void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offse
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st);
 
+// Photographic tone mapping (rtg_tonemap.hip); hdr / out are device arrays.
+int tonemap_white_index(int n, float burn_percent);
+int tonemap_device(const float* hdr, int nx, int ny, const rtg_tonemap_desc& tm, float* out, hipStream_t st,
+                   std::string& err);
+
 // GPU BVH construction (rtg_bvh_gpu.hip): the reference median-split tree of one object.
 // nodes: breadth-first {left, right, start, end} (children -1: none); box: 6 floats per node
 // (min xyz, max xyz); perm: BVH position -> original primitive.  Inputs must be finite.

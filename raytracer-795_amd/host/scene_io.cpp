@@ -56,6 +56,8 @@ struct InstData {
 struct CamData {
     rtg_camera_desc d{};
     std::string image_name;
+    bool has_tonemap = false;
+    rtg_tonemap_desc tm{};
 };
 
 // ------------------------------------------------------------------ text helpers (tinyxml2 / libc)
@@ -496,6 +498,24 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
                 const float y = (float)tan((double)fovr) * d.near_distance;
                 const float x = aspect * y;
                 d.left = -x; d.right = x; d.bottom = -y; d.top = y;
+            }
+            // hw5 <Tonemap> (pages/Page5.md:47-53; no parser code in src/): Photographic TMO
+            if (const rtgh::XmlElement* tm = ce->child("Tonemap")) {
+                const char* tmo = child_text(tm, "TMO");
+                std::string t = lower(tmo ? tmo : "photographic");
+                size_t a = t.find_first_not_of(" \t\r\n");
+                if (a != std::string::npos && t.compare(a, 12, "photographic") == 0) {
+                    c.has_tonemap = true;
+                    c.tm.tmo = RTG_TMO_PHOTOGRAPHIC;
+                    c.tm.key = 0.18f; c.tm.burn_percent = 1.0f;
+                    if (const char* o = child_text(tm, "TMOOptions")) {
+                        c.tm.key = c.tm.burn_percent = 0.0f;
+                        sscanf(o, "%f %f", &c.tm.key, &c.tm.burn_percent);
+                    }
+                    c.tm.saturation = 1.0f; c.tm.gamma = 2.2f;
+                    query_float(child_text(tm, "Saturation"), c.tm.saturation);
+                    query_float(child_text(tm, "Gamma"), c.tm.gamma);
+                }
             }
             // hw7 (pages/Page7.md): <Renderer>PathTracing</Renderer>, <RendererParams>
             if (const char* r = child_text(ce, "Renderer")) {
@@ -948,6 +968,13 @@ int32_t rtgh_camera(const rtgh_scene* s, int32_t i, rtg_camera_desc* out, char* 
     return RTG_OK;
 }
 
+int32_t rtgh_camera_tonemap(const rtgh_scene* s, int32_t i, rtg_tonemap_desc* out) {
+    if (!s || !out || i < 0 || i >= (int32_t)s->cameras.size()) return fail(RTG_ERR_INVALID, "camera index");
+    if (!s->cameras[i].has_tonemap) return 0;
+    *out = s->cameras[i].tm;
+    return 1;
+}
+
 void rtgh_free(rtgh_scene* s) { delete s; }
 
 int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t ny) {
@@ -1033,8 +1060,22 @@ int32_t rtgh_render_scene(const char* xml_path, int32_t device, uint64_t seed, c
             const size_t s = name.rfind('/');
             name = std::string(out_dir) + "/" + (s == std::string::npos ? name : name.substr(s + 1));
         }
-        rc = rtgh_save_image(name.c_str(), rgb.data(), c.d.nx, c.d.ny);
-        if (rc) break;
+        // hw5 <Tonemap>: the tone-mapped image goes to the name with a .png extension (a .png
+        // ImageName is written tone-mapped instead of clamped), the HDR one to ImageName
+        const bool png = is_png(name.c_str());
+        if (!c.has_tonemap || !png) {
+            rc = rtgh_save_image(name.c_str(), rgb.data(), c.d.nx, c.d.ny);
+            if (rc) break;
+        }
+        if (c.has_tonemap) {
+            std::vector<float> ldr(rgb.size());
+            rc = rtg_tonemap(device, rgb.data(), c.d.nx, c.d.ny, &c.tm, ldr.data());
+            if (rc) { g_err = rtg_last_error(); break; }
+            const size_t dot = name.rfind('.'), sl = name.rfind('/');
+            const std::string tname = (dot == std::string::npos || (sl != std::string::npos && dot < sl) ? name : name.substr(0, dot)) + ".png";
+            rc = rtgh_save_image(tname.c_str(), ldr.data(), c.d.nx, c.d.ny);
+            if (rc) break;
+        }
         rtg_render_stats st{};
         rtg_last_render_stats(gpu, &st);
         printf("%s: %.1f ms, %.1f Mray/s\n", name.c_str(), st.render_ms, st.total_rays / (st.render_ms * 1e3));

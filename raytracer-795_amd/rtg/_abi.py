@@ -134,6 +134,14 @@ class BuildStats(C.Structure):
 RTG_BVH_AUTO, RTG_BVH_HOST, RTG_BVH_GPU = 0, 1, 2
 
 
+class TonemapDesc(C.Structure):
+    _fields_ = [("tmo", C.c_int32), ("key", C.c_float), ("burn_percent", C.c_float), ("saturation", C.c_float),
+                ("gamma", C.c_float)]
+
+
+TMO_PHOTOGRAPHIC = 0
+
+
 class Hit(C.Structure):
     _fields_ = [("full", C.c_int32), ("object", C.c_int32), ("prim", C.c_int32), ("material", C.c_int32),
                 ("t", C.c_float), ("point", F3), ("normal", F3)]
@@ -153,6 +161,9 @@ EXPORTS = {
     "rtg_render_device": (C.c_int32, [C.c_void_p, C.POINTER(CameraDesc), C.POINTER(RenderOpts), C.c_void_p,
                                       C.c_void_p]),
     "rtg_last_render_stats": (C.c_int32, [C.c_void_p, C.POINTER(RenderStats)]),
+    "rtg_tonemap": (C.c_int32, [C.c_int32, PF, C.c_int32, C.c_int32, C.POINTER(TonemapDesc), PF]),
+    "rtg_tonemap_device": (C.c_int32, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(TonemapDesc), C.c_void_p,
+                                       C.c_void_p]),
     "rtg_trace_closest": (C.c_int32, [C.c_void_p, C.POINTER(Ray), C.c_int32, C.POINTER(Hit), C.c_int32]),
     "rtg_scene_object_bvh": (C.c_int32, [C.c_void_p, C.c_int32, PI, PI, PI, PI, PF]),
     "rtg_scene_object_matrices": (C.c_int32, [C.c_void_p, C.c_int32, PF, PF]),

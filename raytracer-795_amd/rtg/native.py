@@ -31,6 +31,8 @@ def load():
         lib.rtgh_num_cameras.restype = C.c_int32
         lib.rtgh_camera.argtypes = [C.c_void_p, C.c_int32, C.POINTER(A.CameraDesc), C.c_char_p, C.c_int32]
         lib.rtgh_camera.restype = C.c_int32
+        lib.rtgh_camera_tonemap.argtypes = [C.c_void_p, C.c_int32, C.POINTER(A.TonemapDesc)]
+        lib.rtgh_camera_tonemap.restype = C.c_int32
         lib.rtgh_free.argtypes = [C.c_void_p]
         lib.rtgh_free.restype = None
         lib.rtgh_save_image.argtypes = [C.c_char_p, A.PF, C.c_int32, C.c_int32]
@@ -61,6 +63,11 @@ class NativeScene:
             name = C.create_string_buffer(4096)
             _check(self.lib.rtgh_camera(h, i, C.byref(cd), name, 4096))
             self.cameras.append((cd, name.value.decode()))
+        self.tonemaps = []
+        for i in range(len(self.cameras)):
+            tm = A.TonemapDesc()
+            has = self.lib.rtgh_camera_tonemap(h, i, C.byref(tm))
+            self.tonemaps.append((tm.key, tm.burn_percent, tm.saturation, tm.gamma) if has == 1 else None)
 
     def close(self):
         if getattr(self, "handle", None):

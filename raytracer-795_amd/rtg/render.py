@@ -212,13 +212,36 @@ def save_image(name: str, rgb: np.ndarray) -> str:
     return name
 
 
+def tonemap(img: np.ndarray, key=0.18, burn=1.0, saturation=1.0, gamma=2.2, device: int = 0) -> np.ndarray:
+    """hw5 Photographic tone mapping on the GPU (rtg_tonemap): 0..255 floats."""
+    lib = A.load_library()
+    a = np.ascontiguousarray(img, np.float32)
+    out = np.zeros_like(a)
+    tm = A.TonemapDesc(A.TMO_PHOTOGRAPHIC, key, burn, saturation, gamma)
+    A.check(lib.rtg_tonemap(device, a.ctypes.data_as(A.PF), a.shape[1], a.shape[0], C.byref(tm),
+                            out.ctypes.data_as(A.PF)), lib)
+    return out
+
+
+def tonemapped_name(name: str) -> str:
+    """Where a camera's tone-mapped image goes: its ImageName with the extension set to .png."""
+    stem, _ = os.path.splitext(name)
+    return stem + ".png"
+
+
 def render_scene(scene: Scene, out_dir: str | None = None, device: int = 0, seed: int = DEFAULT_SEED) -> list:
-    """Scene::renderScene (src/Scene.cpp:425-494): every camera rendered and saved."""
+    """Scene::renderScene (src/Scene.cpp:425-494): every camera rendered and saved.  A camera
+    with a hw5 <Tonemap> also gets its tone-mapped image (tonemapped_name; a .png ImageName is
+    written tone-mapped instead of clamped)."""
     written = []
     print("BVH construction complete.")
     with Renderer(scene, device) as r:
         for cam in scene.cameras:
             img = r.render(cam, seed=seed)
             name = cam.image_name if out_dir is None else os.path.join(out_dir, os.path.basename(cam.image_name))
-            written.append(save_image(name, img))
+            tm = None if cam.tonemap is None else tonemap(img, *cam.tonemap, device=device)
+            if tm is None or not _is_png(name):
+                written.append(save_image(name, img))
+            if tm is not None:
+                written.append(save_image(tonemapped_name(name), tm))
     return written

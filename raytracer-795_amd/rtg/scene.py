@@ -60,6 +60,7 @@ class Camera:                       # src/Camera.h, src/Parser.h:52-164
     left_handed: bool = False
     integrator: int = A.INTEGRATOR_REFERENCE     # hw7 <Renderer>PathTracing</Renderer>
     pt_flags: int = 0                            # hw7 <RendererParams> (A.PT_*)
+    tonemap: tuple | None = None                 # hw5 <Tonemap>: (key, burn %, saturation, gamma)
     # XML-only conveniences kept for write_xml round trips
     gaze_point: np.ndarray | None = None
     fov_y: float | None = None
@@ -552,6 +553,14 @@ def parse_xml(xml_path: str) -> Scene:
             y = f32(f32(math.tan(float(fovr))) * f32(cam.near_distance))
             x = f32(aspect * y)
             cam.near_plane = (float(-x), float(x), float(-y), float(y))
+        # hw5 <Tonemap> (pages/Page5.md:47-53; no parser code in src/): Photographic TMO only
+        tm = ce.find("Tonemap")
+        if tm is not None and (_text(tm, "TMO") or "Photographic").strip().lower().startswith("photographic"):
+            opts = [float(f32(float(v))) for v in (_text(tm, "TMOOptions") or "0.18 1").split()[:2]]
+            while len(opts) < 2:
+                opts.append(0.0)
+            cam.tonemap = (opts[0], opts[1], _query_float(_text(tm, "Saturation"), 1.0),
+                           _query_float(_text(tm, "Gamma"), float(f32(2.2))))
         # hw7 (pages/Page7.md; the reference parser has no such tags): <Renderer>PathTracing</Renderer>
         # and <RendererParams>ImportanceSampling NextEventEstimation RussianRoulette</RendererParams>
         ren = _text(ce, "Renderer")
@@ -878,6 +887,10 @@ def write_xml(sc: Scene, xml_path: str, images: dict | None = None) -> str:
             out.append(f"<FocusDistance>{_fmt(c.focus_distance)}</FocusDistance>")
             out.append(f"<ApertureSize>{_fmt(c.aperture_size)}</ApertureSize>")
         out.append(f"<ImageName>{c.image_name}</ImageName>")
+        if c.tonemap is not None:
+            k, b, sat, g = c.tonemap
+            out.append(f"<Tonemap><TMO>Photographic</TMO><TMOOptions>{_fmt(k)} {_fmt(b)}</TMOOptions>"
+                       f"<Saturation>{_fmt(sat)}</Saturation><Gamma>{_fmt(g)}</Gamma></Tonemap>")
         if c.integrator == A.INTEGRATOR_PATH:
             out.append("<Renderer>PathTracing</Renderer>")
             toks = [n for f, n in ((A.PT_IMPORTANCE, "ImportanceSampling"), (A.PT_NEE, "NextEventEstimation"),

@@ -38,9 +38,9 @@ def test_library_exports_every_declared_symbol(lib):
 def test_struct_layouts_match_c():
     structs = ["rtg_xform_ref", "rtg_object_desc", "rtg_instance_desc", "rtg_material_desc", "rtg_texture_desc",
                "rtg_light_desc", "rtg_scene_desc", "rtg_camera_desc", "rtg_render_opts", "rtg_render_stats",
-               "rtg_ray", "rtg_hit", "rtg_build_opts", "rtg_build_stats"]
+               "rtg_ray", "rtg_hit", "rtg_build_opts", "rtg_build_stats", "rtg_tonemap_desc"]
     py = [A.XformRef, A.ObjectDesc, A.InstanceDesc, A.MaterialDesc, A.TextureDesc, A.LightDesc, A.SceneDesc,
-          A.CameraDesc, A.RenderOpts, A.RenderStats, A.Ray, A.Hit, A.BuildOpts, A.BuildStats]
+          A.CameraDesc, A.RenderOpts, A.RenderStats, A.Ray, A.Hit, A.BuildOpts, A.BuildStats, A.TonemapDesc]
     body = "\n".join(f'printf("%zu\\n", sizeof({s}));' for s in structs)
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "s.c")

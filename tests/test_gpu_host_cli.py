@@ -46,3 +46,19 @@ def test_cli_exr_output(gpu, tmp_path):
         img = r.render(0)
     from rtg.render import exr_half_bytes
     assert (tmp_path / "pt.exr").read_bytes() == exr_half_bytes(img)
+
+
+def test_cli_tonemap_outputs(gpu, tmp_path):
+    """A camera with a hw5 <Tonemap>: the HDR image under its ImageName and the tone-mapped
+    one next to it as .png, identical between the native and the Python host."""
+    sc = scenegen.cornell_pt(32, 24, spp=2)
+    sc.cameras[0].image_name = "tm.exr"
+    sc.cameras[0].tonemap = (0.18, 1.0, 1.0, 2.2)
+    xml = write_xml(sc, str(tmp_path / "tm.xml"))
+    cli_dir, py_dir = tmp_path / "cli", tmp_path / "py"
+    cli_dir.mkdir()
+    py_dir.mkdir()
+    native.render_scene(xml, device=gpu, out_dir=str(cli_dir))
+    rtg.render_scene(parse_xml(xml), out_dir=str(py_dir), device=gpu)
+    for f in ("tm.exr", "tm.png"):
+        assert (cli_dir / f).read_bytes() == (py_dir / f).read_bytes(), f

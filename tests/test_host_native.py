@@ -39,9 +39,12 @@ def _compare(xml):
     with native.NativeScene(xml) as ns:
         _eq(native.desc_to_dict(d_py), native.desc_to_dict(ns.desc))
         assert len(ns.cameras) == len(py.cameras)
-        for (cd, name), cam in zip(ns.cameras, py.cameras):
+        for (cd, name), tm, cam in zip(ns.cameras, ns.tonemaps, py.cameras):
             assert name == cam.image_name
             assert bytes(cd) == bytes(cam.desc())
+            assert (tm is None) == (cam.tonemap is None)
+            if tm is not None:
+                assert np.array_equal(np.float32(tm), np.float32(cam.tonemap))
     return py
 
 
@@ -52,7 +55,13 @@ SCENES = {
     "cornell": lambda: scenegen.cornell(16, 12, spp=4),
     "multilight": lambda: scenegen.multilight(16, 12),
     "cornell_pt": lambda: scenegen.cornell_pt(16, 12, spp=4),
+    "cornell_pt_tonemap": lambda: _with_tonemap(scenegen.cornell_pt(16, 12, spp=4)),
 }
+
+
+def _with_tonemap(sc):
+    sc.cameras[0].tonemap = (0.18, 1.5, 0.9, 2.2)
+    return sc
 
 
 @pytest.mark.parametrize("name", list(SCENES))
@@ -184,7 +193,7 @@ def test_host_library_exports_every_declared_symbol():
     hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rtg_host.h")
     decl = set(re.findall(r"^\s*(?:int32_t|const char\*|void|const rtg_scene_desc\*)\s+(rtgh_\w+)\s*\(",
                           open(hdr).read(), re.M))
-    assert len(decl) == 8
+    assert len(decl) == 9
     out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], capture_output=True, text=True, check=True)
     syms = set(re.findall(r"\sT\s(rtgh_\w+)", out.stdout))
     assert decl <= syms, decl - syms
