@@ -36,6 +36,13 @@ int32_t rtgh_camera(const rtgh_scene* scene, int32_t i, rtg_camera_desc* out, ch
 int32_t rtgh_camera_tonemap(const rtgh_scene* scene, int32_t i, rtg_tonemap_desc* out);
 void rtgh_free(rtgh_scene* scene);
 
+/* Decode an image texture the way the reference's Texture constructor sees it
+   (src/Texture.cpp:7-21, 41-74): *rgb = malloc'd ny*nx*3 floats [y][x][c], raw 0..255 for
+   PNG/JPEG/PPM, linear floats for OpenEXR (LoadEXR's R,G,B, src/Helper.cpp:346-359).
+   Release with rtgh_free_image. */
+int32_t rtgh_read_image(const char* path, float** rgb, int32_t* nx, int32_t* ny);
+void rtgh_free_image(float* rgb);
+
 /* rgb: ny*nx*3 floats [y][x][c] (Image::_data). */
 int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t ny);
 

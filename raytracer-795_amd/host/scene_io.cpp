@@ -32,6 +32,7 @@
 #include <jpeglib.h>
 #endif
 
+#include "exr_read.hpp"
 #include "xml.hpp"
 
 namespace {
@@ -409,6 +410,15 @@ bool ends_with(const std::string& s, const char* t) { size_t k = strlen(t); retu
 int load_image(const std::string& path, std::vector<float>& px, int& w, int& h) {
     const std::string l = lower(path);
     if (ends_with(l, ".ppm") || ends_with(l, ".pnm")) return read_ppm(path, px, w, h);
+    if (ends_with(l, ".exr")) {             // Texture::ReadExr (src/Texture.cpp:185-189): linear floats
+        std::vector<float> rgba;
+        std::string e;
+        if (!rtgh::read_exr_rgba(path, rgba, w, h, e)) return fail(RTG_ERR_INVALID, e);
+        px.resize((size_t)w * h * 3);
+        for (size_t i = 0; i < (size_t)w * h; i++)
+            for (int c = 0; c < 3; c++) px[3 * i + c] = rgba[4 * i + c];
+        return RTG_OK;
+    }
 #ifdef RTGH_HAVE_PNG
     if (ends_with(l, ".png")) return read_png(path, px, w, h);
 #endif
@@ -976,6 +986,24 @@ int32_t rtgh_camera_tonemap(const rtgh_scene* s, int32_t i, rtg_tonemap_desc* ou
 }
 
 void rtgh_free(rtgh_scene* s) { delete s; }
+
+int32_t rtgh_read_image(const char* path, float** rgb, int32_t* nx, int32_t* ny) {
+    if (!path || !rgb || !nx || !ny) return fail(RTG_ERR_INVALID, "null argument");
+    *rgb = nullptr;
+    std::vector<float> px;
+    int w = 0, h = 0;
+    int rc = load_image(path, px, w, h);
+    if (rc) return rc;
+    float* out = (float*)malloc(sizeof(float) * (px.empty() ? 1 : px.size()));
+    if (!out) return fail(RTG_ERR_OOM, "host allocation");
+    memcpy(out, px.data(), sizeof(float) * px.size());
+    *rgb = out;
+    *nx = w;
+    *ny = h;
+    return RTG_OK;
+}
+
+void rtgh_free_image(float* rgb) { free(rgb); }
 
 int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t ny) {
     if (!name || !rgb || nx < 1 || ny < 1) return fail(RTG_ERR_INVALID, "bad image");

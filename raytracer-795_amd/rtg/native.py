@@ -39,6 +39,10 @@ def load():
         lib.rtgh_save_image.restype = C.c_int32
         lib.rtgh_render_scene.argtypes = [C.c_char_p, C.c_int32, C.c_uint64, C.c_char_p]
         lib.rtgh_render_scene.restype = C.c_int32
+        lib.rtgh_read_image.argtypes = [C.c_char_p, C.POINTER(A.PF), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        lib.rtgh_read_image.restype = C.c_int32
+        lib.rtgh_free_image.argtypes = [A.PF]
+        lib.rtgh_free_image.restype = None
         _lib = lib
     return _lib
 
@@ -46,6 +50,19 @@ def load():
 def _check(rc):
     if rc != 0:
         raise A.RtgError(f"{A.STATUS.get(rc, rc)}: {_lib.rtgh_last_error().decode()}")
+
+
+def read_image(path: str) -> np.ndarray:
+    """rtgh_read_image: the texels a texture sees, (h, w, 3) float32 (raw 0..255 for
+    PNG/JPEG/PPM, linear floats for OpenEXR)."""
+    lib = load()
+    p = A.PF()
+    w, h = C.c_int32(), C.c_int32()
+    _check(lib.rtgh_read_image(path.encode(), C.byref(p), C.byref(w), C.byref(h)))
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 3)).copy()
+    finally:
+        lib.rtgh_free_image(p)
 
 
 class NativeScene:

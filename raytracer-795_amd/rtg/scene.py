@@ -374,10 +374,12 @@ def _parse_textures_list(text: str) -> list:
 
 def load_image(path: str) -> np.ndarray:
     """Decode an image texture the way src/Texture.cpp:133-300 exposes it: 8-bit RGB(A) raw
-    values 0..255 as floats, row 0 first.  EXR is not supported (tinyexr is vendored only)."""
+    values 0..255 as floats, row 0 first.  OpenEXR goes through the native decoder
+    (librtghost rtgh_read_image, host/exr_read.cpp): LoadEXR's linear R, G, B floats."""
     low = path.lower()
     if low.endswith(".exr"):
-        raise NotImplementedError("EXR textures are not supported by the host loader")
+        from . import native
+        return native.read_image(path)
     if low.endswith(".ppm") or low.endswith(".pnm"):
         return read_ppm(path)
     from PIL import Image  # decode is host I/O, out of the hot path

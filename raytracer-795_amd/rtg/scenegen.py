@@ -376,6 +376,56 @@ def multilight(nx=320, ny=240, spp=1) -> Scene:
     return sc
 
 
+def sky_texture(w=64, h=32, sun=(0.3, 0.28), sun_radiance=40.0) -> np.ndarray:
+    """Linear HDR latitude-longitude sky (what an .exr environment map decodes to): a
+    horizon-to-zenith gradient, a dark ground half and a small bright sun disc.  Values are
+    rounded through float16 so that an OpenEXR HALF file round-trips them exactly."""
+    v, u = np.mgrid[0:h, 0:w].astype(f32)
+    v = (v + 0.5) / h
+    u = (u + 0.5) / w
+    up = np.clip(1.0 - 2.0 * v, 0.0, 1.0)[..., None]
+    sky = (np.array([0.9, 1.0, 1.1], f32) * (1 - up) + np.array([0.25, 0.45, 1.0], f32) * up) * 1.5
+    ground = np.array([0.18, 0.15, 0.12], f32) * np.ones_like(sky)
+    img = np.where((v < 0.5)[..., None], sky, ground)
+    du = np.minimum(np.abs(u - sun[0]), 1 - np.abs(u - sun[0]))
+    d2 = (du * 2) ** 2 + (v - sun[1]) ** 2
+    img = img + (d2 < 0.004)[..., None] * np.array([1.0, 0.9, 0.7], f32) * sun_radiance
+    return img.astype(np.float16).astype(f32)
+
+
+def envmap(nx=96, ny=72, spp=4, max_depth=3) -> Scene:
+    """hw6 image-based lighting: a SphericalDirectionalLight (src/Light.cpp:551-660) over an
+    HDR sky (`sky_texture`, written as `sky.exr` by tests) lighting diffuse, Blinn-Phong,
+    BRDF, mirror and dielectric objects; primary misses show the environment map
+    (src/Scene.cpp:413-435)."""
+    sc = Scene(max_depth=max_depth, background=(0, 0, 0), ambient=(0, 0, 0))
+    sc.cameras.append(_cam((0, 1.3, 5.5), (0, -0.15, -1), (0, 1, 0), nx, ny, fov_deg=55, spp=spp,
+                           name="env.exr"))
+    sc.materials += [
+        Material(ambient=(0, 0, 0), diffuse=(0.6, 0.6, 0.6), specular=(0, 0, 0), phong_exp=1),
+        Material(ambient=(0, 0, 0), diffuse=(0.7, 0.3, 0.2), specular=(0.4, 0.4, 0.4), phong_exp=30),
+        Material(type=A.MAT_MIRROR, ambient=(0, 0, 0), diffuse=(0.05, 0.05, 0.05), specular=(0, 0, 0),
+                 mirror=(0.85, 0.85, 0.85), phong_exp=1),
+        Material(type=A.MAT_DIELECTRIC, ambient=(0, 0, 0), diffuse=(0, 0, 0), specular=(0, 0, 0),
+                 refraction_index=1.5, absorption_coeff=(0.05, 0.02, 0.01)),
+        Material(ambient=(0, 0, 0), diffuse=(0.3, 0.5, 0.7), specular=(0.5, 0.5, 0.5), phong_exp=50,
+                 brdf=A.BRDF_MBPN),
+    ]
+    c = _add_vertices(sc, [(-1.7, 0.6, -0.6), (0.0, 0.6, -1.2), (1.7, 0.6, -0.6), (0.8, 0.4, 0.9)])
+    for k, mat in enumerate([2, 3, 4, 5]):
+        sc.objects.append(Object(type=A.OBJ_SPHERE, id=k + 1, material=mat, center=c + k,
+                                 radius=0.6 if k < 3 else 0.4))
+    fl = _add_vertices(sc, [(-5, 0, 5), (5, 0, 5), (5, 0, -5), (-5, 0, -5)])
+    sc.objects.append(Object(type=A.OBJ_MESH, id=1, material=1,
+                             faces=np.array([[fl, fl + 1, fl + 2], [fl, fl + 2, fl + 3]], np.int32)))
+    sc.images = ["sky.exr"]
+    sc.textures.append(Texture(kind=A.TEX_IMAGE, decal=A.DECAL_NONE, interp=A.INTERP_BILINEAR, normalizer=1,
+                               bump_factor=1.0, texels=sky_texture(), image_id=1))
+    sc.environment_light = len(sc.lights)
+    sc.lights.append(Light(type=A.LIGHT_ENVIRONMENT, texture=len(sc.textures) - 1, image_id=1))
+    return sc
+
+
 CONFIGS = {
     "simple": simple,
     "bunny5k": bunny5k,
@@ -384,4 +434,5 @@ CONFIGS = {
     "cornell_pt": cornell_pt,
     "textured": textured,
     "multilight": multilight,
+    "envmap": envmap,
 }

@@ -1,0 +1,141 @@
+"""OpenEXR texture decoding (host/exr_read.cpp via rtgh_read_image): what the reference's
+Texture::ReadExr -> LoadEXR hands the texture code (src/Texture.cpp:185-189,
+src/Helper.cpp:346-359), on every codec LoadEXR reads.  Files come from the independent
+test-side encoder tests/exr_codec.py; decoded texels must equal the stored values bit for bit."""
+import os
+
+import numpy as np
+import pytest
+
+from rtg import native
+from rtg._abi import RtgError
+
+import exr_codec as X
+
+pytestmark = pytest.mark.skipif(not os.path.exists(native.LIB_PATH), reason="librtghost.so not built")
+
+
+def _image(h, w, seed, alpha=False, scale=4.0):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    ch = {
+        "R": (xx / w) * scale,                                       # smooth ramp
+        "G": rng.standard_normal((h, w)).astype(np.float32) * scale,  # noise, negatives
+        "B": np.where((xx // 7 + yy // 5) % 2 == 0, 0.25, 1e3).astype(np.float32),  # runs
+    }
+    ch["B"][: h // 3] = 0.0                                           # a zero band
+    if alpha:
+        ch["A"] = np.full((h, w), 0.5, np.float32)
+    return ch
+
+
+def _check(path, ch, ptype):
+    got = native.read_image(path)
+    want = X.expected_rgba(ch, ptype)[..., :3]
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint32), want.astype(np.float32).view(np.uint32))
+
+
+CODECS = [("none", X.NONE), ("rle", X.RLE), ("zips", X.ZIPS), ("zip", X.ZIP), ("piz", X.PIZ)]
+
+
+@pytest.mark.parametrize("cname,comp", CODECS)
+@pytest.mark.parametrize("ptype", [X.HALF, X.FLOAT], ids=["half", "float"])
+@pytest.mark.parametrize("tile", [0, 16], ids=["scanline", "tiled"])
+def test_codecs_roundtrip(tmp_path, cname, comp, ptype, tile):
+    ch = _image(45, 37, seed=hash((cname, ptype, tile)) & 0xFFFF, alpha=(ptype == X.FLOAT))
+    p = str(tmp_path / f"t_{cname}.exr")
+    X.write_exr(p, ch, comp, ptype, tile=tile)
+    _check(p, ch, ptype)
+
+
+def test_piz_16bit_wavelet_and_runs(tmp_path):
+    """> 2^14 distinct 16-bit words switch PIZ to the 16-bit lifting; long runs exercise the
+    Huffman run-length symbol."""
+    rng = np.random.default_rng(7)
+    h, w = 64, 300
+    ch = {c: rng.uniform(-5e4, 5e4, (h, w)).astype(np.float32) for c in "RGB"}
+    ch["G"][10:30] = 3.0
+    p = str(tmp_path / "big.exr")
+    X.write_exr(p, ch, X.PIZ, X.FLOAT)
+    _check(p, ch, X.FLOAT)
+
+
+def test_mixed_pixel_types_and_window(tmp_path):
+    ch = _image(20, 33, seed=3)
+    types = {"R": X.HALF, "G": X.FLOAT, "B": X.UINT}
+    ch["B"] = np.arange(20 * 33, dtype=np.float32).reshape(20, 33) * 1000
+    for comp in (X.NONE, X.ZIP, X.PIZ):
+        p = str(tmp_path / f"mixed{comp}.exr")
+        X.write_exr(p, ch, comp, types, data_origin=(-5, 12))
+        _check(p, ch, types)
+
+
+def test_single_channel_replicated(tmp_path):
+    ch = {"Y": np.linspace(0, 2, 24 * 18, dtype=np.float32).reshape(18, 24)}
+    p = str(tmp_path / "y.exr")
+    X.write_exr(p, ch, X.ZIP, X.HALF)
+    _check(p, ch, X.HALF)
+
+
+def test_layer_names_use_last_component(tmp_path):
+    base = _image(12, 10, seed=5)
+    ch = {"diffuse." + k: v for k, v in base.items()}
+    p = str(tmp_path / "layer.exr")
+    X.write_exr(p, ch, X.RLE, X.HALF)
+    got = native.read_image(p)
+    want = X.expected_rgba(base, X.HALF)[..., :3]
+    assert np.array_equal(got, want)
+
+
+def test_missing_channel_fails_loudly(tmp_path):
+    ch = _image(8, 8, seed=1)
+    del ch["B"]
+    p = str(tmp_path / "rg.exr")
+    X.write_exr(p, ch, X.NONE, X.HALF)
+    with pytest.raises(RtgError, match="B channel not found"):
+        native.read_image(p)
+
+
+def test_corrupt_and_unsupported_fail_loudly(tmp_path):
+    ch = _image(40, 16, seed=2)
+    p = str(tmp_path / "c.exr")
+    data = X.write_exr(p, ch, X.PIZ, X.HALF)
+    with open(p, "wb") as fh:                      # truncate inside the last chunk
+        fh.write(data[:-40])
+    with pytest.raises(RtgError):
+        native.read_image(p)
+    q = str(tmp_path / "not.exr")
+    with open(q, "wb") as fh:
+        fh.write(b"P3\n1 1\n255\n0 0 0\n")
+    with pytest.raises(RtgError, match="not an OpenEXR"):
+        native.read_image(q)
+
+
+def test_native_writer_reads_back(tmp_path):
+    """rtgh_save_image's OpenEXR HALF output (Image::saveImage, src/Helper.cpp:361-412)
+    decodes to the half-rounded framebuffer."""
+    rng = np.random.default_rng(11)
+    img = (rng.uniform(0, 300, (17, 23, 3))).astype(np.float32)
+    p = str(tmp_path / "out.exr")
+    native.save_image(p, img)
+    got = native.read_image(p)
+    assert np.array_equal(got, img.astype(np.float16).astype(np.float32))
+
+
+def test_scene_texture_exr_matches_native_parse(tmp_path):
+    """An .exr <Image> reaches rtg_texture_desc.texels identically through both hosts."""
+    from rtg import scenegen
+    from rtg.scene import parse_xml, write_xml
+    ch = _image(16, 32, seed=9, scale=2.0)
+    X.write_exr(str(tmp_path / "env.exr"), ch, X.PIZ, X.HALF)
+    sc = scenegen.textured(32, 24)
+    sc.images = [str(tmp_path / "env.exr")] + list(sc.images[1:])
+    xml = write_xml(sc, str(tmp_path / "s.xml"))
+    py = parse_xml(xml)
+    with native.NativeScene(xml) as ns:
+        d = native.desc_to_dict(ns.desc)
+    t0 = py.textures[0]
+    want = X.expected_rgba(ch, X.HALF)[..., :3]
+    assert np.array_equal(np.asarray(t0.texels, np.float32).reshape(want.shape), want)
+    assert np.array_equal(np.asarray(d["textures"][0]["texels"], np.float32).reshape(want.shape), want)

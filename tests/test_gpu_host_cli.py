@@ -62,3 +62,26 @@ def test_cli_tonemap_outputs(gpu, tmp_path):
     rtg.render_scene(parse_xml(xml), out_dir=str(py_dir), device=gpu)
     for f in ("tm.exr", "tm.png"):
         assert (cli_dir / f).read_bytes() == (py_dir / f).read_bytes(), f
+
+
+def test_cli_envmap_exr_texture(gpu, tmp_path):
+    """hw6 image-based lighting from an OpenEXR sky (decoded by host/exr_read.cpp in both
+    hosts), HDR output plus the tone-mapped .png: native == Python host, and the frame equals
+    the oracle's on the generated (in-memory) scene."""
+    import pyoracle
+    from rtg.render import exr_half_bytes
+    sc = scenegen.envmap(40, 30, spp=2)
+    sc.cameras[0].tonemap = (0.18, 0.5, 1.0, 2.2)
+    cli_dir, py_dir = tmp_path / "cli", tmp_path / "py"
+    cli_dir.mkdir()
+    py_dir.mkdir()
+    (tmp_path / "sky.exr").write_bytes(exr_half_bytes(sc.textures[0].texels))
+    xml = write_xml(sc, str(tmp_path / "env.xml"))
+    native.render_scene(xml, device=gpu, out_dir=str(cli_dir))
+    rtg.render_scene(parse_xml(xml), out_dir=str(py_dir), device=gpu)
+    for f in ("env.exr", "env.png"):
+        assert (cli_dir / f).read_bytes() == (py_dir / f).read_bytes(), f
+    with rtg.Renderer(parse_xml(xml), device=gpu) as r:
+        img = r.render(0)
+    ref, _, _, _ = pyoracle.Oracle(sc).render(0)
+    assert float(np.nanmax(np.abs(img.astype(np.float64) - ref))) < 1e-3

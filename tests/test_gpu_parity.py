@@ -26,6 +26,7 @@ SCENES = {
     "textured_ms": lambda: scenegen.textured(32, 24, spp=2),
     "multilight": lambda: scenegen.multilight(64, 48),
     "multilight_ms": lambda: scenegen.multilight(32, 24, spp=3),
+    "envmap": lambda: scenegen.envmap(48, 36, spp=2),
 }
 
 

@@ -86,6 +86,19 @@ def test_native_parser_textures(tmp_path, fmt):
     assert py.textures[0].texels is not None
 
 
+def test_native_parser_envmap_exr(tmp_path):
+    """hw6 SphericalDirectionalLight over an OpenEXR sky: both hosts decode the file (native
+    rtgh_read_image) to the same linear texels, normalizer 1, bilinear."""
+    from rtg.render import exr_half_bytes
+    sc = scenegen.envmap(16, 12)
+    sky = sc.textures[0].texels
+    (tmp_path / "sky.exr").write_bytes(exr_half_bytes(sky))
+    xml = write_xml(sc, str(tmp_path / "env.xml"))
+    py = _compare(xml)
+    assert py.environment_light == 0
+    assert np.array_equal(np.asarray(py.textures[0].texels, np.float32).reshape(sky.shape), sky)
+
+
 def test_native_parser_quirks(tmp_path):
     """Hand-written XML: FovY / GazePoint cameras, composite-first transformation lists,
     texture-map state carried over, XML faces with offsets, instances, entity escapes."""
@@ -193,7 +206,7 @@ def test_host_library_exports_every_declared_symbol():
     hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rtg_host.h")
     decl = set(re.findall(r"^\s*(?:int32_t|const char\*|void|const rtg_scene_desc\*)\s+(rtgh_\w+)\s*\(",
                           open(hdr).read(), re.M))
-    assert len(decl) == 9
+    assert len(decl) == 11
     out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], capture_output=True, text=True, check=True)
     syms = set(re.findall(r"\sT\s(rtgh_\w+)", out.stdout))
     assert decl <= syms, decl - syms
