@@ -115,6 +115,7 @@ def main():
 
     t0 = time.perf_counter()
     from rtg import scenegen
+    from rtg.shard import shard_opts
     make, spp_default, wl_text, data_text = WORKLOADS[args.workload]
     scene = getattr(scenegen, make)(args.width, args.height, spp=args.spp or spp_default)
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
@@ -126,7 +127,7 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(**kw):
-        r.render_device(0, frame.data_ptr(), stream, row_offset=rank, row_stride=world, **kw)
+        r.render_device(0, frame.data_ptr(), stream, **shard_opts(rank, world), **kw)
         st = r.stats()
         if dist is not None:
             dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
@@ -194,7 +195,7 @@ def main():
                 "data": data_text,
                 "config": {"workload": wl_text,
                            "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
-                           "parallelism": f"row-interleaved pixel shards x{world} + RCCL reduce"},
+                           "parallelism": f"8-row-block interleaved pixel shards x{world} + RCCL reduce"},
                 "rays_per_frame": rays // max(args.steps, 1),
                 "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
                 "kernel_ms_rank0_streams1": {"trace": round(st_roof["trace_ms"], 2),

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 2
+#define RTG_ABI_VERSION 3
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -218,13 +218,15 @@ typedef enum rtg_pt_flags {
 
 typedef struct rtg_render_opts {
     uint64_t seed;           /* Philox key for all stochastic draws (reference: random_device) */
-    int32_t row_offset;      /* render only rows y with y % row_stride == row_offset; other */
-    int32_t row_stride;      /* rows are written as 0 (multi-GPU pixel sharding). 0/1 = all */
+    int32_t row_offset;      /* render only rows y with (y / row_block) % row_stride == row_offset; */
+    int32_t row_stride;      /* other rows are written as 0 (multi-GPU pixel sharding). 0/1 = all */
     int32_t traversal;       /* 0 = ordered + pruned (default), 1 = exhaustive (literal line test) */
     int32_t max_batch_rays;  /* 0 = auto */
     int32_t collect_stats;   /* 1 = count BVH node visits / triangle tests (slower) */
     int32_t collect_timing;  /* 1 = HIP-event time every closest-hit / shadow launch */
     int32_t streams;         /* passes in flight on separate HIP streams (0 = library default, 3) */
+    int32_t row_block;       /* rows per shard interleave block (0/1 = single rows; 8 keeps each rank's
+                                8x8 pixel tiles image-contiguous) */
 } rtg_render_opts;
 
 typedef struct rtg_render_stats {

@@ -31,7 +31,7 @@ def load():
         lib.orc_scene_destroy.argtypes = [C.c_void_p]
         lib.orc_scene_destroy.restype = None
         lib.orc_render.argtypes = [C.c_void_p, C.POINTER(A.CameraDesc), C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
-                                   C.c_int, A.PF, A.PI, A.PI, A.PF]
+                                   C.c_int, C.c_int, A.PF, A.PI, A.PI, A.PF]
         lib.orc_render.restype = C.c_int
         lib.orc_last_ray_counts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         lib.orc_last_ray_counts.restype = None
@@ -74,14 +74,15 @@ class Oracle:
         except Exception:
             pass
 
-    def render(self, camera=0, seed=0x5EED2026, nthreads=0, row_offset=0, row_stride=1, row_begin=0, row_end=0):
+    def render(self, camera=0, seed=0x5EED2026, nthreads=0, row_offset=0, row_stride=1, row_begin=0, row_end=0,
+               row_block=1):
         cam = self.scene.cameras[camera] if isinstance(camera, int) else camera
         cd = cam.desc()
         rgb = np.zeros((cam.ny, cam.nx, 3), np.float32)
         obj = np.full((cam.ny, cam.nx), -2, np.int32)
         prim = np.full((cam.ny, cam.nx), -2, np.int32)
         t = np.zeros((cam.ny, cam.nx), np.float32)
-        rc = self.lib.orc_render(self.handle, C.byref(cd), seed, nthreads, row_offset, row_stride, row_begin, row_end,
+        rc = self.lib.orc_render(self.handle, C.byref(cd), seed, nthreads, row_offset, row_stride, row_block, row_begin, row_end,
                                  rgb.ctypes.data_as(A.PF), obj.ctypes.data_as(A.PI), prim.ctypes.data_as(A.PI),
                                  t.ctypes.data_as(A.PF))
         if rc != 0:

@@ -1685,12 +1685,14 @@ int orc_scene_create(const rtg_scene_desc* d, orc_scene** out) {
 
 /* ------------------------------------------------------------------ API */
 int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthreads, int row_offset,
-               int row_stride, int row_begin, int row_end, float* rgb, int32_t* pobj, int32_t* pprim, float* pt) {
+               int row_stride, int row_block, int row_begin, int row_end, float* rgb, int32_t* pobj,
+               int32_t* pprim, float* pt) {
     if (!s || !cd || !rgb) return RTG_ERR_INVALID;
     Cam cam;
     cam_init(&cam, cd);
     int nx = cd->nx, ny = cd->ny;
     if (row_stride <= 0) row_stride = 1;
+    if (row_block <= 0) row_block = 1;
     if (row_end <= 0 || row_end > ny) row_end = ny;
     if (row_begin < 0) row_begin = 0;
     uint64_t np = 0, nsec = 0, nsh = 0;
@@ -1701,7 +1703,7 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
 #endif
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : np, nsec, nsh)
     for (int y = row_begin; y < row_end; y++) {
-        if (y % row_stride != row_offset % row_stride) continue;
+        if ((y / row_block) % row_stride != row_offset % row_stride) continue;
         Ctx cx = {s, {seed, 0, 0}, 0, 0, 0};
         for (int x = 0; x < nx; x++) {
             uint32_t pixel = (uint32_t)(y * nx + x);

@@ -24,13 +24,14 @@ typedef struct orc_scene orc_scene;
 int orc_scene_create(const rtg_scene_desc* desc, orc_scene** out);
 void orc_scene_destroy(orc_scene* s);
 
-/* Render rows [row_begin,row_end) that satisfy y % row_stride == row_offset.
+/* Render rows [row_begin,row_end) that satisfy (y / row_block) % row_stride == row_offset
+   (row_block <= 1: single-row interleave; the multi-GPU shard of rtg_render_opts).
    rgb: ny*nx*3 floats (rows not rendered are left untouched).
    prim_obj/prim_prim/prim_t (optional, ny*nx each): the closest hit of the primary ray
    of sample 0 (obj -1 on miss), prim in original primitive order.
    nthreads <= 0: OpenMP default. */
 int orc_render(orc_scene* s, const rtg_camera_desc* cam, uint64_t seed, int nthreads,
-               int row_offset, int row_stride, int row_begin, int row_end, float* rgb,
+               int row_offset, int row_stride, int row_block, int row_begin, int row_end, float* rgb,
                int32_t* prim_obj, int32_t* prim_prim, float* prim_t);
 /* rays traced by the last orc_render: [0]=primary [1]=secondary [2]=shadow */
 void orc_last_ray_counts(const orc_scene* s, uint64_t counts[3]);

@@ -1262,7 +1262,7 @@ DEV void slot_pixel(const CameraDev& cam, const PassDev& ps, int slot, uint32_t&
     const int pl = slot / ps.ns, sl = slot - pl * ps.ns;
     int k;
     tile_pixel(ps.p0 + pl, cam.nx, ps.rows_owned, x, k);
-    y = ps.row_offset + k * ps.row_stride;
+    y = shard_row(k, ps.row_offset, ps.row_stride, ps.row_block);
     pixel = (uint32_t)(y * cam.nx + x);
     sample = (uint32_t)(ps.s0 + sl);
 }
@@ -2003,13 +2003,14 @@ __global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ 
 }
 
 __global__ void __launch_bounds__(256) k_finalize(const float* __restrict__ acc, float* __restrict__ out, int nx,
-                                                  int ny, int row_offset, int row_stride, int total) {
+                                                  int ny, int row_offset, int row_stride, int row_block, int total) {
     int pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= nx * ny) return;
     int y = pix / nx, x = pix - y * nx;
     float r = 0.0f, g = 0.0f, b = 0.0f;
-    if (y % row_stride == row_offset) {
-        int pl = (y / row_stride) * nx + x;
+    const int k = shard_owned_index(y, row_offset, row_stride, row_block);
+    if (k >= 0) {
+        int pl = k * nx + x;
         r = acc[3 * pl]; g = acc[3 * pl + 1]; b = acc[3 * pl + 2];
         if (total > 1) { r = r / (float)total; g = g / (float)total; b = b / (float)total; }
     }
@@ -2112,12 +2113,12 @@ void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int
     if (ps.npass <= 0) return;
     hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, 256)), dim3(256), 0, st, level0, acc, ps, nx, mode);
 }
-void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int total,
-                     hipStream_t st) {
+void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block,
+                     int total, hipStream_t st) {
     int n = nx * ny;
     if (n <= 0) return;
     hipLaunchKernelGGL(k_finalize, dim3(nblk(n, 256)), dim3(256), 0, st, acc, out, nx, ny, row_offset, row_stride,
-                       total);
+                       row_block, total);
 }
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st) {

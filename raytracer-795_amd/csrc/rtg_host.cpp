@@ -1020,9 +1020,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     int stride = o.row_stride > 1 ? o.row_stride : 1;
     int off = o.row_offset;
     if (off < 0 || off >= stride) return fail(RTG_ERR_INVALID, "row_offset out of range");
+    const int block = o.row_block > 1 ? o.row_block : 1;
     CameraDev cd = make_camera(cam);
-    int rows_owned = (cam->ny - off + stride - 1) / stride;
-    if (rows_owned < 0) rows_owned = 0;
+    int rows_owned = 0;                      // rows y with (y / block) % stride == off
+    for (int b = off; (long long)b * block < cam->ny; b += stride) rows_owned += std::min(block, cam->ny - b * block);
     long long npix_ll = (long long)rows_owned * cam->nx;
     if (npix_ll > (1LL << 30)) return fail(RTG_ERR_UNSUPPORTED, "image too large");
     int npix = (int)npix_ll;
@@ -1077,7 +1078,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             PassDev ps;
             ps.s0 = s0; ps.ns = std::min(ns_chunk, total - s0);
             ps.p0 = p0; ps.npass = std::min(np_pass, npix - p0);
-            ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned;
+            ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned; ps.row_block = block;
             plist.push_back(ps);
         }
     const int nranges = npix > 0 ? (npix + np_pass - 1) / np_pass : 1;
@@ -1222,7 +1223,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         HIP_TRY(hipEventRecord(ejoin, s->lanes[k].st));
         HIP_TRY(hipStreamWaitEvent(st, ejoin, 0));
     }
-    launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, cam->ny, off, stride, total, st);
+    launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, cam->ny, off, stride, block, total, st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e1, st));
     HIP_TRY(hipEventSynchronize(e1));

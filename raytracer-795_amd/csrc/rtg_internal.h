@@ -165,8 +165,20 @@ struct PathRec {       // 16 B
 // all samples of a pixel are adjacent, so a wavefront traces near-identical rays.
 struct PassDev {
     int s0, ns, p0, npass;
-    int row_offset, row_stride, rows_owned;
+    int row_offset, row_stride, rows_owned, row_block;
 };
+
+// Shard row ownership (rtg_render_opts.row_block): owned row k <-> image row y.
+__host__ __device__ inline int shard_row(int k, int off, int stride, int block) {
+    const int b = k / block;
+    return (b * stride + off) * block + (k - b * block);
+}
+// owned index of image row y, or -1 when another shard owns it
+__host__ __device__ inline int shard_owned_index(int y, int off, int stride, int block) {
+    const int b = y / block;
+    if (b % stride != off) return -1;
+    return (b / stride) * block + (y - b * block);
+}
 
 struct CameraDev {
     float pos[3], gaze[3], up[3], right[3];
@@ -247,7 +259,7 @@ void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRe
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
 void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);
-void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int total,
+void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block, int total,
                      hipStream_t st);
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st);

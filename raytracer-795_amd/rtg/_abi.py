@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 2
+RTG_ABI_VERSION = 3
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -106,7 +106,7 @@ class CameraDesc(C.Structure):
 class RenderOpts(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("row_offset", C.c_int32), ("row_stride", C.c_int32),
                 ("traversal", C.c_int32), ("max_batch_rays", C.c_int32), ("collect_stats", C.c_int32),
-                ("collect_timing", C.c_int32), ("streams", C.c_int32)]
+                ("collect_timing", C.c_int32), ("streams", C.c_int32), ("row_block", C.c_int32)]
 
 
 class RenderStats(C.Structure):

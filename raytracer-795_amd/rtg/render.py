@@ -53,10 +53,10 @@ class Renderer:
 
     @staticmethod
     def opts(seed=DEFAULT_SEED, row_offset=0, row_stride=1, traversal=0, max_batch_rays=0, collect_stats=0,
-             collect_timing=0, streams=0):
+             collect_timing=0, streams=0, row_block=1):
         o = A.RenderOpts()
         o.seed = seed
-        o.row_offset, o.row_stride = row_offset, row_stride
+        o.row_offset, o.row_stride, o.row_block = row_offset, row_stride, row_block
         o.traversal = traversal
         o.max_batch_rays = max_batch_rays
         o.collect_stats = collect_stats

@@ -1,8 +1,10 @@
 """Multi-GPU pixel sharding.
 
-Rank r of G renders the rows y with y % G == r (the reference interleaves pixel columns
-over its 8 threads, src/Scene.cpp:400-423; rows keep each GPU's rays scanline-coherent)
-into a zero-initialised full-frame accumulator.  Summing the G frames is exact because
+Rank r of G renders the rows y with (y // B) % G == r, B = ROW_BLOCK = 8 (the reference
+interleaves pixel columns over its 8 threads, src/Scene.cpp:400-423; 8-row blocks keep
+each GPU's 8x8 pixel tiles image-contiguous, so its rays stay as coherent as on one GPU,
+while the fine interleave keeps the ranks' loads balanced) into a zero-initialised
+full-frame accumulator.  Summing the G frames is exact because
 their supports are disjoint (x + 0 == x), so one reduce (RCCL over xGMI on GPUs, gloo on
 CPU) yields the single-device frame bit for bit.
 """
@@ -11,12 +13,16 @@ from __future__ import annotations
 import numpy as np
 
 
-def owned_rows(ny: int, rank: int, world: int) -> np.ndarray:
-    return np.arange(rank, ny, world)
+ROW_BLOCK = 8
 
 
-def shard_opts(rank: int, world: int) -> dict:
-    return {"row_offset": rank, "row_stride": world}
+def owned_rows(ny: int, rank: int, world: int, block: int = ROW_BLOCK) -> np.ndarray:
+    y = np.arange(ny)
+    return y[(y // max(block, 1)) % world == rank]
+
+
+def shard_opts(rank: int, world: int, block: int = ROW_BLOCK) -> dict:
+    return {"row_offset": rank, "row_stride": world, "row_block": block}
 
 
 def reduce_frame(frame, dist, dst: int = 0):
@@ -27,11 +33,11 @@ def reduce_frame(frame, dist, dst: int = 0):
 
 
 def render_sharded(render_rows, ny: int, nx: int, rank: int, world: int, dist=None):
-    """render_rows(row_offset, row_stride) -> (ny, nx, 3) float32 frame with only the owned rows
-    written (others zero).  Returns the reduced frame on rank 0 (torch CPU tensor)."""
+    """render_rows(**shard_opts(rank, world)) -> (ny, nx, 3) float32 frame with only the owned
+    rows written (others zero).  Returns the reduced frame on rank 0 (torch CPU tensor)."""
     import torch
 
-    part = np.asarray(render_rows(rank, world), np.float32)
+    part = np.asarray(render_rows(**shard_opts(rank, world)), np.float32)
     mask = np.zeros(ny, bool)
     mask[owned_rows(ny, rank, world)] = True
     part = np.where(mask[:, None, None], part, np.float32(0.0)).astype(np.float32)

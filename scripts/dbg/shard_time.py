@@ -12,7 +12,7 @@ st = torch.cuda.current_stream().cuda_stream
 for streams in (0,):
     for N in (1, 2, 4, 8):
         for rank in ((0, N - 1) if N > 1 else (0,)):
-            kw = dict(row_offset=rank, row_stride=N, streams=streams)
+            kw = dict(row_offset=rank, row_stride=N, streams=streams, row_block=int(sys.argv[2]) if len(sys.argv) > 2 else 8)
             r.render_device(0, frame.data_ptr(), st, **kw)
             torch.cuda.synchronize()
             t = time.perf_counter()

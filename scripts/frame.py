@@ -13,5 +13,5 @@ sc = getattr(scenegen, w)(1920, 1080, spp=int(os.environ.get("RTG_SPP", "256" if
 r = rtg.Renderer(sc, 0)
 stride = int(os.environ.get("RTG_ROW_STRIDE", "1"))     # one multi-GPU rank's row shard
 for _ in range(n):
-    r.render(0, row_offset=0, row_stride=stride)
+    r.render(0, row_offset=0, row_stride=stride, row_block=int(os.environ.get("RTG_ROW_BLOCK", "8")))
 print("frame ms", round(r.stats()["render_ms"], 1))

@@ -1,4 +1,4 @@
-"""N>1 path on CPU: world_size-2 gloo.  Each rank renders its row shard (y % 2 == rank)
+"""N>1 path on CPU: world_size-2 gloo.  Each rank renders its row shard ((y // 8) % 2 == rank)
 and the frames are summed onto rank 0 with one reduce — the same partition + collective
 bench.py uses over RCCL.  The oracle stands in for the GPU renderer here (test infra);
 the reduced frame must equal the single-process frame bit for bit."""
@@ -35,8 +35,8 @@ def _worker(rank, world, port, out_path):
     sc = scenegen.cornell(24, 17, spp=2)
     orc = pyoracle.Oracle(sc)
 
-    def rows(off, stride):
-        return orc.render(0, nthreads=1, row_offset=off, row_stride=stride)[0]
+    def rows(row_offset, row_stride, row_block):
+        return orc.render(0, nthreads=1, row_offset=row_offset, row_stride=row_stride, row_block=row_block)[0]
 
     frame = render_sharded(rows, 17, 24, rank, world, dist)
     if rank == 0:
@@ -60,5 +60,6 @@ def test_row_shards_reduce_to_single_frame(tmp_path, world):
 def test_owned_rows_partition():
     from rtg.shard import owned_rows
     for world in (1, 2, 3, 8):
-        rows = np.concatenate([owned_rows(1080, r, world) for r in range(world)])
-        assert sorted(rows.tolist()) == list(range(1080))
+        for ny, block in ((1080, 8), (1080, 1), (37, 8), (5, 8)):
+            rows = np.concatenate([owned_rows(ny, r, world, block) for r in range(world)])
+            assert sorted(rows.tolist()) == list(range(ny))

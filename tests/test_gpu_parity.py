@@ -75,14 +75,21 @@ def test_trace_matches_oracle(gpu, name):
             assert np.array_equal(h["normal"][m].view(np.int32), ref["normal"][m].view(np.int32))
 
 
-def test_row_shards_sum_to_full_frame(gpu):
-    """Multi-GPU partition (rows y % G == rank) + exact sum == the single-device frame."""
+@pytest.mark.parametrize("block", [1, 8, 5])
+def test_row_shards_sum_to_full_frame(gpu, block):
+    """Multi-GPU partition (rows (y // block) % G == rank, incl. a partial last block) +
+    exact sum == the single-device frame; each shard writes exactly its own rows."""
+    from rtg.shard import owned_rows
     sc = scenegen.cornell(40, 30, spp=2)
     with rtg.Renderer(sc, device=gpu) as r:
         full = r.render(0)
         acc = np.zeros_like(full)
         for rank in range(3):
-            acc += r.render(0, row_offset=rank, row_stride=3)
+            part = r.render(0, row_offset=rank, row_stride=3, row_block=block)
+            mask = np.zeros(30, bool)
+            mask[owned_rows(30, rank, 3, block)] = True
+            assert not part[~mask].any()
+            acc += part
     assert np.array_equal(acc.view(np.int32), full.view(np.int32))
 
 
@@ -187,11 +194,13 @@ def test_pruned_equals_exhaustive_full_res(gpu, name):
 
 
 def test_full_frame_shards_sum_exactly(gpu):
-    """1080p dragon1m at 2 spp split over 4 row shards sums to the single-device frame."""
+    """1080p dragon1m at 2 spp split over 4 row shards (bench's 8-row blocks) sums to the
+    single-device frame."""
+    from rtg.shard import shard_opts
     sc = scenegen.dragon1m(1920, 1080, spp=2)
     with rtg.Renderer(sc, device=gpu) as r:
         full = r.render(0)
         acc = np.zeros_like(full)
         for rank in range(4):
-            acc += r.render(0, row_offset=rank, row_stride=4)
+            acc += r.render(0, **shard_opts(rank, 4))
     assert np.array_equal(acc.view(np.int32), full.view(np.int32))

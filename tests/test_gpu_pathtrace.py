@@ -98,7 +98,7 @@ def test_path_trace_row_shards_and_batching(gpu):
         full = r.render(0)
         acc = np.zeros_like(full)
         for rank in range(2):
-            acc += r.render(0, row_offset=rank, row_stride=2)
+            acc += r.render(0, row_offset=rank, row_stride=2, row_block=8)
         b = r.render(0, max_batch_rays=777, streams=2)
         c = r.render(0, max_batch_rays=3, streams=1)       # sample chunks accumulate in order
     assert np.array_equal(acc.view(np.int32), full.view(np.int32))
