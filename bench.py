@@ -115,7 +115,7 @@ def main():
 
     t0 = time.perf_counter()
     from rtg import scenegen
-    from rtg.shard import shard_opts
+    from rtg.shard import gather_frame, max_shard_rows, shard_opts
     make, spp_default, wl_text, data_text = WORKLOADS[args.workload]
     scene = getattr(scenegen, make)(args.width, args.height, spp=args.spp or spp_default)
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
@@ -125,12 +125,18 @@ def main():
     cam = scene.cameras[0]
     frame = torch.zeros((cam.ny, cam.nx, 3), dtype=torch.float32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream().cuda_stream
+    # N > 1: each rank renders its owned rows compactly (1/N of the frame) and rank 0 gathers
+    # them over RCCL (point-to-point xGMI) into the frame — exact, and 1/N of a reduce's bytes
+    part = (torch.zeros((max_shard_rows(cam.ny, world), cam.nx, 3), dtype=torch.float32, device=frame.device)
+            if world > 1 else None)
 
     def step(**kw):
-        r.render_device(0, frame.data_ptr(), stream, **shard_opts(rank, world), **kw)
+        if part is None:
+            r.render_device(0, frame.data_ptr(), stream, **kw)
+            return r.stats()
+        r.render_device(0, part.data_ptr(), stream, **shard_opts(rank, world), compact_rows=1, **kw)
         st = r.stats()
-        if dist is not None:
-            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+        gather_frame(part, frame, rank, world, dist)
         return st
 
     # traversal statistics for the roofline model (outside the timed region)
@@ -195,7 +201,7 @@ def main():
                 "data": data_text,
                 "config": {"workload": wl_text,
                            "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
-                           "parallelism": f"8-row-block interleaved pixel shards x{world} + RCCL reduce"},
+                           "parallelism": f"8-row-block interleaved pixel shards x{world}" + (" + RCCL gather" if world > 1 else "")},
                 "rays_per_frame": rays // max(args.steps, 1),
                 "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
                 "kernel_ms_rank0_streams1": {"trace": round(st_roof["trace_ms"], 2),

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 3
+#define RTG_ABI_VERSION 4
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -227,7 +227,13 @@ typedef struct rtg_render_opts {
     int32_t streams;         /* passes in flight on separate HIP streams (0 = library default, 3) */
     int32_t row_block;       /* rows per shard interleave block (0/1 = single rows; 8 keeps each rank's
                                 8x8 pixel tiles image-contiguous) */
+    int32_t compact_rows;    /* 1: the output holds only the owned rows, in image order
+                                (rows_owned*nx*3 floats; rows_owned = rtg_shard_rows()), for a
+                                gather of the shards instead of a full-frame reduce */
 } rtg_render_opts;
+
+/* Number of image rows y < ny with (y / row_block) % row_stride == row_offset. */
+int32_t rtg_shard_rows(int32_t ny, int32_t row_offset, int32_t row_stride, int32_t row_block);
 
 typedef struct rtg_render_stats {
     uint64_t primary_rays;
@@ -300,7 +306,8 @@ typedef struct rtg_build_stats {
 int32_t rtg_scene_build_stats(const rtg_scene* scene, rtg_build_stats* out);
 int32_t rtg_scene_destroy(rtg_scene* scene);
 
-/* Render one camera; rgb_out is caller-owned host memory of ny*nx*3 floats ([y][x][c]). */
+/* Render one camera; rgb_out is caller-owned host memory of ny*nx*3 floats ([y][x][c])
+   (rows_owned*nx*3 with opts->compact_rows). */
 int32_t rtg_render(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_opts* opts,
                    float* rgb_out);
 /* Same, output left in device memory (caller-owned, ny*nx*3 floats on the scene's device),

@@ -18,6 +18,7 @@
 #include <new>
 #include <string>
 #include <deque>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -1022,8 +1023,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     if (off < 0 || off >= stride) return fail(RTG_ERR_INVALID, "row_offset out of range");
     const int block = o.row_block > 1 ? o.row_block : 1;
     CameraDev cd = make_camera(cam);
-    int rows_owned = 0;                      // rows y with (y / block) % stride == off
-    for (int b = off; (long long)b * block < cam->ny; b += stride) rows_owned += std::min(block, cam->ny - b * block);
+    const int rows_owned = rtg_shard_rows(cam->ny, off, stride, block);
     long long npix_ll = (long long)rows_owned * cam->nx;
     if (npix_ll > (1LL << 30)) return fail(RTG_ERR_UNSUPPORTED, "image too large");
     int npix = (int)npix_ll;
@@ -1176,14 +1176,29 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         ln.busy = false;
     };
     std::deque<int> waiting;           // lanes with a level in flight, in enqueue order
+    // next lane to service: the first (in enqueue order) whose count read-back has landed, so a
+    // lane with a long level does not hold up the others (head-of-line blocking)
+    auto next_ready = [&](int& pick) -> int {
+        for (;;) {
+            for (size_t i = 0; i < waiting.size(); i++) {
+                const hipError_t q = hipEventQuery(s->lanes[waiting[i]].ev_count);
+                if (q == hipSuccess) { pick = (int)i; return RTG_OK; }
+                if (q != hipErrorNotReady) HIP_TRY(q);
+            }
+            if (waiting.size() == 1) { pick = 0; return RTG_OK; }
+            std::this_thread::yield();
+        }
+    };
     for (int k = 0; k < L; k++)
         if (!s->lanes[k].passes.empty() && npix > 0) {
             if ((rc = start_pass(s->lanes[k]))) return rc;
             waiting.push_back(k);
         }
     while (!waiting.empty()) {
-        const int k = waiting.front();
-        waiting.pop_front();
+        int pick = 0;
+        if ((rc = next_ready(pick))) return rc;
+        const int k = waiting[pick];
+        waiting.erase(waiting.begin() + pick);
         Lane& ln = s->lanes[k];
         HIP_TRY(hipEventSynchronize(ln.ev_count));
         const unsigned long long q = *ln.h_count;
@@ -1223,7 +1238,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         HIP_TRY(hipEventRecord(ejoin, s->lanes[k].st));
         HIP_TRY(hipStreamWaitEvent(st, ejoin, 0));
     }
-    launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, cam->ny, off, stride, block, total, st);
+    if (o.compact_rows)
+        launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, rows_owned, 0, 1, 1, total, st);
+    else
+        launch_finalize(s->d_acc.as<float>(), out_dev, cam->nx, cam->ny, off, stride, block, total, st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e1, st));
     HIP_TRY(hipEventSynchronize(e1));
@@ -1256,12 +1274,22 @@ int32_t rtg_render_device(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
     return render_impl(s, cam, opts, rgb_out_device, (hipStream_t)stream);
 }
 
+int32_t rtg_shard_rows(int32_t ny, int32_t row_offset, int32_t row_stride, int32_t row_block) {
+    const int stride = row_stride > 1 ? row_stride : 1, block = row_block > 1 ? row_block : 1;
+    if (ny <= 0 || row_offset < 0 || row_offset >= stride) return 0;
+    int rows = 0;
+    for (long long b = row_offset; b * block < ny; b += stride) rows += (int)std::min<long long>(block, ny - b * block);
+    return rows;
+}
+
 int32_t rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, float* rgb_out) {
     if (!s || !cam || !rgb_out) return fail(RTG_ERR_INVALID, "null argument");
     if (cam->nx < 1 || cam->ny < 1) return fail(RTG_ERR_INVALID, "bad camera");
     if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
     HIP_TRY(hipSetDevice(s->device));
-    size_t bytes = sizeof(float) * 3 * (size_t)cam->nx * cam->ny;
+    const int out_rows = opts && opts->compact_rows ? rtg_shard_rows(cam->ny, opts->row_offset, opts->row_stride,
+                                                                     opts->row_block) : cam->ny;
+    size_t bytes = sizeof(float) * 3 * (size_t)cam->nx * std::max(out_rows, 1);
     float* d_out = nullptr;
     HIP_TRY(hipMalloc(&d_out, bytes));
     int rc = render_impl(s, cam, opts, d_out, nullptr);

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 3
+RTG_ABI_VERSION = 4
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -106,7 +106,8 @@ class CameraDesc(C.Structure):
 class RenderOpts(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("row_offset", C.c_int32), ("row_stride", C.c_int32),
                 ("traversal", C.c_int32), ("max_batch_rays", C.c_int32), ("collect_stats", C.c_int32),
-                ("collect_timing", C.c_int32), ("streams", C.c_int32), ("row_block", C.c_int32)]
+                ("collect_timing", C.c_int32), ("streams", C.c_int32), ("row_block", C.c_int32),
+                ("compact_rows", C.c_int32)]
 
 
 class RenderStats(C.Structure):
@@ -161,6 +162,7 @@ EXPORTS = {
     "rtg_render_device": (C.c_int32, [C.c_void_p, C.POINTER(CameraDesc), C.POINTER(RenderOpts), C.c_void_p,
                                       C.c_void_p]),
     "rtg_last_render_stats": (C.c_int32, [C.c_void_p, C.POINTER(RenderStats)]),
+    "rtg_shard_rows": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rtg_tonemap": (C.c_int32, [C.c_int32, PF, C.c_int32, C.c_int32, C.POINTER(TonemapDesc), PF]),
     "rtg_tonemap_device": (C.c_int32, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(TonemapDesc), C.c_void_p,
                                        C.c_void_p]),

@@ -53,7 +53,7 @@ class Renderer:
 
     @staticmethod
     def opts(seed=DEFAULT_SEED, row_offset=0, row_stride=1, traversal=0, max_batch_rays=0, collect_stats=0,
-             collect_timing=0, streams=0, row_block=1):
+             collect_timing=0, streams=0, row_block=1, compact_rows=0):
         o = A.RenderOpts()
         o.seed = seed
         o.row_offset, o.row_stride, o.row_block = row_offset, row_stride, row_block
@@ -62,13 +62,16 @@ class Renderer:
         o.collect_stats = collect_stats
         o.collect_timing = collect_timing
         o.streams = streams
+        o.compact_rows = compact_rows
         return o
 
     def render(self, camera: Camera | int = 0, **kw) -> np.ndarray:
         cam = self.scene.cameras[camera] if isinstance(camera, int) else camera
-        out = np.empty((cam.ny, cam.nx, 3), np.float32)
-        cd = cam.desc()
         o = self.opts(**kw)
+        rows = (self.lib.rtg_shard_rows(cam.ny, o.row_offset, o.row_stride, o.row_block) if o.compact_rows
+                else cam.ny)
+        out = np.empty((rows, cam.nx, 3), np.float32)
+        cd = cam.desc()
         A.check(self.lib.rtg_render(self.handle, C.byref(cd), C.byref(o), out.ctypes.data_as(A.PF)), self.lib)
         return out
 

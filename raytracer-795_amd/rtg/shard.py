@@ -32,6 +32,48 @@ def reduce_frame(frame, dist, dst: int = 0):
     return frame
 
 
+def gather_frame(part, frame, rank: int, world: int, dist, block: int = ROW_BLOCK, dst: int = 0):
+    """Collect the ranks' compact owned-row buffers (`part`: (max_rows, nx, 3), rows beyond the
+    rank's own count unused) onto `dst` and place them in `frame` ((ny, nx, 3), same device).
+    One gather of 1/G of the frame per rank instead of a full-frame reduce: rank `dst` receives
+    G-1 buffers over its point-to-point links; exact (a copy, not a sum)."""
+    import torch
+
+    ny = frame.shape[0]
+    if dist is None or not dist.is_initialized() or world == 1:
+        rows = _row_index(ny, rank, world, block, frame.device)
+        frame.index_copy_(0, rows, part[:len(rows)])
+        return frame
+    key = (id(part), world)
+    if rank == dst and _GATHER_BUFS.get("key") != key:
+        _GATHER_BUFS.update(key=key, bufs=[torch.empty_like(part) for _ in range(world)])
+    parts = _GATHER_BUFS["bufs"] if rank == dst else None
+    dist.gather(part, parts, dst=dst)
+    if rank == dst:
+        for r in range(world):
+            rows = _row_index(ny, r, world, block, frame.device)
+            frame.index_copy_(0, rows, parts[r][:len(rows)])
+    return frame
+
+
+_GATHER_BUFS: dict = {}
+_ROW_INDEX: dict = {}
+
+
+def _row_index(ny, rank, world, block, device):
+    """Owned-row index tensor on `device`, built once (no host->device copy per frame)."""
+    import torch
+
+    k = (ny, rank, world, block, str(device))
+    if k not in _ROW_INDEX:
+        _ROW_INDEX[k] = torch.as_tensor(owned_rows(ny, rank, world, block), device=device)
+    return _ROW_INDEX[k]
+
+
+def max_shard_rows(ny: int, world: int, block: int = ROW_BLOCK) -> int:
+    return max(len(owned_rows(ny, r, world, block)) for r in range(world))
+
+
 def render_sharded(render_rows, ny: int, nx: int, rank: int, world: int, dist=None):
     """render_rows(**shard_opts(rank, world)) -> (ny, nx, 3) float32 frame with only the owned
     rows written (others zero).  Returns the reduced frame on rank 0 (torch CPU tensor)."""

@@ -89,6 +89,8 @@ def test_row_shards_sum_to_full_frame(gpu, block):
             mask = np.zeros(30, bool)
             mask[owned_rows(30, rank, 3, block)] = True
             assert not part[~mask].any()
+            compact = r.render(0, row_offset=rank, row_stride=3, row_block=block, compact_rows=1)
+            assert np.array_equal(compact.view(np.int32), part[mask].view(np.int32))
             acc += part
     assert np.array_equal(acc.view(np.int32), full.view(np.int32))
 
