@@ -1834,20 +1834,20 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     Stats st = {0, 0, 0, 0};
     if (j < (int)*scount) {
         const int idx = slist[j];
-        const ShadowRec sr = shadows[idx];
-        const f3 o = mk(sr.o.x, sr.o.y, sr.o.z), d = mk(sr.d.x, sr.d.y, sr.d.z);
+        const float4 so = shadows[idx].o, sd = shadows[idx].d;
+        const f3 o = mk(so.x, so.y, so.z), d = mk(sd.x, sd.y, sd.z);
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
-        const int i = idx / sv.num_lights;
-        const NodeRec& nr = nodes[i];   // (p, lp: only for t_cert; re-read after the traversal)
-        const f3 p = mk(nr.px, nr.py, nr.pz);
-        const f3 lp = mk(sr.L.x, sr.L.y, sr.L.z);
         // Certification bound (closest_hit ANY): for 0 < t <= t_cert the computed
         // norm(p - (o + d t)) stays below the computed norm(p - L) (the point-light test of
         // PointLight::IsShadow, src/Light.cpp:188-205): |p - hp| <= |p - o| + t|d| plus rounding
         // of hp, of the difference and of the norm, all inside the 1e-5 relative margins.
         // Directional / environment queries are blocked by any hit (t_cert = inf).
         float t_cert = 0.0f;
-        if (!EXHAUSTIVE) {
+        if (!EXHAUSTIVE && RTG_SHADOW_ANY) {
+            const ShadowRec sr = shadows[idx];
+            const int i = idx / sv.num_lights;
+            const f3 p = mk(nodes[i].px, nodes[i].py, nodes[i].pz);
+            const f3 lp = mk(sr.L.x, sr.L.y, sr.L.z);
             if (sr.c.w == 1.0f) {
                 const float DL = norm(p - lp);
                 const float po = norm(p - o), dn = norm(d);
@@ -1860,13 +1860,19 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 t_cert = INFINITY;
             }
         }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, !EXHAUSTIVE && RTG_SHADOW_ANY>(sv, o, d, sr.o.w, EXHAUSTIVE ? FLT_MAX : sr.d.w,
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, !EXHAUSTIVE && RTG_SHADOW_ANY>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : sd.w,
                                                                s_stack + threadIdx.x, kTraceBlock, s_wnode[threadIdx.x >> 6],
                                                                s_wmask[threadIdx.x >> 6], st, t_cert);
+        // the query's contribution / mode are re-read rather than kept live across the traversal
+        // (register pressure: 128 VGPRs for 4 waves per SIMD)
+        const float* scp = reinterpret_cast<const float*>(&shadows[idx].c);
+        const float4 sc = make_float4(__builtin_nontemporal_load(scp), __builtin_nontemporal_load(scp + 1),
+                                      __builtin_nontemporal_load(scp + 2), __builtin_nontemporal_load(scp + 3));
+        const int i = idx / sv.num_lights;
         bool blocked;
         if (h.pad == 1) {
             blocked = true;         // certified by closest_hit (ANY)
-        } else if (sr.c.w == 1.0f || sr.c.w == 3.0f) {
+        } else if (sc.w == 1.0f || sc.w == 3.0f) {
             blocked = false;
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
@@ -1876,7 +1882,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 const f3 l_ = mk(ld(q + 12), ld(q + 13), ld(q + 14));
                 const f3 p_ = mk(ld(&nodes[i].px), ld(&nodes[i].py), ld(&nodes[i].pz));
                 f3 hp = o_ + d_ * h.t;
-                if (sr.c.w == 1.0f) {
+                if (sc.w == 1.0f) {
                     blocked = norm(p_ - l_) > norm(p_ - hp);
                 } else {   // object light (hw7, Page7.md:143-147): an occluder nearer than the sample
                     const float dl = norm(p_ - l_);
@@ -1887,7 +1893,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             blocked = h.obj >= 0;
         }
         if (sv.num_lights == 1) {
-            f3 add = blocked ? mk(0, 0, 0) : mk(sr.c.x, sr.c.y, sr.c.z);
+            f3 add = blocked ? mk(0, 0, 0) : mk(sc.x, sc.y, sc.z);
             nodes[i].cr = nodes[i].cr + add.x;
             nodes[i].cg = nodes[i].cg + add.y;
             nodes[i].cb = nodes[i].cb + add.z;

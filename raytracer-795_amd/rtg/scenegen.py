@@ -127,6 +127,22 @@ def simple(nx=800, ny=800) -> Scene:
     return sc
 
 
+def bgtex(nx=48, ny=32, spp=1, interp=A.INTERP_NN) -> Scene:
+    """`simple` in front of a replace_background image texture (src/Scene.cpp:544-566): at 1 spp
+    SingleSample passes (row = x, col = y), so the background is looked up transposed; at > 1
+    spp it is not (src/Scene.cpp:496-542)."""
+    sc = simple(nx, ny)
+    sc.cameras[0].num_samples = spp
+    sc.cameras[0].image_name = "bgtex.png"
+    v, u = np.mgrid[0:12, 0:20].astype(f32)
+    img = np.stack([u * 12.0, v * 20.0, ((u + v) % 3) * 100.0], -1).astype(f32)
+    sc.textures.append(Texture(kind=A.TEX_IMAGE, decal=A.DECAL_REPLACE_BACKGROUND, interp=interp, normalizer=255,
+                               bump_factor=1.0, texels=img, image_id=1))
+    sc.images = ["bg.ppm"]
+    sc.background_texture = len(sc.textures) - 1
+    return sc
+
+
 def bunny5k(nx=1920, ny=1080, level=4, spp=1) -> Scene:
     """C2: ~5K-tri displaced icosphere (flat), mirror floor, glass sphere, Whitted depth 6."""
     sc = Scene(max_depth=6, background=(10, 10, 20), ambient=(20, 20, 20))

@@ -33,6 +33,9 @@ SCENES = {
     "dragon_small": lambda: scenegen.dragon1m(16, 9, spp=2, nu=40, nv=20),
     "cornell_pt": lambda: scenegen.cornell_pt(12, 9, spp=3),
     "furnace_pt": lambda: scenegen.furnace(8, 6, spp=4),
+    "envmap": lambda: scenegen.envmap(16, 12, spp=2),
+    "bgtex_1spp": lambda: scenegen.bgtex(16, 12, spp=1),
+    "bgtex_ms": lambda: scenegen.bgtex(16, 12, spp=2, interp=1),
 }
 SEED = 0x5EED2026
 TRACE_SCENES = ["simple", "bunny", "cornell_dof", "dragon_small"]

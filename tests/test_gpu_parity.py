@@ -27,6 +27,8 @@ SCENES = {
     "multilight": lambda: scenegen.multilight(64, 48),
     "multilight_ms": lambda: scenegen.multilight(32, 24, spp=3),
     "envmap": lambda: scenegen.envmap(48, 36, spp=2),
+    "bgtex": lambda: scenegen.bgtex(48, 32, spp=1),
+    "bgtex_ms": lambda: scenegen.bgtex(48, 32, spp=3, interp=1),
 }
 
 

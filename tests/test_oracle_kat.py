@@ -162,3 +162,28 @@ def test_oracle_render_is_deterministic_and_finite():
     b = o.render(0, nthreads=1)[0]
     assert np.array_equal(a.view(np.int32), b.view(np.int32))
     assert np.isfinite(a).all()
+
+
+def test_background_texture_transposed_at_1spp():
+    """Scene::SingleSample passes (row = x, col = y) to GetBackgroundColor (src/Scene.cpp:496-511,
+    544-566), so at 1 spp a replace_background texture is looked up at (u, v) = (y/nx, x/ny);
+    MultiSample (> 1 spp) uses (x/nx, y/ny); coordinates wrap (src/Texture.cpp:111-119)."""
+    nx, ny = 48, 32
+    for spp in (1, 4):
+        sc = scenegen.bgtex(nx, ny, spp=spp)
+        img, obj, _, _ = pyoracle.Oracle(sc).render(0)
+        tex = sc.textures[0].texels
+        h, w, _ = tex.shape
+        ys, xs = np.nonzero(obj == -1)
+        assert len(ys) > 100
+        for y, x in zip(ys[::37], xs[::37]):
+            if spp == 1:
+                u, v = np.float32(y) / np.float32(nx), np.float32(x) / np.float32(ny)
+            else:
+                u, v = np.float32(x) / np.float32(nx), np.float32(y) / np.float32(ny)
+            u, v = u - np.floor(u), v - np.floor(v)          # Texture::GetColorAtCoordinates wrap
+            i, j = min(int(u * np.float32(w)), w - 1), min(int(v * np.float32(h)), h - 1)
+            if spp == 1:
+                assert np.array_equal(img[y, x], tex[j, i]), (y, x)
+            else:   # every sample of a background pixel sees the same texel at NN
+                assert np.allclose(img[y, x], tex[j, i], rtol=1e-6), (y, x)
