@@ -1,0 +1,80 @@
+"""Edge cases of the render path on the GPU, each against the oracle bit for bit: empty and
+light-less scenes, degenerate image sizes, MaxRecursionDepth 0, many lights (the in-order
+light sum of Scene::RecursiveShading, src/Scene.cpp:279-350), every primary ray missing, and
+empty / NaN ray batches for rtg_trace_closest (src/Helper.cpp:28-30 returns {} on NaN)."""
+import numpy as np
+import pytest
+
+import pyoracle
+import rtg
+from rtg import _abi as A
+from rtg import scenegen
+from rtg.scene import Light, Scene
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(sc, **kw):
+    with rtg.Renderer(sc, device=0) as r:
+        img = r.render(0, **kw)
+    ref = pyoracle.Oracle(sc).render(0, **kw)[0]      # same row shard (others stay 0)
+    assert img.shape == ref.shape
+    assert np.array_equal(np.isnan(img), np.isnan(ref))
+    assert np.array_equal(np.nan_to_num(img).view(np.int32), np.nan_to_num(ref).view(np.int32))
+    return img
+
+
+def test_empty_scene_is_background(gpu):
+    sc = Scene(background=(12, 34, 56), ambient=(1, 1, 1))
+    sc.cameras.append(scenegen._cam((0, 0, 0), (0, 0, -1), (0, 1, 0), 7, 5, spp=3))
+    img = _same(sc)
+    assert np.all(img == np.float32([12, 34, 56]))
+
+
+def test_scene_without_lights_is_ambient_only(gpu):
+    sc = scenegen.simple(20, 14)
+    sc.lights = []
+    _same(sc)
+
+
+@pytest.mark.parametrize("nx,ny,spp", [(1, 1, 1), (1, 1, 5), (1, 9, 2), (13, 1, 1), (37, 13, 3)])
+def test_degenerate_image_sizes(gpu, nx, ny, spp):
+    sc = scenegen.multilight(nx, ny, spp=spp)
+    _same(sc)
+    if ny > 1:
+        _same(sc, row_offset=1, row_stride=2, row_block=8)
+
+
+def test_max_recursion_depth_zero(gpu):
+    sc = scenegen.multilight(32, 24)
+    sc.max_depth = 0
+    _same(sc)
+
+
+def test_many_lights_in_order(gpu):
+    sc = scenegen.simple(24, 18)
+    rng = np.random.default_rng(3)
+    for k in range(24):
+        kind = (A.LIGHT_POINT, A.LIGHT_DIRECTIONAL, A.LIGHT_SPOT)[k % 3]
+        sc.lights.append(Light(type=kind, position=tuple(rng.uniform(-3, 3, 3) + (0, 4, 0)),
+                               direction=tuple(rng.uniform(-1, 1, 3) - (0, 1, 0)),
+                               intensity=tuple(rng.uniform(10, 400, 3)), coverage_deg=40, falloff_deg=20))
+    _same(sc)
+
+
+def test_all_primary_rays_miss(gpu):
+    sc = scenegen.simple(16, 12)
+    sc.cameras[0].gaze = np.float32([0, 1, 0])        # looking up, away from every object
+    sc.cameras[0].up = np.float32([0, 0, 1])
+    img = _same(sc)
+    assert np.all(img == 0)
+
+
+def test_trace_empty_and_nan_batches(gpu):
+    sc = scenegen.simple(8, 8)
+    with rtg.Renderer(sc, device=0) as r:
+        h = r.trace(np.zeros((0, 3), np.float32), np.zeros((0, 3), np.float32))
+        assert len(h["full"]) == 0
+        nan = np.float32(np.nan)
+        h = r.trace([(0, 0, 0), (nan, 0, 0), (0, 0, 0)], [(0, 0, -1), (0, 0, -1), (nan, 0, -1)])
+        assert list(h["full"]) == [1, 0, 0]
