@@ -432,7 +432,7 @@ struct rtg_scene {
     std::vector<Lane> lanes;
     DBuf d_acc, d_counters, d_stats;
     rtg_render_stats stats{};
-    int num_lanes = 3;                       // default passes in flight (env RTG_STREAMS overrides)
+    int num_lanes = 8;                       // default passes in flight (env RTG_STREAMS overrides)
     int bvh_builder = RTG_BVH_AUTO;
     double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
     int bvh_gpu_objects = 0;                 // objects whose BVH the GPU built
@@ -1028,16 +1028,31 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     if (npix_ll > (1LL << 30)) return fail(RTG_ERR_UNSUPPORTED, "image too large");
     int npix = (int)npix_ll;
     int total = cam->num_samples;
-    // auto batch: 8M-ray passes, but at least one pass per stream in flight for small frames
-    // (a multi-GPU rank's row shard) so one pass's level tail overlaps another's work
-    // (1/8 of the 1080p64 dragon frame: 9.6 -> 9.0 ms with 5.5M-ray passes)
+    // auto batch: a whole multiple of the lanes in flight, as few passes as the 24M-ray cap
+    // allows, at least 2M rays each -- every lane gets the same number of equal passes, so the
+    // lanes' level tails end together and overlap each other's work (1080p64 dragon, passes x
+    // lanes: 1 GPU 16x3 -> 8x8 58.2 -> 58.1 ms; a 1/4 row shard 4x3 -> 8x8 16.0 -> 15.2 ms; a 1/8
+    // shard 3x3 -> 8x8 9.15 -> 8.1 ms)
     const int lanes_req = o.streams > 0 ? std::min(o.streams, 8) : s->num_lanes;
     const long long frame_rays = (long long)npix * total;
-    long long max_batch = o.max_batch_rays > 0 ? o.max_batch_rays
-                        : std::min(8LL << 20, std::max(2LL << 20, frame_rays / std::max(1, lanes_req) + 1));
-    // passes: all samples of a pixel range (chunks of samples only when spp exceeds the batch)
-    const int ns_chunk = (int)std::max<long long>(1, std::min<long long>(total, max_batch));
-    const int np_pass = (int)std::max<long long>(1, std::min<long long>(npix, max_batch / ns_chunk));
+    int ns_chunk, np_pass;
+    if (o.max_batch_rays > 0) {
+        const long long max_batch = o.max_batch_rays;
+        // passes: all samples of a pixel range (chunks of samples only when spp exceeds the batch)
+        ns_chunk = (int)std::max<long long>(1, std::min<long long>(total, max_batch));
+        np_pass = (int)std::max<long long>(1, std::min<long long>(npix, max_batch / ns_chunk));
+    } else {
+        const long long kMin = 2LL << 20, kMax = 24LL << 20;
+        const long long lanes_eff = std::max(1LL, std::min<long long>(lanes_req, (frame_rays + kMin - 1) / kMin));
+        const long long passes = lanes_eff * ((frame_rays + lanes_eff * kMax - 1) / (lanes_eff * kMax));
+        if (total > kMax) {                 // absurd spp: sample chunks of one pixel
+            ns_chunk = (int)kMax;
+            np_pass = 1;
+        } else {
+            ns_chunk = total;
+            np_pass = (int)std::max<long long>(1, (npix + passes - 1) / passes);   // `passes` pixel ranges
+        }
+    }
     int exhaustive = o.traversal == 1;
     if (cam->integrator != RTG_INTEGRATOR_REFERENCE && cam->integrator != RTG_INTEGRATOR_PATH)
         return fail(RTG_ERR_INVALID, "unknown integrator");
