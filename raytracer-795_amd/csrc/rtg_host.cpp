@@ -1146,6 +1146,11 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             launch_shade(sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                          Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), Ln.rays.as<RayRec>(),
                          Ln.meta.as<RayMeta>(), qc, n, ln.st);
+        // the next level's size is known once shade is done: read it back now, so the host can
+        // enqueue that level while this level's shadow queries still run (no host round trip
+        // between the levels on the stream)
+        HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
+        HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
         launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
@@ -1156,8 +1161,6 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), Lc.shadows.as<ShadowRec>(), nL,
                              ln.levels[0].nodes.as<NodeRec>(), level, n, ln.st);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
-        HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
         return RTG_OK;
     };
     auto start_pass = [&](Lane& ln) -> int {
@@ -1225,6 +1228,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             stt.trace_ms += a;
             stt.trace_launches++;
             if (nL > 0) {
+                HIP_TRY(hipEventSynchronize(ln.ev_t[3]));   // the count arrives before the shadow pass ends
                 HIP_TRY(hipEventElapsedTime(&b, ln.ev_t[2], ln.ev_t[3]));
                 stt.shadow_ms += b;
                 stt.shadow_launches++;
