@@ -225,8 +225,8 @@ typedef struct rtg_render_opts {
     int32_t collect_stats;   /* 1 = count BVH node visits / triangle tests (slower) */
     int32_t collect_timing;  /* 1 = HIP-event time every closest-hit / shadow launch */
     int32_t streams;         /* passes in flight on separate HIP streams (0 = library default, 8) */
-    int32_t row_block;       /* rows per shard interleave block (0/1 = single rows; 8 keeps each rank's
-                                8x8 pixel tiles image-contiguous) */
+    int32_t row_block;       /* rows per shard interleave block (0/1 = single rows; the pass's pixel
+                                tiles become (64/b) x b for b = 1, 2, 4, so they stay image-contiguous) */
     int32_t compact_rows;    /* 1: the output holds only the owned rows, in image order
                                 (rows_owned*nx*3 floats; rows_owned = rtg_shard_rows()), for a
                                 gather of the shards instead of a full-frame reduce */

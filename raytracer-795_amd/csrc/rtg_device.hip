@@ -1246,22 +1246,25 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
 // ------------------------------------------------------------------ camera / background
 // Tiled order of the owned pixels: bands of 8 owned rows, each band in blocks of 8 columns
 // (edge bands/blocks narrower), row-major inside a block.  t -> (x, k = owned-row index).
-DEV void tile_pixel(int t, int nx, int rows_owned, int& x, int& k) {
-    const int band = t / (8 * nx);
-    const int u = t - band * 8 * nx;
-    const int hb = min(8, rows_owned - 8 * band);
-    const int c = u / (8 * hb);
-    const int u2 = u - c * 8 * hb;
-    const int wb = min(8, nx - 8 * c);
+// Pixel order of a pass: tiles of (64 / th) x th pixels over the owned rows, row-major inside a
+// tile; th = the shard's row block (<= 8), so a tile is always image-contiguous.
+DEV void tile_pixel(int t, int nx, int rows_owned, int th, int& x, int& k) {
+    const int tw = 64 / th;
+    const int band = t / (th * nx);
+    const int u = t - band * th * nx;
+    const int hb = min(th, rows_owned - th * band);
+    const int c = u / (tw * hb);
+    const int u2 = u - c * tw * hb;
+    const int wb = min(tw, nx - tw * c);
     const int r = u2 / wb;
-    x = 8 * c + (u2 - r * wb);
-    k = 8 * band + r;
+    x = tw * c + (u2 - r * wb);
+    k = th * band + r;
 }
 DEV void slot_pixel(const CameraDev& cam, const PassDev& ps, int slot, uint32_t& pixel, uint32_t& sample, int& x,
                     int& y) {
     const int pl = slot / ps.ns, sl = slot - pl * ps.ns;
     int k;
-    tile_pixel(ps.p0 + pl, cam.nx, ps.rows_owned, x, k);
+    tile_pixel(ps.p0 + pl, cam.nx, ps.rows_owned, ps.tile_h, x, k);
     y = shard_row(k, ps.row_offset, ps.row_stride, ps.row_block);
     pixel = (uint32_t)(y * cam.nx + x);
     sample = (uint32_t)(ps.s0 + sl);
@@ -1988,7 +1991,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ 
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ps.npass) return;
     int x, k;
-    tile_pixel(ps.p0 + j, nx, ps.rows_owned, x, k);
+    tile_pixel(ps.p0 + j, nx, ps.rows_owned, ps.tile_h, x, k);
     const size_t p = (size_t)k * nx + x;        // acc is in natural owned-row order
     f3 a;
     int s = 0;

@@ -1094,6 +1094,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             ps.s0 = s0; ps.ns = std::min(ns_chunk, total - s0);
             ps.p0 = p0; ps.npass = std::min(np_pass, npix - p0);
             ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned; ps.row_block = block;
+            ps.tile_h = stride > 1 && block < 8 ? (block >= 4 ? 4 : block >= 2 ? 2 : 1) : 8;
             plist.push_back(ps);
         }
     const int nranges = npix > 0 ? (npix + np_pass - 1) / np_pass : 1;

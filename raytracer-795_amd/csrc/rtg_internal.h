@@ -160,12 +160,13 @@ struct PathRec {       // 16 B
     int flags;         // bit 0: previous bounce specular; bits 8..: medium material (1-based, 0 none)
 };
 
-// One batch ("pass") of the frame: pixels [p0, p0 + npass) of the tiled pixel order (8x8
+// One batch ("pass") of the frame: pixels [p0, p0 + npass) of the tiled pixel order (8x8, or 16x4 / 32x2 / 64x1 for row-block shards;
 // blocks over the rank's owned rows) x samples [s0, s0 + ns).  Ray slot = (t - p0) * ns + (s - s0):
 // all samples of a pixel are adjacent, so a wavefront traces near-identical rays.
 struct PassDev {
     int s0, ns, p0, npass;
     int row_offset, row_stride, rows_owned, row_block;
+    int tile_h;        // pixel tile height: 8, or the shard's row block when that is smaller
 };
 
 // Shard row ownership (rtg_render_opts.row_block): owned row k <-> image row y.

@@ -1,10 +1,10 @@
 """Multi-GPU pixel sharding.
 
-Rank r of G renders the rows y with (y // B) % G == r, B = ROW_BLOCK = 8 (the reference
-interleaves pixel columns over its 8 threads, src/Scene.cpp:400-423; 8-row blocks keep
-each GPU's 8x8 pixel tiles image-contiguous, so its rays stay as coherent as on one GPU,
-while the fine interleave keeps the ranks' loads balanced) into a zero-initialised
-full-frame accumulator.  Summing the G frames is exact because
+Rank r of G renders the rows y with (y // B) % G == r, B = ROW_BLOCK = 4 (the reference
+interleaves pixel columns over its 8 threads, src/Scene.cpp:400-423; the library tiles a
+shard's pixels 16x4 for B = 4, so each tile stays image-contiguous and its rays as coherent
+as on one GPU, while 270 blocks over the ranks keep their loads balanced) into a
+zero-initialised full-frame accumulator, or compactly (gather_frame).  Summing the G frames is exact because
 their supports are disjoint (x + 0 == x), so one reduce (RCCL over xGMI on GPUs, gloo on
 CPU) yields the single-device frame bit for bit.
 """
@@ -13,7 +13,7 @@ from __future__ import annotations
 import numpy as np
 
 
-ROW_BLOCK = 8
+ROW_BLOCK = 4
 
 
 def owned_rows(ny: int, rank: int, world: int, block: int = ROW_BLOCK) -> np.ndarray:

@@ -42,7 +42,7 @@ def test_degenerate_image_sizes(gpu, nx, ny, spp):
     sc = scenegen.multilight(nx, ny, spp=spp)
     _same(sc)
     if ny > 1:
-        _same(sc, row_offset=1, row_stride=2, row_block=8)
+        _same(sc, row_offset=1, row_stride=2, row_block=4)
 
 
 def test_max_recursion_depth_zero(gpu):

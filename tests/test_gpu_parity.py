@@ -77,7 +77,7 @@ def test_trace_matches_oracle(gpu, name):
             assert np.array_equal(h["normal"][m].view(np.int32), ref["normal"][m].view(np.int32))
 
 
-@pytest.mark.parametrize("block", [1, 8, 5])
+@pytest.mark.parametrize("block", [1, 2, 4, 5, 8])
 def test_row_shards_sum_to_full_frame(gpu, block):
     """Multi-GPU partition (rows (y // block) % G == rank, incl. a partial last block) +
     exact sum == the single-device frame; each shard writes exactly its own rows."""
