@@ -478,6 +478,7 @@ bool read_exr_rgba(const std::string& path, std::vector<float>& rgba, int& w, in
     if (tiled && (tx == 0 || ty == 0 || level_mode != 0)) { err = "only one-level tiled EXR images are supported: " + path; return false; }
     const int lpb = comp == kZip ? 16 : comp == kPiz ? 32 : 1;
     const int64_t nchunks = tiled ? (int64_t)((w + tx - 1) / tx) * ((h + ty - 1) / ty) : (h + lpb - 1) / lpb;
+    if (nchunks <= 0 || (uint64_t)nchunks * 8 > file.size()) { err = "EXR offset table exceeds the file: " + path; return false; }
     std::vector<uint64_t> offsets(nchunks);
     for (auto& o : offsets) o = r.u64();
     if (!r.ok) { err = "truncated EXR offset table: " + path; return false; }
@@ -492,9 +493,12 @@ bool read_exr_rgba(const std::string& path, std::vector<float>& rgba, int& w, in
         if (tiled) {
             const int tix = c.i32(), tiy = c.i32();
             c.i32(); c.i32();               // level (0, 0)
+            if (tix < 0 || tiy < 0 || (int64_t)tix * tx >= w || (int64_t)tiy * ty >= h) {
+                err = "bad EXR tile coordinates in " + path;
+                return false;
+            }
             x0 = tix * (int)tx;
             y0 = tiy * (int)ty;
-            if (tix < 0 || tiy < 0 || x0 >= w || y0 >= h) { err = "bad EXR tile coordinates in " + path; return false; }
             nx = std::min<int>((int)tx, w - x0);
             ny = std::min<int>((int)ty, h - y0);
         } else {
