@@ -438,6 +438,18 @@ struct rtg_scene {
     int bvh_gpu_objects = 0;                 // objects whose BVH the GPU built
 };
 
+// Exceptions (std::bad_alloc from host containers, ...) never cross the C ABI.
+template <class F>
+static int32_t guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return fail(RTG_ERR_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(RTG_ERR_INVALID, std::string("internal error: ") + e.what());
+    }
+}
+
 extern "C" {
 
 int32_t rtg_abi_version(void) { return RTG_ABI_VERSION; }
@@ -950,33 +962,35 @@ int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene**
 }
 
 int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rtg_build_opts* opts, rtg_scene** out) {
-    if (!out) return fail(RTG_ERR_INVALID, "null out pointer");
-    if (opts && (opts->bvh_builder < RTG_BVH_AUTO || opts->bvh_builder > RTG_BVH_GPU))
-        return fail(RTG_ERR_INVALID, "bvh_builder");
-    *out = nullptr;
-    int rc = validate(desc);
-    if (rc) return rc;
-    if (device >= 0) {
-        int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RTG_ERR_NO_DEVICE, "no HIP device");
-        if (device >= n) return fail(RTG_ERR_NO_DEVICE, "device index out of range");
-        HIP_TRY(hipSetDevice(device));
-    } else if (device != RTG_DEVICE_HOST_ONLY) {
-        return fail(RTG_ERR_INVALID, "device index");
-    }
-    rtg_scene* s = new (std::nothrow) rtg_scene();
-    if (!s) return fail(RTG_ERR_OOM, "host allocation");
-    s->device = device;
-    if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
-    s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
-    rc = build_scene(s, desc);
-    if (rc) {
-        scene_free(s);
-        delete s;
-        return rc;
-    }
-    *out = s;
-    return RTG_OK;
+    return guarded([&]() -> int32_t {
+        if (!out) return fail(RTG_ERR_INVALID, "null out pointer");
+        if (opts && (opts->bvh_builder < RTG_BVH_AUTO || opts->bvh_builder > RTG_BVH_GPU))
+            return fail(RTG_ERR_INVALID, "bvh_builder");
+        *out = nullptr;
+        int rc = validate(desc);
+        if (rc) return rc;
+        if (device >= 0) {
+            int n = 0;
+            if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RTG_ERR_NO_DEVICE, "no HIP device");
+            if (device >= n) return fail(RTG_ERR_NO_DEVICE, "device index out of range");
+            HIP_TRY(hipSetDevice(device));
+        } else if (device != RTG_DEVICE_HOST_ONLY) {
+            return fail(RTG_ERR_INVALID, "device index");
+        }
+        rtg_scene* s = new (std::nothrow) rtg_scene();
+        if (!s) return fail(RTG_ERR_OOM, "host allocation");
+        s->device = device;
+        if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
+        s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
+        rc = build_scene(s, desc);
+        if (rc) {
+            scene_free(s);
+            delete s;
+            return rc;
+        }
+        *out = s;
+        return RTG_OK;
+    });
 }
 
 // Camera::Camera (src/Camera.cpp:7-61)
@@ -1288,10 +1302,12 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
 
 int32_t rtg_render_device(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, float* rgb_out_device,
                           void* stream) {
-    if (!s || !cam || !rgb_out_device) return fail(RTG_ERR_INVALID, "null argument");
-    if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
-    HIP_TRY(hipSetDevice(s->device));
-    return render_impl(s, cam, opts, rgb_out_device, (hipStream_t)stream);
+    return guarded([&]() -> int32_t {
+        if (!s || !cam || !rgb_out_device) return fail(RTG_ERR_INVALID, "null argument");
+        if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
+        HIP_TRY(hipSetDevice(s->device));
+        return render_impl(s, cam, opts, rgb_out_device, (hipStream_t)stream);
+    });
 }
 
 int32_t rtg_shard_rows(int32_t ny, int32_t row_offset, int32_t row_stride, int32_t row_block) {
@@ -1303,22 +1319,24 @@ int32_t rtg_shard_rows(int32_t ny, int32_t row_offset, int32_t row_stride, int32
 }
 
 int32_t rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, float* rgb_out) {
-    if (!s || !cam || !rgb_out) return fail(RTG_ERR_INVALID, "null argument");
-    if (cam->nx < 1 || cam->ny < 1) return fail(RTG_ERR_INVALID, "bad camera");
-    if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
-    HIP_TRY(hipSetDevice(s->device));
-    const int out_rows = opts && opts->compact_rows ? rtg_shard_rows(cam->ny, opts->row_offset, opts->row_stride,
-                                                                     opts->row_block) : cam->ny;
-    size_t bytes = sizeof(float) * 3 * (size_t)cam->nx * std::max(out_rows, 1);
-    float* d_out = nullptr;
-    HIP_TRY(hipMalloc(&d_out, bytes));
-    int rc = render_impl(s, cam, opts, d_out, nullptr);
-    if (rc == RTG_OK) {
-        hipError_t e = hipMemcpy(rgb_out, d_out, bytes, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) rc = fail(RTG_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
-    }
-    (void)hipFree(d_out);
-    return rc;
+    return guarded([&]() -> int32_t {
+        if (!s || !cam || !rgb_out) return fail(RTG_ERR_INVALID, "null argument");
+        if (cam->nx < 1 || cam->ny < 1) return fail(RTG_ERR_INVALID, "bad camera");
+        if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
+        HIP_TRY(hipSetDevice(s->device));
+        const int out_rows = opts && opts->compact_rows ? rtg_shard_rows(cam->ny, opts->row_offset, opts->row_stride,
+                                                                         opts->row_block) : cam->ny;
+        size_t bytes = sizeof(float) * 3 * (size_t)cam->nx * std::max(out_rows, 1);
+        float* d_out = nullptr;
+        HIP_TRY(hipMalloc(&d_out, bytes));
+        int rc = render_impl(s, cam, opts, d_out, nullptr);
+        if (rc == RTG_OK) {
+            hipError_t e = hipMemcpy(rgb_out, d_out, bytes, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) rc = fail(RTG_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+        }
+        (void)hipFree(d_out);
+        return rc;
+    });
 }
 
 static int check_tonemap(int32_t device, int32_t nx, int32_t ny, const rtg_tonemap_desc* tm) {
@@ -1334,34 +1352,38 @@ static int check_tonemap(int32_t device, int32_t nx, int32_t ny, const rtg_tonem
 
 int32_t rtg_tonemap_device(int32_t device, const float* hdr, int32_t nx, int32_t ny, const rtg_tonemap_desc* tm,
                            float* out, void* stream) {
-    if (!hdr || !out) return fail(RTG_ERR_INVALID, "null argument");
-    int rc = check_tonemap(device, nx, ny, tm);
-    if (rc) return rc;
-    HIP_TRY(hipSetDevice(device));
-    std::string err;
-    if (tonemap_device(hdr, nx, ny, *tm, out, (hipStream_t)stream, err)) return fail(RTG_ERR_HIP, err);
-    return RTG_OK;
+    return guarded([&]() -> int32_t {
+        if (!hdr || !out) return fail(RTG_ERR_INVALID, "null argument");
+        int rc = check_tonemap(device, nx, ny, tm);
+        if (rc) return rc;
+        HIP_TRY(hipSetDevice(device));
+        std::string err;
+        if (tonemap_device(hdr, nx, ny, *tm, out, (hipStream_t)stream, err)) return fail(RTG_ERR_HIP, err);
+        return RTG_OK;
+    });
 }
 
 int32_t rtg_tonemap(int32_t device, const float* hdr, int32_t nx, int32_t ny, const rtg_tonemap_desc* tm, float* out) {
-    if (!hdr || !out) return fail(RTG_ERR_INVALID, "null argument");
-    int rc = check_tonemap(device, nx, ny, tm);
-    if (rc) return rc;
-    HIP_TRY(hipSetDevice(device));
-    const size_t bytes = sizeof(float) * 3 * (size_t)nx * ny;
-    float *dh = nullptr, *dl = nullptr;
-    if (hipMalloc(&dh, bytes) != hipSuccess || hipMalloc(&dl, bytes) != hipSuccess) {
-        if (dh) (void)hipFree(dh);
-        return fail(RTG_ERR_OOM, "tonemap buffers");
-    }
-    std::string err;
-    rc = RTG_OK;
-    if (hipMemcpy(dh, hdr, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = fail(RTG_ERR_HIP, "tonemap upload");
-    else if (tonemap_device(dh, nx, ny, *tm, dl, nullptr, err)) rc = fail(RTG_ERR_HIP, err);
-    else if (hipMemcpy(out, dl, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RTG_ERR_HIP, "tonemap download");
-    (void)hipFree(dh);
-    (void)hipFree(dl);
-    return rc;
+    return guarded([&]() -> int32_t {
+        if (!hdr || !out) return fail(RTG_ERR_INVALID, "null argument");
+        int rc = check_tonemap(device, nx, ny, tm);
+        if (rc) return rc;
+        HIP_TRY(hipSetDevice(device));
+        const size_t bytes = sizeof(float) * 3 * (size_t)nx * ny;
+        float *dh = nullptr, *dl = nullptr;
+        if (hipMalloc(&dh, bytes) != hipSuccess || hipMalloc(&dl, bytes) != hipSuccess) {
+            if (dh) (void)hipFree(dh);
+            return fail(RTG_ERR_OOM, "tonemap buffers");
+        }
+        std::string err;
+        rc = RTG_OK;
+        if (hipMemcpy(dh, hdr, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = fail(RTG_ERR_HIP, "tonemap upload");
+        else if (tonemap_device(dh, nx, ny, *tm, dl, nullptr, err)) rc = fail(RTG_ERR_HIP, err);
+        else if (hipMemcpy(out, dl, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(RTG_ERR_HIP, "tonemap download");
+        (void)hipFree(dh);
+        (void)hipFree(dl);
+        return rc;
+    });
 }
 
 int32_t rtg_scene_build_stats(const rtg_scene* s, rtg_build_stats* out) {
@@ -1379,43 +1401,47 @@ int32_t rtg_last_render_stats(const rtg_scene* s, rtg_render_stats* out) {
 }
 
 int32_t rtg_trace_closest(rtg_scene* s, const rtg_ray* rays, int32_t n, rtg_hit* hits, int32_t traversal) {
-    if (!s || n < 0 || (n && (!rays || !hits))) return fail(RTG_ERR_INVALID, "bad arguments");
-    if (n == 0) return RTG_OK;
-    if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot trace");
-    HIP_TRY(hipSetDevice(s->device));
-    std::vector<RayRec> rr(n);
-    for (int i = 0; i < n; i++) {
-        rr[i].o_t = make_float4(rays[i].origin[0], rays[i].origin[1], rays[i].origin[2], rays[i].time);
-        rr[i].d = make_float4(rays[i].direction[0], rays[i].direction[1], rays[i].direction[2], FLT_MAX);
-    }
-    DBuf dr, dh, dout;
-    int rc;
-    if ((rc = upload(dr, rr)) || (rc = dh.grow(sizeof(HitRec) * (size_t)n)) || (rc = dout.grow(sizeof(rtg_hit) * (size_t)n))) {
+    return guarded([&]() -> int32_t {
+        if (!s || n < 0 || (n && (!rays || !hits))) return fail(RTG_ERR_INVALID, "bad arguments");
+        if (n == 0) return RTG_OK;
+        if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot trace");
+        HIP_TRY(hipSetDevice(s->device));
+        std::vector<RayRec> rr(n);
+        for (int i = 0; i < n; i++) {
+            rr[i].o_t = make_float4(rays[i].origin[0], rays[i].origin[1], rays[i].origin[2], rays[i].time);
+            rr[i].d = make_float4(rays[i].direction[0], rays[i].direction[1], rays[i].direction[2], FLT_MAX);
+        }
+        DBuf dr, dh, dout;
+        int rc;
+        if ((rc = upload(dr, rr)) || (rc = dh.grow(sizeof(HitRec) * (size_t)n)) || (rc = dout.grow(sizeof(rtg_hit) * (size_t)n))) {
+            dr.release(); dh.release(); dout.release();
+            return rc;
+        }
+        launch_trace(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), n, traversal == 1, nullptr, nullptr);
+        launch_hit_details(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), dout.as<rtg_hit>(), s->d_origprim.as<int>(), n, nullptr);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpy(hits, dout.p, sizeof(rtg_hit) * (size_t)n, hipMemcpyDeviceToHost);
         dr.release(); dh.release(); dout.release();
-        return rc;
-    }
-    launch_trace(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), n, traversal == 1, nullptr, nullptr);
-    launch_hit_details(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), dout.as<rtg_hit>(), s->d_origprim.as<int>(), n, nullptr);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpy(hits, dout.p, sizeof(rtg_hit) * (size_t)n, hipMemcpyDeviceToHost);
-    dr.release(); dh.release(); dout.release();
-    if (e != hipSuccess) return fail(RTG_ERR_HIP, std::string("trace: ") + hipGetErrorString(e));
-    return RTG_OK;
+        if (e != hipSuccess) return fail(RTG_ERR_HIP, std::string("trace: ") + hipGetErrorString(e));
+        return RTG_OK;
+    });
 }
 
 int32_t rtg_scene_object_bvh(const rtg_scene* s, int32_t object, int32_t* num_prims, int32_t* num_nodes, int32_t* perm,
                              int32_t* nodes, float* boxes) {
-    if (!s || object < 0 || object >= s->num_objects) return fail(RTG_ERR_INVALID, "object index");
-    const ObjBVH& b = s->bvh[object];
-    if (num_prims) *num_prims = (int)b.perm.size();
-    if (num_nodes) *num_nodes = (int)b.nodes.size();
-    if (perm) memcpy(perm, b.perm.data(), sizeof(int) * b.perm.size());
-    for (size_t k = 0; k < b.nodes.size(); k++) {
-        const HNode& h = b.nodes[k];
-        if (nodes) { nodes[4 * k] = h.left; nodes[4 * k + 1] = h.right; nodes[4 * k + 2] = h.start; nodes[4 * k + 3] = h.end; }
-        if (boxes) for (int z = 0; z < 3; z++) { boxes[6 * k + z] = h.mn[z]; boxes[6 * k + 3 + z] = h.mx[z]; }
-    }
-    return RTG_OK;
+    return guarded([&]() -> int32_t {
+        if (!s || object < 0 || object >= s->num_objects) return fail(RTG_ERR_INVALID, "object index");
+        const ObjBVH& b = s->bvh[object];
+        if (num_prims) *num_prims = (int)b.perm.size();
+        if (num_nodes) *num_nodes = (int)b.nodes.size();
+        if (perm) memcpy(perm, b.perm.data(), sizeof(int) * b.perm.size());
+        for (size_t k = 0; k < b.nodes.size(); k++) {
+            const HNode& h = b.nodes[k];
+            if (nodes) { nodes[4 * k] = h.left; nodes[4 * k + 1] = h.right; nodes[4 * k + 2] = h.start; nodes[4 * k + 3] = h.end; }
+            if (boxes) for (int z = 0; z < 3; z++) { boxes[6 * k + z] = h.mn[z]; boxes[6 * k + 3 + z] = h.mx[z]; }
+        }
+        return RTG_OK;
+    });
 }
 
 int32_t rtg_scene_object_matrices(const rtg_scene* s, int32_t top, float* inv16, float* invT16) {

@@ -21,6 +21,7 @@
 #include <cstdint>
 #include <fstream>
 #include <sstream>
+#include <stdexcept>
 
 namespace rtgh {
 namespace {
@@ -414,7 +415,8 @@ bool decode_chunk(int comp, const unsigned char* data, size_t n, int nx, int ny,
 
 }  // namespace
 
-bool read_exr_rgba(const std::string& path, std::vector<float>& rgba, int& w, int& h, std::string& err) {
+namespace {
+bool read_exr_impl(const std::string& path, std::vector<float>& rgba, int& w, int& h, std::string& err) {
     std::string file;
     {
         std::ifstream f(path, std::ios::binary);
@@ -475,7 +477,7 @@ bool read_exr_rgba(const std::string& path, std::vector<float>& rgba, int& w, in
     }
     w = xmax - xmin + 1;
     h = ymax - ymin + 1;
-    if (tiled && (tx == 0 || ty == 0 || level_mode != 0)) { err = "only one-level tiled EXR images are supported: " + path; return false; }
+    if (tiled && (tx == 0 || ty == 0 || tx > (1u << 20) || ty > (1u << 20) || level_mode != 0)) { err = "only one-level tiled EXR images are supported: " + path; return false; }
     const int lpb = comp == kZip ? 16 : comp == kPiz ? 32 : 1;
     const int64_t nchunks = tiled ? (int64_t)((w + tx - 1) / tx) * ((h + ty - 1) / ty) : (h + lpb - 1) / lpb;
     if (nchunks <= 0 || (uint64_t)nchunks * 8 > file.size()) { err = "EXR offset table exceeds the file: " + path; return false; }
@@ -549,6 +551,17 @@ bool read_exr_rgba(const std::string& path, std::vector<float>& rgba, int& w, in
         rgba[4 * i + 3] = iA >= 0 ? planes[iA][i] : 1.0f;
     }
     return true;
+}
+
+}  // namespace
+
+bool read_exr_rgba(const std::string& path, std::vector<float>& rgba, int& w, int& h, std::string& err) {
+    try {                               // the C ABI above never throws
+        return read_exr_impl(path, rgba, w, h, err);
+    } catch (const std::exception& e) {
+        err = std::string("EXR decode of ") + path + ": " + e.what();
+        return false;
+    }
 }
 
 }  // namespace rtgh

@@ -949,20 +949,34 @@ uint16_t half_of(float f) {            // IEEE binary16, round to nearest even
 
 }  // namespace
 
+// Exceptions (std::bad_alloc from host containers, ...) never cross the C ABI.
+template <class F>
+static int32_t guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return fail(RTG_ERR_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(RTG_ERR_INVALID, std::string("internal error: ") + e.what());
+    }
+}
+
 extern "C" {
 
 const char* rtgh_last_error(void) { return g_err.c_str(); }
 
 int32_t rtgh_parse_xml(const char* path, rtgh_scene** out) {
-    if (!path || !out) return fail(RTG_ERR_INVALID, "null argument");
-    *out = nullptr;
-    rtgh_scene* sc = new (std::nothrow) rtgh_scene();
-    if (!sc) return fail(RTG_ERR_OOM, "host allocation");
-    int rc = parse(path, *sc);
-    if (rc) { delete sc; return rc; }
-    flatten(*sc);
-    *out = sc;
-    return RTG_OK;
+    return guarded([&]() -> int32_t {
+        if (!path || !out) return fail(RTG_ERR_INVALID, "null argument");
+        *out = nullptr;
+        rtgh_scene* sc = new (std::nothrow) rtgh_scene();
+        if (!sc) return fail(RTG_ERR_OOM, "host allocation");
+        int rc = parse(path, *sc);
+        if (rc) { delete sc; return rc; }
+        flatten(*sc);
+        *out = sc;
+        return RTG_OK;
+    });
 }
 
 const rtg_scene_desc* rtgh_scene_desc(const rtgh_scene* s) { return s ? &s->desc : nullptr; }
@@ -988,129 +1002,135 @@ int32_t rtgh_camera_tonemap(const rtgh_scene* s, int32_t i, rtg_tonemap_desc* ou
 void rtgh_free(rtgh_scene* s) { delete s; }
 
 int32_t rtgh_read_image(const char* path, float** rgb, int32_t* nx, int32_t* ny) {
-    if (!path || !rgb || !nx || !ny) return fail(RTG_ERR_INVALID, "null argument");
-    *rgb = nullptr;
-    std::vector<float> px;
-    int w = 0, h = 0;
-    int rc = load_image(path, px, w, h);
-    if (rc) return rc;
-    float* out = (float*)malloc(sizeof(float) * (px.empty() ? 1 : px.size()));
-    if (!out) return fail(RTG_ERR_OOM, "host allocation");
-    memcpy(out, px.data(), sizeof(float) * px.size());
-    *rgb = out;
-    *nx = w;
-    *ny = h;
-    return RTG_OK;
+    return guarded([&]() -> int32_t {
+        if (!path || !rgb || !nx || !ny) return fail(RTG_ERR_INVALID, "null argument");
+        *rgb = nullptr;
+        std::vector<float> px;
+        int w = 0, h = 0;
+        int rc = load_image(path, px, w, h);
+        if (rc) return rc;
+        float* out = (float*)malloc(sizeof(float) * (px.empty() ? 1 : px.size()));
+        if (!out) return fail(RTG_ERR_OOM, "host allocation");
+        memcpy(out, px.data(), sizeof(float) * px.size());
+        *rgb = out;
+        *nx = w;
+        *ny = h;
+        return RTG_OK;
+    });
 }
 
 void rtgh_free_image(float* rgb) { free(rgb); }
 
 int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t ny) {
-    if (!name || !rgb || nx < 1 || ny < 1) return fail(RTG_ERR_INVALID, "bad image");
-    FILE* f = fopen(name, "wb");
-    if (!f) return fail(RTG_ERR_INVALID, std::string("cannot write ") + name);
-    if (is_png(name)) {                      // Image::SavePng (src/Image.cpp:222-263): P3 text
-        fprintf(f, "P3\n%d %d\n255\n", nx, ny);
-        std::string row;
-        for (int y = 0; y < ny; y++) {
-            row.clear();
-            for (int x = 0; x < nx * 3; x++) {
-                float v = rgb[(size_t)y * nx * 3 + x];
-                if (v > 255) v = 255;
-                const int u = (v == v && v > 0) ? ((int)truncf(v) & 0xFF) : 0;
-                row += std::to_string(u);
-                row += (x + 1 < nx * 3) ? " " : " \n";
+    return guarded([&]() -> int32_t {
+        if (!name || !rgb || nx < 1 || ny < 1) return fail(RTG_ERR_INVALID, "bad image");
+        FILE* f = fopen(name, "wb");
+        if (!f) return fail(RTG_ERR_INVALID, std::string("cannot write ") + name);
+        if (is_png(name)) {                      // Image::SavePng (src/Image.cpp:222-263): P3 text
+            fprintf(f, "P3\n%d %d\n255\n", nx, ny);
+            std::string row;
+            for (int y = 0; y < ny; y++) {
+                row.clear();
+                for (int x = 0; x < nx * 3; x++) {
+                    float v = rgb[(size_t)y * nx * 3 + x];
+                    if (v > 255) v = 255;
+                    const int u = (v == v && v > 0) ? ((int)truncf(v) & 0xFF) : 0;
+                    row += std::to_string(u);
+                    row += (x + 1 < nx * 3) ? " " : " \n";
+                }
+                fputs(row.c_str(), f);
             }
-            fputs(row.c_str(), f);
+        } else {                                 // ExrLibrary::SaveExr (src/Helper.cpp:415-466): HALF B,G,R
+            std::string h;
+            auto i32 = [&](int32_t v) { h.append((const char*)&v, 4); };
+            auto attr = [&](const char* n, const char* t, const std::string& data) {
+                h += n; h += '\0'; h += t; h += '\0'; i32((int32_t)data.size()); h += data;
+            };
+            h.append("\x76\x2f\x31\x01", 4);
+            i32(2);
+            std::string chl;
+            for (const char* ch : {"B", "G", "R"}) {
+                chl += ch; chl += '\0';
+                int32_t pt = 1; chl.append((const char*)&pt, 4);
+                chl += '\0'; chl.append(3, '\0');
+                int32_t one = 1; chl.append((const char*)&one, 4); chl.append((const char*)&one, 4);
+            }
+            chl += '\0';
+            attr("channels", "chlist", chl);
+            attr("compression", "compression", std::string(1, '\0'));
+            int32_t box[4] = {0, 0, nx - 1, ny - 1};
+            attr("dataWindow", "box2i", std::string((const char*)box, 16));
+            attr("displayWindow", "box2i", std::string((const char*)box, 16));
+            attr("lineOrder", "lineOrder", std::string(1, '\0'));
+            float par = 1.0f, swc[2] = {0, 0}, sww = 1.0f;
+            attr("pixelAspectRatio", "float", std::string((const char*)&par, 4));
+            attr("screenWindowCenter", "v2f", std::string((const char*)swc, 8));
+            attr("screenWindowWidth", "float", std::string((const char*)&sww, 4));
+            h += '\0';
+            const int64_t line_bytes = (int64_t)nx * 2 * 3;
+            const int64_t first = (int64_t)h.size() + 8 * (int64_t)ny;
+            for (int y = 0; y < ny; y++) { int64_t o = first + y * (8 + line_bytes); h.append((const char*)&o, 8); }
+            fwrite(h.data(), 1, h.size(), f);
+            std::vector<uint16_t> line((size_t)nx * 3);
+            for (int y = 0; y < ny; y++) {
+                int32_t hdr[2] = {y, (int32_t)line_bytes};
+                fwrite(hdr, 4, 2, f);
+                for (int c = 2, k = 0; c >= 0; c--, k++)
+                    for (int x = 0; x < nx; x++) line[(size_t)k * nx + x] = half_of(rgb[((size_t)y * nx + x) * 3 + c]);
+                fwrite(line.data(), 2, line.size(), f);
+            }
         }
-    } else {                                 // ExrLibrary::SaveExr (src/Helper.cpp:415-466): HALF B,G,R
-        std::string h;
-        auto i32 = [&](int32_t v) { h.append((const char*)&v, 4); };
-        auto attr = [&](const char* n, const char* t, const std::string& data) {
-            h += n; h += '\0'; h += t; h += '\0'; i32((int32_t)data.size()); h += data;
-        };
-        h.append("\x76\x2f\x31\x01", 4);
-        i32(2);
-        std::string chl;
-        for (const char* ch : {"B", "G", "R"}) {
-            chl += ch; chl += '\0';
-            int32_t pt = 1; chl.append((const char*)&pt, 4);
-            chl += '\0'; chl.append(3, '\0');
-            int32_t one = 1; chl.append((const char*)&one, 4); chl.append((const char*)&one, 4);
-        }
-        chl += '\0';
-        attr("channels", "chlist", chl);
-        attr("compression", "compression", std::string(1, '\0'));
-        int32_t box[4] = {0, 0, nx - 1, ny - 1};
-        attr("dataWindow", "box2i", std::string((const char*)box, 16));
-        attr("displayWindow", "box2i", std::string((const char*)box, 16));
-        attr("lineOrder", "lineOrder", std::string(1, '\0'));
-        float par = 1.0f, swc[2] = {0, 0}, sww = 1.0f;
-        attr("pixelAspectRatio", "float", std::string((const char*)&par, 4));
-        attr("screenWindowCenter", "v2f", std::string((const char*)swc, 8));
-        attr("screenWindowWidth", "float", std::string((const char*)&sww, 4));
-        h += '\0';
-        const int64_t line_bytes = (int64_t)nx * 2 * 3;
-        const int64_t first = (int64_t)h.size() + 8 * (int64_t)ny;
-        for (int y = 0; y < ny; y++) { int64_t o = first + y * (8 + line_bytes); h.append((const char*)&o, 8); }
-        fwrite(h.data(), 1, h.size(), f);
-        std::vector<uint16_t> line((size_t)nx * 3);
-        for (int y = 0; y < ny; y++) {
-            int32_t hdr[2] = {y, (int32_t)line_bytes};
-            fwrite(hdr, 4, 2, f);
-            for (int c = 2, k = 0; c >= 0; c--, k++)
-                for (int x = 0; x < nx; x++) line[(size_t)k * nx + x] = half_of(rgb[((size_t)y * nx + x) * 3 + c]);
-            fwrite(line.data(), 2, line.size(), f);
-        }
-    }
-    fclose(f);
-    return RTG_OK;
+        fclose(f);
+        return RTG_OK;
+    });
 }
 
 // Scene::renderScene (src/Scene.cpp:425-494): precompute once, render and save every camera.
 int32_t rtgh_render_scene(const char* xml_path, int32_t device, uint64_t seed, const char* out_dir) {
-    rtgh_scene* sc = nullptr;
-    int rc = rtgh_parse_xml(xml_path, &sc);
-    if (rc) return rc;
-    rtg_scene* gpu = nullptr;
-    rtg_build_opts bo{RTG_BVH_AUTO};
-    rc = rtg_scene_create_ex(&sc->desc, device, &bo, &gpu);
-    if (rc) { g_err = rtg_last_error(); rtgh_free(sc); return rc; }
-    printf("BVH construction complete.\n");
-    for (const CamData& c : sc->cameras) {
-        std::vector<float> rgb((size_t)c.d.nx * c.d.ny * 3);
-        rtg_render_opts o{};
-        o.seed = seed;
-        rc = rtg_render(gpu, &c.d, &o, rgb.data());
-        if (rc) { g_err = rtg_last_error(); break; }
-        std::string name = c.image_name;
-        if (out_dir && *out_dir) {
-            const size_t s = name.rfind('/');
-            name = std::string(out_dir) + "/" + (s == std::string::npos ? name : name.substr(s + 1));
-        }
-        // hw5 <Tonemap>: the tone-mapped image goes to the name with a .png extension (a .png
-        // ImageName is written tone-mapped instead of clamped), the HDR one to ImageName
-        const bool png = is_png(name.c_str());
-        if (!c.has_tonemap || !png) {
-            rc = rtgh_save_image(name.c_str(), rgb.data(), c.d.nx, c.d.ny);
-            if (rc) break;
-        }
-        if (c.has_tonemap) {
-            std::vector<float> ldr(rgb.size());
-            rc = rtg_tonemap(device, rgb.data(), c.d.nx, c.d.ny, &c.tm, ldr.data());
+    return guarded([&]() -> int32_t {
+        rtgh_scene* sc = nullptr;
+        int rc = rtgh_parse_xml(xml_path, &sc);
+        if (rc) return rc;
+        rtg_scene* gpu = nullptr;
+        rtg_build_opts bo{RTG_BVH_AUTO};
+        rc = rtg_scene_create_ex(&sc->desc, device, &bo, &gpu);
+        if (rc) { g_err = rtg_last_error(); rtgh_free(sc); return rc; }
+        printf("BVH construction complete.\n");
+        for (const CamData& c : sc->cameras) {
+            std::vector<float> rgb((size_t)c.d.nx * c.d.ny * 3);
+            rtg_render_opts o{};
+            o.seed = seed;
+            rc = rtg_render(gpu, &c.d, &o, rgb.data());
             if (rc) { g_err = rtg_last_error(); break; }
-            const size_t dot = name.rfind('.'), sl = name.rfind('/');
-            const std::string tname = (dot == std::string::npos || (sl != std::string::npos && dot < sl) ? name : name.substr(0, dot)) + ".png";
-            rc = rtgh_save_image(tname.c_str(), ldr.data(), c.d.nx, c.d.ny);
-            if (rc) break;
+            std::string name = c.image_name;
+            if (out_dir && *out_dir) {
+                const size_t s = name.rfind('/');
+                name = std::string(out_dir) + "/" + (s == std::string::npos ? name : name.substr(s + 1));
+            }
+            // hw5 <Tonemap>: the tone-mapped image goes to the name with a .png extension (a .png
+            // ImageName is written tone-mapped instead of clamped), the HDR one to ImageName
+            const bool png = is_png(name.c_str());
+            if (!c.has_tonemap || !png) {
+                rc = rtgh_save_image(name.c_str(), rgb.data(), c.d.nx, c.d.ny);
+                if (rc) break;
+            }
+            if (c.has_tonemap) {
+                std::vector<float> ldr(rgb.size());
+                rc = rtg_tonemap(device, rgb.data(), c.d.nx, c.d.ny, &c.tm, ldr.data());
+                if (rc) { g_err = rtg_last_error(); break; }
+                const size_t dot = name.rfind('.'), sl = name.rfind('/');
+                const std::string tname = (dot == std::string::npos || (sl != std::string::npos && dot < sl) ? name : name.substr(0, dot)) + ".png";
+                rc = rtgh_save_image(tname.c_str(), ldr.data(), c.d.nx, c.d.ny);
+                if (rc) break;
+            }
+            rtg_render_stats st{};
+            rtg_last_render_stats(gpu, &st);
+            printf("%s: %.1f ms, %.1f Mray/s\n", name.c_str(), st.render_ms, st.total_rays / (st.render_ms * 1e3));
         }
-        rtg_render_stats st{};
-        rtg_last_render_stats(gpu, &st);
-        printf("%s: %.1f ms, %.1f Mray/s\n", name.c_str(), st.render_ms, st.total_rays / (st.render_ms * 1e3));
-    }
-    rtg_scene_destroy(gpu);
-    rtgh_free(sc);
-    return rc;
+        rtg_scene_destroy(gpu);
+        rtgh_free(sc);
+        return rc;
+    });
 }
 
 }  // extern "C"

@@ -139,3 +139,26 @@ def test_scene_texture_exr_matches_native_parse(tmp_path):
     want = X.expected_rgba(ch, X.HALF)[..., :3]
     assert np.array_equal(np.asarray(t0.texels, np.float32).reshape(want.shape), want)
     assert np.array_equal(np.asarray(d["textures"][0]["texels"], np.float32).reshape(want.shape), want)
+
+
+@pytest.mark.parametrize("comp", [X.RLE, X.ZIP, X.PIZ])
+def test_corrupted_files_never_crash(tmp_path, comp):
+    """Random byte flips / truncations of valid files either decode or fail with RtgError."""
+    ch = _image(40, 23, seed=comp)
+    good = X.write_exr(str(tmp_path / "g.exr"), ch, comp, X.HALF)
+    rng = np.random.default_rng(comp)
+    p = str(tmp_path / "bad.exr")
+    for trial in range(150):
+        b = bytearray(good)
+        if trial % 5 == 4:
+            b = b[:int(rng.integers(8, len(b)))]
+        else:
+            for _ in range(int(rng.integers(1, 8))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+        with open(p, "wb") as fh:
+            fh.write(bytes(b))
+        try:
+            img = native.read_image(p)
+            assert img.ndim == 3 and img.shape[2] == 3
+        except RtgError:
+            pass
