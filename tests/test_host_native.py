@@ -211,3 +211,34 @@ def test_host_library_exports_every_declared_symbol():
     syms = set(re.findall(r"\sT\s(rtgh_\w+)", out.stdout))
     assert decl <= syms, decl - syms
     assert os.access(native.CLI_PATH, os.X_OK)
+
+
+def test_native_parser_survives_corrupted_files(tmp_path):
+    """Truncated / mutated scene files and PLYs parse or fail with an error, never crash
+    (scripts/xml_fuzz.cpp runs the same idea under ASan/UBSan)."""
+    rng = np.random.default_rng(7)
+    sc = scenegen.dragon1m(8, 6, spp=1, nu=20, nv=10)
+    good = open(write_xml(sc, str(tmp_path / "d.xml")), "rb").read()
+    ply = [p for p in os.listdir(tmp_path) if p.endswith(".ply")][0]
+    ply_good = (tmp_path / ply).read_bytes()
+    for t in range(120):
+        b = bytearray(good)
+        if t % 3 == 0:
+            b = b[:int(rng.integers(1, len(b)))]
+        else:
+            for _ in range(int(rng.integers(1, 6))):
+                b[int(rng.integers(0, len(b)))] = int(rng.choice(list(b'<>"-9 e/\0')))
+        if t % 4 == 3:                               # and a damaged mesh file
+            pb = bytearray(ply_good)
+            for _ in range(8):
+                pb[int(rng.integers(0, min(len(pb), 400)))] = int(rng.integers(0, 256))
+            (tmp_path / ply).write_bytes(bytes(pb[:int(rng.integers(1, len(pb)))]))
+        else:
+            (tmp_path / ply).write_bytes(ply_good)
+        x = tmp_path / "m.xml"
+        x.write_bytes(bytes(b))
+        try:
+            with native.NativeScene(str(x)) as ns:
+                assert ns.desc.num_objects >= 0
+        except A.RtgError:
+            pass
