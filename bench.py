@@ -115,7 +115,7 @@ def main():
 
     t0 = time.perf_counter()
     from rtg import scenegen
-    from rtg.shard import gather_frame, max_shard_rows, shard_opts
+    from rtg.shard import ROW_BLOCK, gather_frame, max_shard_rows, shard_opts
     make, spp_default, wl_text, data_text = WORKLOADS[args.workload]
     scene = getattr(scenegen, make)(args.width, args.height, spp=args.spp or spp_default)
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
@@ -201,7 +201,8 @@ def main():
                 "data": data_text,
                 "config": {"workload": wl_text,
                            "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
-                           "parallelism": f"8-row-block interleaved pixel shards x{world}" + (" + RCCL gather" if world > 1 else "")},
+                           "parallelism": (f"{ROW_BLOCK}-row-block interleaved pixel shards x{world} + RCCL gather"
+                                           if world > 1 else "single GPU")},
                 "rays_per_frame": rays // max(args.steps, 1),
                 "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
                 "kernel_ms_rank0_streams1": {"trace": round(st_roof["trace_ms"], 2),
