@@ -1986,29 +1986,47 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __
 }
 
 // Scene::MultiSample sum order: color += sample_i in sample order (src/Scene.cpp:519-540).
+// Scene::MultiSample / SingleSample (src/Scene.cpp:517-542): color += sample_s in sample order.
+// A block takes 64 pixels: their samples' colours are staged through LDS with coalesced loads
+// (the slots of a pixel are adjacent; one lane per slot), then one lane per pixel sums them in
+// order.  mode 2: the single sample itself; 1: first chunk (start from 0); 0: continue the
+// running sum in `acc`.
+constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
 __global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ level0, float* __restrict__ acc,
                                                     const PassDev ps, int nx, int mode) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= ps.npass) return;
-    int x, k;
-    tile_pixel(ps.p0 + j, nx, ps.rows_owned, ps.tile_h, x, k);
-    const size_t p = (size_t)k * nx + x;        // acc is in natural owned-row order
-    f3 a;
-    int s = 0;
-    if (mode == 2) {            // SingleSample: the colour itself
-        const NodeRec& r = level0[(size_t)j * ps.ns];
-        a = mk(r.cr, r.cg, r.cb);
-        s = 1;
-    } else if (mode == 1) {     // MultiSample: Vector3f color = {0,0,0}; color += ...
-        a = mk(0.0f, 0.0f, 0.0f);
-    } else {
-        a = mk(acc[3 * p], acc[3 * p + 1], acc[3 * p + 2]);
+    __shared__ float sr[kAccPix * kAccStride], sg[kAccPix * kAccStride], sb[kAccPix * kAccStride];
+    const int p0 = blockIdx.x * kAccPix;
+    const int np = min(kAccPix, ps.npass - p0);
+    const int t = threadIdx.x;
+    f3 a = mk(0.0f, 0.0f, 0.0f);
+    size_t p = 0;
+    if (t < np) {
+        int x, k;
+        tile_pixel(ps.p0 + p0 + t, nx, ps.rows_owned, ps.tile_h, x, k);
+        p = (size_t)k * nx + x;                 // acc is in natural owned-row order
+        if (mode == 0) a = mk(acc[3 * p], acc[3 * p + 1], acc[3 * p + 2]);
     }
-    for (; s < ps.ns; s++) {
-        const NodeRec& r = level0[(size_t)j * ps.ns + s];
-        a = a + mk(r.cr, r.cg, r.cb);
+    for (int s0 = 0; s0 < ps.ns; s0 += kAccChunk) {
+        const int cs = min(kAccChunk, ps.ns - s0);
+        __syncthreads();
+        for (int e = t; e < np * cs; e += blockDim.x) {
+            const int q = e / cs, s = e - q * cs;
+            const NodeRec& r = level0[(size_t)(p0 + q) * ps.ns + s0 + s];
+            sr[q * kAccStride + s] = r.cr;
+            sg[q * kAccStride + s] = r.cg;
+            sb[q * kAccStride + s] = r.cb;
+        }
+        __syncthreads();
+        if (t < np) {
+            int s = 0;
+            if (mode == 2 && s0 == 0) {         // SingleSample: the colour itself
+                a = mk(sr[t * kAccStride], sg[t * kAccStride], sb[t * kAccStride]);
+                s = 1;
+            }
+            for (; s < cs; s++) a = a + mk(sr[t * kAccStride + s], sg[t * kAccStride + s], sb[t * kAccStride + s]);
+        }
     }
-    acc[3 * p] = a.x; acc[3 * p + 1] = a.y; acc[3 * p + 2] = a.z;
+    if (t < np) { acc[3 * p] = a.x; acc[3 * p + 1] = a.y; acc[3 * p + 2] = a.z; }
 }
 
 __global__ void __launch_bounds__(256) k_finalize(const float* __restrict__ acc, float* __restrict__ out, int nx,
@@ -2120,7 +2138,7 @@ void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_no
 }
 void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st) {
     if (ps.npass <= 0) return;
-    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, 256)), dim3(256), 0, st, level0, acc, ps, nx, mode);
+    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, level0, acc, ps, nx, mode);
 }
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block,
                      int total, hipStream_t st) {
