@@ -1943,15 +1943,12 @@ __global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const Sha
 
 DEV f3 nan_check(f3 c) { return isnan3(c) ? mk(0, 0, 0) : c; }   // Scene::NanCheck :352-359
 
-// Bottom-up combination of RecursiveShading (src/Scene.cpp:279-350) for one level.
-__global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __restrict__ nodes,
-                                                 const NodeRec* __restrict__ child, int n) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    NodeRec nd = nodes[i];
-    int kind = nd.kind & 0xFF;
-    if (kind == NK_FINAL) return;
+// Bottom-up combination of RecursiveShading (src/Scene.cpp:279-350): the colour of one node
+// from its basic shading and its children's (already resolved) colours.
+DEV f3 resolve_node(const SceneView& sv, const NodeRec& nd, const NodeRec* __restrict__ child) {
+    const int kind = nd.kind & 0xFF;
     f3 basic = mk(nd.cr, nd.cg, nd.cb);
+    if (kind == NK_FINAL) return basic;
     f3 c0 = mk(0, 0, 0), c1 = mk(0, 0, 0), q0 = mk(0, 0, 0);
     if (nd.child0 >= 0) { const NodeRec& a = child[nd.child0]; c0 = mk(a.cr, a.cg, a.cb); q0 = mk(a.px, a.py, a.pz); }
     if (nd.child1 >= 0) { const NodeRec& b = child[nd.child1]; c1 = mk(b.cr, b.cg, b.cb); }
@@ -1982,6 +1979,17 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __
             res = nan_check(outside) + nan_check(refl);
         }
     }
+    return res;
+}
+
+// One level of the bottom-up pass (levels >= 1; level 0 is resolved inside k_accumulate).
+__global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __restrict__ nodes,
+                                                 const NodeRec* __restrict__ child, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if ((nodes[i].kind & 0xFF) == NK_FINAL) return;
+    const NodeRec nd = nodes[i];
+    const f3 res = resolve_node(sv, nd, child);
     nodes[i].cr = res.x; nodes[i].cg = res.y; nodes[i].cb = res.z;
 }
 
@@ -1992,8 +2000,9 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __
 // order.  mode 2: the single sample itself; 1: first chunk (start from 0); 0: continue the
 // running sum in `acc`.
 constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
-__global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ level0, float* __restrict__ acc,
-                                                    const PassDev ps, int nx, int mode) {
+__global__ void __launch_bounds__(256) k_accumulate(const SceneView sv, const NodeRec* __restrict__ level0,
+                                                    const NodeRec* __restrict__ level1, bool resolve,
+                                                    float* __restrict__ acc, const PassDev ps, int nx, int mode) {
     __shared__ float sr[kAccPix * kAccStride], sg[kAccPix * kAccStride], sb[kAccPix * kAccStride];
     const int p0 = blockIdx.x * kAccPix;
     const int np = min(kAccPix, ps.npass - p0);
@@ -2012,9 +2021,16 @@ __global__ void __launch_bounds__(256) k_accumulate(const NodeRec* __restrict__ 
         for (int e = t; e < np * cs; e += blockDim.x) {
             const int q = e / cs, s = e - q * cs;
             const NodeRec& r = level0[(size_t)(p0 + q) * ps.ns + s0 + s];
-            sr[q * kAccStride + s] = r.cr;
-            sg[q * kAccStride + s] = r.cg;
-            sb[q * kAccStride + s] = r.cb;
+            f3 c;
+            if (resolve && (r.kind & 0xFF) != NK_FINAL) {   // level 0 of the bottom-up pass
+                const NodeRec nd = r;
+                c = resolve_node(sv, nd, level1);
+            } else {
+                c = mk(r.cr, r.cg, r.cb);
+            }
+            sr[q * kAccStride + s] = c.x;
+            sg[q * kAccStride + s] = c.y;
+            sb[q * kAccStride + s] = c.z;
         }
         __syncthreads();
         if (t < np) {
@@ -2136,9 +2152,11 @@ void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_no
     if (n <= 0) return;
     hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, nodes, child_nodes, n);
 }
-void launch_accumulate(const NodeRec* level0, float* acc, const PassDev& ps, int nx, int mode, hipStream_t st) {
+void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
+                       const PassDev& ps, int nx, int mode, hipStream_t st) {
     if (ps.npass <= 0) return;
-    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, level0, acc, ps, nx, mode);
+    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, level0, level1, resolve, acc,
+                       ps, nx, mode);
 }
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block,
                      int total, hipStream_t st) {
