@@ -104,10 +104,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # RTG_BENCH_REHEARSE=1: rehearse the N>1 path on a 1-GPU box (every rank on cuda:0, gloo
+    # collectives through host memory); the numbers of such a run are not a scaling measurement
+    rehearse = os.environ.get("RTG_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
 
@@ -190,6 +198,15 @@ def main():
             "timing": "HIP events around each launch in a streams=1 frame outside the timed region",
             "roofline_frame_ms": round(st_roof["render_ms"], 2)}
 
+    if rehearse and rank == 0 and world > 1:
+        # the gathered frame must equal this rank's own single-device frame bit for bit
+        full = torch.zeros_like(frame)
+        r.render_device(0, full.data_ptr(), stream)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(full.view(torch.int32), frame.view(torch.int32)))
+        log(f"[rank 0] rehearsal: gathered frame == single-device frame: {same}")
+        if not same:
+            raise SystemExit("rehearsal: gathered frame differs from the single-device frame")
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
@@ -201,8 +218,9 @@ def main():
                 "data": data_text,
                 "config": {"workload": wl_text,
                            "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
-                           "parallelism": (f"{ROW_BLOCK}-row-block interleaved pixel shards x{world} + RCCL gather"
-                                           if world > 1 else "single GPU")},
+                           "parallelism": (f"{ROW_BLOCK}-row-block interleaved pixel shards x{world} + "
+                                           + ("gloo gather (rehearsal, all ranks on one GPU)" if rehearse
+                                              else "RCCL gather") if world > 1 else "single GPU")},
                 "rays_per_frame": rays // max(args.steps, 1),
                 "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
                 "kernel_ms_rank0_streams1": {"trace": round(st_roof["trace_ms"], 2),

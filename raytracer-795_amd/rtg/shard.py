@@ -44,11 +44,15 @@ def gather_frame(part, frame, rank: int, world: int, dist, block: int = ROW_BLOC
         rows = _row_index(ny, rank, world, block, frame.device)
         frame.index_copy_(0, rows, part[:len(rows)])
         return frame
-    key = (id(part), world)
+    staged = part.is_cuda and dist.get_backend() == "gloo"   # gloo gathers host tensors only
+    src = part.cpu() if staged else part
+    key = (id(part), world, staged)
     if rank == dst and _GATHER_BUFS.get("key") != key:
-        _GATHER_BUFS.update(key=key, bufs=[torch.empty_like(part) for _ in range(world)])
+        _GATHER_BUFS.update(key=key, bufs=[torch.empty_like(src) for _ in range(world)])
     parts = _GATHER_BUFS["bufs"] if rank == dst else None
-    dist.gather(part, parts, dst=dst)
+    dist.gather(src, parts, dst=dst)
+    if staged and rank == dst:
+        parts = [q.to(frame.device) for q in parts]
     if rank == dst:
         for r in range(world):
             rows = _row_index(ny, r, world, block, frame.device)
