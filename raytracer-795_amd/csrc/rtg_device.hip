@@ -1286,11 +1286,11 @@ DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassDev ps, uint64_t seed,
-                                                RayRec* __restrict__ rays, RayMeta* __restrict__ meta, int n,
-                                                int max_depth) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// Primary ray of sample slot i of the pass.  k_raygen stores it; the Whitted path's level-0
+// k_trace / k_shade recompute it from the slot instead (same function, so bit-identical),
+// which saves the 48-byte RayRec + RayMeta store and its two re-reads per primary ray.
+DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int i, f3& o_out, f3& d_out,
+                     float& time_out) {
     uint32_t pixel, sample;
     int x, y;
     slot_pixel(cam, ps, i, pixel, sample, x, y);
@@ -1335,6 +1335,17 @@ __global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassD
         f3 dv = m - pos;
         d = dv / norm(dv);
     }
+    o_out = o; d_out = d; time_out = time;
+}
+
+__global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassDev ps, uint64_t seed,
+                                                RayRec* __restrict__ rays, RayMeta* __restrict__ meta, int n,
+                                                int max_depth) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    f3 o, d;
+    float time;
+    primary_ray(cam, ps, seed, i, o, d, time);
     RayRec r;
     r.o_t = make_float4(o.x, o.y, o.z, time);
     r.d = make_float4(d.x, d.y, d.z, FLT_MAX);
@@ -1344,19 +1355,29 @@ __global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassD
     meta[i] = mt;
 }
 
-template <bool EXHAUSTIVE, bool STATS>
+// GEN: level-0 launch of the Whitted path, the ray is primary_ray(slot i) (no RayRec buffer).
+template <bool EXHAUSTIVE, bool STATS, bool GEN = false>
 __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayRec* __restrict__ rays,
-                                                       HitRec* __restrict__ hits, int n, Counters* ctr) {
+                                                       HitRec* __restrict__ hits, int n, Counters* ctr,
+                                                       const CameraDev cam, const PassDev ps, uint64_t seed) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
     __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     Stats st = {0, 0, 0, 0};
     if (i < n) {
-        RayRec r = rays[i];
-        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, mk(r.o_t.x, r.o_t.y, r.o_t.z), mk(r.d.x, r.d.y, r.d.z), r.o_t.w,
-                                                  r.d.w, s_stack + threadIdx.x, kTraceBlock, s_wnode[threadIdx.x >> 6],
-                                                  s_wmask[threadIdx.x >> 6], st);
+        f3 o, d;
+        float time, tmax;
+        if (GEN) {
+            primary_ray(cam, ps, seed, i, o, d, time);
+            tmax = FLT_MAX;
+        } else {
+            RayRec r = rays[i];
+            o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
+            time = r.o_t.w; tmax = r.d.w;
+        }
+        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock,
+                                                  s_wnode[threadIdx.x >> 6], s_wmask[threadIdx.x >> 6], st);
         hits[i] = h;
     }
     if (STATS) {
@@ -1434,11 +1455,19 @@ __global__ void __launch_bounds__(BLOCK) k_shade(const SceneView sv, const Camer
     NodeRec nd;
     unsigned long long smask = 0;   // lights whose shadow query must be traced
     if (i < n) {
-        RayRec r = rays[i];
-        RayMeta mt = meta[i];
         HitRec h = hits[i];
-        f3 o = mk(r.o_t.x, r.o_t.y, r.o_t.z), d = mk(r.d.x, r.d.y, r.d.z);
-        float time = r.o_t.w;
+        f3 o, d;
+        float time;
+        RayMeta mt;
+        if (rays == nullptr) {          // level 0 without a ray buffer: regenerate (k_raygen's record)
+            primary_ray(cam, ps, seed, i, o, d, time);
+            mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
+        } else {
+            RayRec r = rays[i];
+            mt = meta[i];
+            o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
+            time = r.o_t.w;
+        }
         uint32_t pixel, sample;
         int x, y;
         slot_pixel(cam, ps, mt.slot, pixel, sample, x, y);
@@ -2093,12 +2122,20 @@ void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps,
     hipLaunchKernelGGL(k_raygen, dim3(nblk(n, 256)), dim3(256), 0, st, cam, ps, seed, rays, meta, n, sv.max_depth);
 }
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
-                  hipStream_t st) {
+                  hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed) {
     if (n <= 0) return;
     dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
-    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false>), g, b, 0, st, sv, rays, hits, n, ctr);
-    else if (ctr) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, st, sv, rays, hits, n, ctr);
-    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, st, sv, rays, hits, n, ctr);
+    const CameraDev cam = gen_cam ? *gen_cam : CameraDev{};
+    const PassDev ps = gen_ps ? *gen_ps : PassDev{};
+    if (gen_cam) {   // primary rays generated in the kernel (rays unused)
+        if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
+        else if (ctr) hipLaunchKernelGGL((k_trace<false, true, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
+        else hipLaunchKernelGGL((k_trace<false, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
+        return;
+    }
+    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
+    else if (ctr) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
+    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
 }
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
