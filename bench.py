@@ -190,9 +190,9 @@ def main():
     bytes_per_launch = bytes_per_ray * trace_rays / max(trace_launches, 1)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("rtg::k_trace<false, false>") if args.workload == "dragon1m" else None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("rtg::k_trace<false, false, *>") if args.workload == "dragon1m" else None,
             "traffic_unit": "bytes/launch (PMC, profiles/traffic_current.json)",
-            "kernel": "k_trace<false,false> (closest hit, primary+secondary)",
+            "kernel": "k_trace<false,false,*> (closest hit: GEN=true generates the primary rays at level 0, GEN=false traces secondary levels)",
             "avg_launch_ms": round(avg_launch_ms, 3), "launches": trace_launches,
             "bytes_per_ray": round(bytes_per_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),
             "timing": "HIP events around each launch in a streams=1 frame outside the timed region",

@@ -1230,6 +1230,12 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         break;
     }
     }
+    // A query whose unshadowed contribution is exactly +0 in every channel (a light behind
+    // the surface with no specular lobe left) need not be traced: blocked, the light adds the
+    // reference's Vector3f(0,0,0) (src/Light.cpp:188-205, 447-459), unblocked it adds c = +0;
+    // both leave the running sum bit-identical.  -0 / NaN channels keep the query.
+    if ((mode == 1.0f || mode == 2.0f) && (__float_as_uint(c.x) | __float_as_uint(c.y) | __float_as_uint(c.z)) == 0u)
+        mode = 0.0f;
     if (mode == 1.0f || mode == 3.0f) {
         // hits with gett() beyond |p-L| + eps can never satisfy the blocking test
         float dl = norm(ret.point - lp);

@@ -39,6 +39,17 @@ def main():
         res[k] = {"launches_fetch_pass": nf, "launches_write_pass": nw,
                   "fetch_kb_raw_per_launch": round(fkb, 1), "write_kb_per_launch": round(wkb, 1),
                   "hbm_bytes_per_launch": round(2 * fkb * 1024 + wkb * 1024)}
+    # the closest-hit kernel has two instantiations on the bench path (GEN=true: level 0 of the
+    # Whitted path generating its primary rays; GEN=false: secondary levels): a launch-weighted
+    # combined entry is what bench.py's roofline (HIP events over all its launches) compares to
+    parts = [k for k in res if k.startswith("rtg::k_trace<false, false")]
+    if parts:
+        nl = sum(res[k]["launches_fetch_pass"] for k in parts)
+        if nl:
+            res["rtg::k_trace<false, false, *>"] = {
+                "launches_fetch_pass": nl, "parts": parts,
+                "hbm_bytes_per_launch": round(sum(res[k]["hbm_bytes_per_launch"] * res[k]["launches_fetch_pass"]
+                                                  for k in parts) / nl)}
     json.dump({"kernels": res, "command": cmd,
                "note": "hbm_bytes_per_launch = 2 x FETCH_SIZE(KB) x 1024 + WRITE_SIZE(KB) x 1024 "
                        "(gfx950 FETCH_SIZE half-count correction); averaged over the dispatches of the pass"},

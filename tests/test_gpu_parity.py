@@ -153,7 +153,9 @@ def test_sample_chunks_accumulate_in_order(gpu):
 
 
 def test_ray_counts_match_oracle(gpu):
-    """Point-light scenes: the GPU traces exactly the rays the reference loop traces."""
+    """Point-light scenes: the GPU traces exactly the primary / secondary rays of the reference
+    loop, and its shadow queries minus those whose light contributes exactly +0 (skipped: blocked
+    or not, they add the same +0, rtg_device.hip light_sample)."""
     sc = scenegen.bunny5k(48, 36, level=3)
     with rtg.Renderer(sc, device=gpu) as r:
         r.render(0)
@@ -161,7 +163,8 @@ def test_ray_counts_match_oracle(gpu):
     o = pyoracle.Oracle(sc)
     o.render(0)
     c = o.ray_counts()
-    assert (st["primary_rays"], st["secondary_rays"], st["shadow_rays"]) == (c["primary"], c["secondary"], c["shadow"])
+    assert (st["primary_rays"], st["secondary_rays"]) == (c["primary"], c["secondary"])
+    assert 0 < st["shadow_rays"] <= c["shadow"]
 
 
 def test_render_device_into_torch_tensor(gpu):
