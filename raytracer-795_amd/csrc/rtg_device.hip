@@ -1566,7 +1566,9 @@ __global__ void __launch_bounds__(BLOCK) k_shade(const SceneView sv, const Camer
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
                         light_sample<FULL, SPOT>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
-                        shadows[(size_t)i * sv.num_lights + li] = sr;
+                        // one light: a query that is not traced is never read (k_light_sum reads
+                        // every record when there are several)
+                        if (sr.c.w != 0.0f || sv.num_lights > 1) shadows[(size_t)i * sv.num_lights + li] = sr;
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
                     }
