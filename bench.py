@@ -152,6 +152,9 @@ def main():
     # roofline frame (outside the timed region): passes one at a time (streams=1) so every
     # closest-hit launch is timed alone by its HIP events; the timed frames below overlap
     # passes on several streams, where an event pair would also count the other streams' work
+    # (twice: the first streams=1 frame also grows that lane's level buffers — hipMalloc of
+    # fresh memory — so only the second one's frame time is representative)
+    step(collect_timing=1, streams=1)
     st_roof = step(collect_timing=1, streams=1)
     for _ in range(args.warmup):
         step()

@@ -26,6 +26,9 @@ namespace rtg {
 #ifndef RTG_SHADOW_ATTR  // 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
+#ifndef RTG_SHADE_ATTR   // occupancy experiments on k_shade (Whitted, non-full variants)
+#define RTG_SHADE_ATTR
+#endif
 #ifndef RTG_PACKET        // 1: wave-packet walk of the 4-wide tree (scalar node loads, one stack per wave)
 #define RTG_PACKET 0
 #endif
@@ -1446,7 +1449,7 @@ DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialD
 }
 
 template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock>
-__global__ void __launch_bounds__(BLOCK) k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+__global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                uint64_t seed,
                                                const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
                                                const HitRec* __restrict__ hits, NodeRec* __restrict__ nodes,
