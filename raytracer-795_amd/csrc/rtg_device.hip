@@ -1452,7 +1452,7 @@ template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock>
 __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                uint64_t seed,
                                                const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
-                                               const HitRec* __restrict__ hits, NodeRec* __restrict__ nodes,
+                                               const HitRec* __restrict__ hits, const NodePlanes nodes,
                                                ShadowRec* __restrict__ shadows, int* __restrict__ slist,
                                                RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
                                                unsigned long long* qcount, int n) {
@@ -1461,6 +1461,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     RayRec c0r, c1r;
     RayMeta c0m, c1m;
     bool has0 = false, has1 = false;
+    bool hit = false;
     NodeRec nd;
     unsigned long long smask = 0;   // lights whose shadow query must be traced
     if (i < n) {
@@ -1497,6 +1498,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                 nd.cr = bg.x; nd.cg = bg.y; nd.cb = bg.z;
             }
         } else {
+            hit = true;
             Ret ret = hit_record<FULL>(sv, o, d, time, h);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
@@ -1610,7 +1612,9 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     if (i < n) {
         if (has0) { next_rays[idx] = c0r; next_meta[idx] = c0m; nd.child0 = idx; idx++; }
         if (has1) { next_rays[idx] = c1r; next_meta[idx] = c1m; nd.child1 = idx; }
-        nodes[i] = nd;
+        nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind | (hit ? kNodeHit : 0)));
+        if (hit) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
+        if ((nd.kind & 0xFF) != NK_FINAL) nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, 0);
     }
     unsigned sb = (unsigned)(s_base >> 32) + s_ws[w];
     for (int li = 0; li < sv.num_lights; li++) {
@@ -1867,8 +1871,11 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        ShadowRec* __restrict__ shadows,
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount,
-                                                                       NodeRec* __restrict__ nodes,
+                                                                       float* __restrict__ ncol,
+                                                                       const float* __restrict__ npnt, int nstride,
                                                                        unsigned* nan_queries, Counters* ctr) {
+    // node i's colour at ncol + i * nstride, its hit point at npnt + i * nstride (NodePlanes:
+    // stride 4 floats; the path tracer's NodeRec array: stride 12)
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
     __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
@@ -1889,7 +1896,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         if (!EXHAUSTIVE && RTG_SHADOW_ANY) {
             const ShadowRec sr = shadows[idx];
             const int i = idx / sv.num_lights;
-            const f3 p = mk(nodes[i].px, nodes[i].py, nodes[i].pz);
+            const float* pp = npnt + (size_t)i * nstride;
+            const f3 p = mk(pp[0], pp[1], pp[2]);
             const f3 lp = mk(sr.L.x, sr.L.y, sr.L.z);
             if (sr.c.w == 1.0f) {
                 const float DL = norm(p - lp);
@@ -1923,7 +1931,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
                 const f3 o_ = mk(ld(q + 0), ld(q + 1), ld(q + 2)), d_ = mk(ld(q + 4), ld(q + 5), ld(q + 6));
                 const f3 l_ = mk(ld(q + 12), ld(q + 13), ld(q + 14));
-                const f3 p_ = mk(ld(&nodes[i].px), ld(&nodes[i].py), ld(&nodes[i].pz));
+                const float* pp = npnt + (size_t)i * nstride;
+                const f3 p_ = mk(ld(pp), ld(pp + 1), ld(pp + 2));
                 f3 hp = o_ + d_ * h.t;
                 if (sc.w == 1.0f) {
                     blocked = norm(p_ - l_) > norm(p_ - hp);
@@ -1937,9 +1946,10 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         }
         if (sv.num_lights == 1) {
             f3 add = blocked ? mk(0, 0, 0) : mk(sc.x, sc.y, sc.z);
-            nodes[i].cr = nodes[i].cr + add.x;
-            nodes[i].cg = nodes[i].cg + add.y;
-            nodes[i].cb = nodes[i].cb + add.z;
+            float* cp = ncol + (size_t)i * nstride;
+            cp[0] = cp[0] + add.x;
+            cp[1] = cp[1] + add.y;
+            cp[2] = cp[2] + add.z;
         } else {
             shadows[idx].L.w = blocked ? 0.0f : 1.0f;
         }
@@ -1967,33 +1977,42 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
 
 // Several lights: Scene::RecursiveShading's in-order sum col = ((amb + L0) + L1) + ...
 __global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const ShadowRec* __restrict__ shadows,
-                                                   NodeRec* __restrict__ nodes, int n) {
+                                                   const NodePlanes nodes, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const NodeRec nd = nodes[i];
-    if (!(nd.kind & 0x100)) return;
-    f3 col = mk(nd.cr, nd.cg, nd.cb);
+    const float4 nc = nodes.col[i];
+    if (!(__float_as_int(nc.w) & 0x100)) return;
+    f3 col = mk(nc.x, nc.y, nc.z);
     for (int li = 0; li < sv.num_lights; li++) {
         const ShadowRec sr = shadows[(size_t)i * sv.num_lights + li];
         const bool lit = sr.c.w != 0.0f && sr.L.w == 1.0f;
         col = col + (lit ? mk(sr.c.x, sr.c.y, sr.c.z) : mk(0, 0, 0));
     }
-    nodes[i].cr = col.x; nodes[i].cg = col.y; nodes[i].cb = col.z;
+    nodes.col[i] = make_float4(col.x, col.y, col.z, nc.w);
 }
 
 DEV f3 nan_check(f3 c) { return isnan3(c) ? mk(0, 0, 0) : c; }   // Scene::NanCheck :352-359
 
 // Bottom-up combination of RecursiveShading (src/Scene.cpp:279-350): the colour of one node
 // from its basic shading and its children's (already resolved) colours.
-DEV f3 resolve_node(const SceneView& sv, const NodeRec& nd, const NodeRec* __restrict__ child) {
-    const int kind = nd.kind & 0xFF;
-    f3 basic = mk(nd.cr, nd.cg, nd.cb);
+// Node i of `self` (colour record nc) against its children in `child`.  A missed refracted
+// child's point is (0,0,0) (src/Helper.cpp:75): the child's point plane is read only for hits.
+DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& self, const NodePlanes& child) {
+    const int kind = __float_as_int(nc.w) & 0xFF;
+    f3 basic = mk(nc.x, nc.y, nc.z);
     if (kind == NK_FINAL) return basic;
+    const int4 lk = self.link[i];
+    const float4 pf = self.pnt[i];
     f3 c0 = mk(0, 0, 0), c1 = mk(0, 0, 0), q0 = mk(0, 0, 0);
-    if (nd.child0 >= 0) { const NodeRec& a = child[nd.child0]; c0 = mk(a.cr, a.cg, a.cb); q0 = mk(a.px, a.py, a.pz); }
-    if (nd.child1 >= 0) { const NodeRec& b = child[nd.child1]; c1 = mk(b.cr, b.cg, b.cb); }
-    const MaterialDev& m = sv.materials[nd.material - 1];
-    f3 p = mk(nd.px, nd.py, nd.pz);
+    if (lk.x >= 0) {
+        const float4 a = child.col[lk.x];
+        c0 = mk(a.x, a.y, a.z);
+        if (__float_as_int(a.w) & kNodeHit) { const float4 ap = child.pnt[lk.x]; q0 = mk(ap.x, ap.y, ap.z); }
+    }
+    if (lk.y >= 0) { const float4 b = child.col[lk.y]; c1 = mk(b.x, b.y, b.z); }
+    const struct { float F; } nd = {pf.w};
+    const MaterialDev& m = sv.materials[lk.z - 1];
+    f3 p = mk(pf.x, pf.y, pf.z);
     f3 res;
     if (kind == NK_MIRROR) {
         res = basic + cw(ld3(m.mirror), c1);
@@ -2023,14 +2042,14 @@ DEV f3 resolve_node(const SceneView& sv, const NodeRec& nd, const NodeRec* __res
 }
 
 // One level of the bottom-up pass (levels >= 1; level 0 is resolved inside k_accumulate).
-__global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __restrict__ nodes,
-                                                 const NodeRec* __restrict__ child, int n) {
+__global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodePlanes nodes, const NodePlanes child,
+                                                 int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if ((nodes[i].kind & 0xFF) == NK_FINAL) return;
-    const NodeRec nd = nodes[i];
-    const f3 res = resolve_node(sv, nd, child);
-    nodes[i].cr = res.x; nodes[i].cg = res.y; nodes[i].cb = res.z;
+    const float4 nc = nodes.col[i];
+    if ((__float_as_int(nc.w) & 0xFF) == NK_FINAL) return;
+    const f3 res = resolve_node(sv, nc, i, nodes, child);
+    nodes.col[i] = make_float4(res.x, res.y, res.z, nc.w);
 }
 
 // Scene::MultiSample sum order: color += sample_i in sample order (src/Scene.cpp:519-540).
@@ -2040,8 +2059,11 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, NodeRec* __
 // order.  mode 2: the single sample itself; 1: first chunk (start from 0); 0: continue the
 // running sum in `acc`.
 constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
-__global__ void __launch_bounds__(256) k_accumulate(const SceneView sv, const NodeRec* __restrict__ level0,
-                                                    const NodeRec* __restrict__ level1, bool resolve,
+// Colours are read at ncol + slot * nstride (the NodePlanes colour plane: stride 4; the path
+// tracer's NodeRec array: stride 12); `resolve` (Whitted only) evaluates non-final level-0 nodes
+// against level 1 first.
+__global__ void __launch_bounds__(256) k_accumulate(const SceneView sv, const float* __restrict__ ncol, int nstride,
+                                                    const NodePlanes level0, const NodePlanes level1, bool resolve,
                                                     float* __restrict__ acc, const PassDev ps, int nx, int mode) {
     __shared__ float sr[kAccPix * kAccStride], sg[kAccPix * kAccStride], sb[kAccPix * kAccStride];
     const int p0 = blockIdx.x * kAccPix;
@@ -2060,13 +2082,17 @@ __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv, const No
         __syncthreads();
         for (int e = t; e < np * cs; e += blockDim.x) {
             const int q = e / cs, s = e - q * cs;
-            const NodeRec& r = level0[(size_t)(p0 + q) * ps.ns + s0 + s];
+            const size_t slot = (size_t)(p0 + q) * ps.ns + s0 + s;
             f3 c;
-            if (resolve && (r.kind & 0xFF) != NK_FINAL) {   // level 0 of the bottom-up pass
-                const NodeRec nd = r;
-                c = resolve_node(sv, nd, level1);
+            if (nstride == 4) {
+                const float4 nc = level0.col[slot];
+                if (resolve && (__float_as_int(nc.w) & 0xFF) != NK_FINAL)   // level 0 of the bottom-up pass
+                    c = resolve_node(sv, nc, (int)slot, level0, level1);
+                else
+                    c = mk(nc.x, nc.y, nc.z);
             } else {
-                c = mk(r.cr, r.cg, r.cb);
+                const float* cp = ncol + slot * nstride;
+                c = mk(cp[0], cp[1], cp[2]);
             }
             sr[q * kAccStride + s] = c.x;
             sg[q * kAccStride + s] = c.y;
@@ -2154,26 +2180,31 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
                   unsigned long long* qcount, int n, hipStream_t st) {
     if (n <= 0) return;
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
+    const NodePlanes np = node_planes(nodes, n);
     if (sv.full)
-        hipLaunchKernelGGL((k_shade<true, true>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta, hits, nodes, shadows,
+        hipLaunchKernelGGL((k_shade<true, true>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, shadows,
                            slist, next_rays, next_meta, qcount, n);
     else if (sv.spot)
-        hipLaunchKernelGGL((k_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, nodes,
+        hipLaunchKernelGGL((k_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np,
                            shadows, slist, next_rays, next_meta, qcount, n);
     else
-        hipLaunchKernelGGL((k_shade<false, false>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, nodes,
+        hipLaunchKernelGGL((k_shade<false, false>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np,
                            shadows, slist, next_rays, next_meta, qcount, n);
 }
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool light_sum) {
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted) {
     if (n <= 0 || sv.num_lights == 0) return;
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, nodes, nan_queries, ctr);
-    if (sv.num_lights > 1 && light_sum)
-        hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, shadows, nodes, n);
+    const NodePlanes np = node_planes(nodes, n);
+    float* ncol = whitted ? reinterpret_cast<float*>(np.col) : &nodes[0].cr;
+    const float* npnt = whitted ? reinterpret_cast<const float*>(np.pnt) : &nodes[0].px;
+    const int ns = whitted ? 4 : (int)(sizeof(NodeRec) / sizeof(float));
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, slist, scount, ncol, npnt, ns, nan_queries, ctr);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, slist, scount, ncol, npnt, ns, nan_queries, ctr);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, ncol, npnt, ns, nan_queries, ctr);
+    if (sv.num_lights > 1 && whitted)
+        hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, shadows, np, n);
 }
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
@@ -2196,15 +2227,21 @@ void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRe
     if (n <= 0) return;
     hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, nodes, paths, shadows, nL, level0, level, n);
 }
-void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st) {
+void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child, hipStream_t st) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, nodes, child_nodes, n);
+    hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, node_planes(nodes, n),
+                       node_planes(const_cast<NodeRec*>(child_nodes), n_child), n);
 }
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
-                       const PassDev& ps, int nx, int mode, hipStream_t st) {
+                       const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1) {
     if (ps.npass <= 0) return;
-    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, level0, level1, resolve, acc,
-                       ps, nx, mode);
+    NodeRec* l0 = const_cast<NodeRec*>(level0);
+    const NodePlanes p0 = whitted ? node_planes(l0, n0) : NodePlanes{};
+    const NodePlanes p1 = (whitted && level1) ? node_planes(const_cast<NodeRec*>(level1), n1) : NodePlanes{};
+    const float* ncol = whitted ? reinterpret_cast<const float*>(p0.col) : &l0[0].cr;
+    const int ns = whitted ? 4 : (int)(sizeof(NodeRec) / sizeof(float));
+    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, ncol, ns, p0, p1,
+                       resolve && whitted, acc, ps, nx, mode);
 }
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block,
                      int total, hipStream_t st) {

@@ -1209,11 +1209,12 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         // bottom-up: levels level-1 .. 1 here, level 0 inside the accumulation
         for (int l = level - 1; l >= 1 && !pt; l--)
             launch_resolve(sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(), ln.counts[l],
+                           ln.counts[l + 1],
                            ln.st);
         const int mode = (total == 1) ? 2 : (ps.s0 == 0 ? 1 : 0);
         const NodeRec* level1 = level >= 1 ? ln.levels[1].nodes.as<NodeRec>() : nullptr;
         launch_accumulate(sv, ln.levels[0].nodes.as<NodeRec>(), level1, !pt && level >= 1, s->d_acc.as<float>(), ps,
-                          cam->nx, mode, ln.st);
+                          cam->nx, mode, ln.st, !pt, ln.counts[0], level >= 1 ? ln.counts[1] : 0);
         stt.passes++;
         ln.busy = false;
     };

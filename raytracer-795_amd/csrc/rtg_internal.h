@@ -227,6 +227,21 @@ struct NodeRec {        // 48 B, one per traced ray
     int slot;
 };
 
+// Whitted path: a level's n node records as three planes in the same 48 n bytes (structure of
+// arrays), so the kernels that only need a node's colour (accumulate, light sums, final nodes in
+// resolve) read 16 B of it, and k_shade stores the point only for hits and the links only for
+// non-final nodes.  The path tracer keeps the NodeRec array (k_pt_shade / k_pt_gather).
+struct NodePlanes {
+    float4* col;    // cr, cg, cb, kind (int bits; kNodeHit set for hits)
+    float4* pnt;    // px, py, pz, F               (hit nodes only)
+    int4* link;     // child0, child1, material, -  (kind != NK_FINAL only)
+};
+constexpr int kNodeHit = 0x400;
+inline NodePlanes node_planes(NodeRec* base, long long n) {
+    float4* b = reinterpret_cast<float4*>(base);
+    return NodePlanes{b, b + n, reinterpret_cast<int4*>(b + 2 * n)};
+}
+
 struct ShadowRec {      // 64 B, nLights per shading node
     float4 o;           // origin.xyz, time
     float4 d;           // direction.xyz, tmax (world t bound; +inf for directional/env)
@@ -252,17 +267,18 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
                   ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta,
                   unsigned long long* qcount, int n, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool light_sum = true);
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted = true);
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st);
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
                       int level, int n, hipStream_t st);
-void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, hipStream_t st);
+void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
+// whitted: level0 / level1 hold NodePlanes over n0 / n1 nodes (else NodeRec arrays, path tracer)
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
-                       const PassDev& ps, int nx, int mode, hipStream_t st);
+                       const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1);
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block, int total,
                      hipStream_t st);
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,
