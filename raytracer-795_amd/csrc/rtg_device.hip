@@ -1097,6 +1097,21 @@ DEV f3 env_radiance(const SceneView& sv, const LightDev& L, f3 dir) {   // Light
 }
 
 // Unshadowed contribution of light li plus the shadow query it needs.
+// Shadow-ray direction toward a light point and the query's t bound: shared by light_sample
+// and the lean k_shadow, which rebuilds them from the stored origin / hit point (bit-identical).
+DEV f3 toward(f3 lpos, f3 p) {
+    f3 dv = lpos - p;
+    return dv / norm(dv);
+}
+DEV float shadow_tmax(f3 origin, f3 p, f3 lp, float eps) {
+    // hits with gett() beyond |p-L| + eps can never satisfy the blocking test
+    float dl = norm(p - lp);
+    float oabs = fmaxf(fmaxf(fabsf(origin.x), fabsf(origin.y)), fabsf(origin.z));
+    float tmax = (dl + eps) * (1.0f + 1e-4f) + 1e-5f * oabs + 1e-30f;
+    if (!(tmax == tmax)) tmax = FLT_MAX;
+    return tmax;
+}
+
 template <bool FULL = true, bool SPOT = true, bool BRDF = FULL>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
                       uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
@@ -1109,8 +1124,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     switch (L.type) {
     case RTG_LIGHT_POINT: {                                     // PointLight::BasicShading :376-388
         f3 pos = ld3(L.pos);
-        f3 dv = pos - ret.point;
-        dir = dv / norm(dv);
+        dir = toward(pos, ret.point);
         lp = pos;
         mode = 1.0f;
         float dist = norm(ret.point - pos);
@@ -1126,8 +1140,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     }
     case RTG_LIGHT_SPOT: if constexpr (FULL || SPOT) {          // :547-574
         f3 pos = ld3(L.pos);
-        f3 dv = pos - ret.point;
-        dir = dv / norm(dv);
+        dir = toward(pos, ret.point);
         lp = pos;
         f3 dtp = normalized(ret.point - pos);
         float angle = f_acos(dot(dtp, ld3(L.dir)));
@@ -1239,13 +1252,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     // both leave the running sum bit-identical.  -0 / NaN channels keep the query.
     if ((mode == 1.0f || mode == 2.0f) && (__float_as_uint(c.x) | __float_as_uint(c.y) | __float_as_uint(c.z)) == 0u)
         mode = 0.0f;
-    if (mode == 1.0f || mode == 3.0f) {
-        // hits with gett() beyond |p-L| + eps can never satisfy the blocking test
-        float dl = norm(ret.point - lp);
-        float oabs = fmaxf(fmaxf(fabsf(origin.x), fabsf(origin.y)), fabsf(origin.z));
-        tmax = (dl + sv.shadow_eps) * (1.0f + 1e-4f) + 1e-5f * oabs + 1e-30f;
-        if (!(tmax == tmax)) tmax = FLT_MAX;
-    }
+    if (mode == 1.0f || mode == 3.0f) tmax = shadow_tmax(origin, ret.point, lp, sv.shadow_eps);
     sr.o = make_float4(origin.x, origin.y, origin.z, time);
     sr.d = make_float4(dir.x, dir.y, dir.z, tmax);
     sr.c = make_float4(c.x, c.y, c.z, mode);
@@ -1453,7 +1460,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                                                uint64_t seed,
                                                const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
                                                const HitRec* __restrict__ hits, const NodePlanes nodes,
-                                               ShadowRec* __restrict__ shadows, int* __restrict__ slist,
+                                               const ShadowPlanes shadows, int* __restrict__ slist,
                                                RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
                                                unsigned long long* qcount, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1573,7 +1580,12 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                         light_sample<FULL, SPOT>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         // one light: a query that is not traced is never read (k_light_sum reads
                         // every record when there are several)
-                        if (sr.c.w != 0.0f || sv.num_lights > 1) shadows[(size_t)i * sv.num_lights + li] = sr;
+                        if (sr.c.w != 0.0f || sv.num_lights > 1) {
+                            const size_t k = (size_t)i * sv.num_lights + li;
+                            shadows.o[k] = sr.o;
+                            shadows.c[k] = sr.c;
+                            if (!sv.lean_shadow) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
+                        }
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
                     }
@@ -1666,7 +1678,7 @@ __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const Came
                                                   uint64_t seed, const RayRec* __restrict__ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
                                                   PathRec* __restrict__ paths, NodeRec* __restrict__ nodes,
-                                                  ShadowRec* __restrict__ shadows, int* __restrict__ slist,
+                                                  const ShadowPlanes shadows, int* __restrict__ slist,
                                                   RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
                                                   PathRec* __restrict__ next_paths, unsigned long long* qcount, int n) {
     constexpr int BLOCK = 256;
@@ -1742,7 +1754,8 @@ __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const Came
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
                         light_sample<FULL, SPOT, BRDF>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
-                        shadows[(size_t)i * sv.num_lights + li] = sr;
+                        const size_t k = (size_t)i * sv.num_lights + li;
+                        shadows.o[k] = sr.o; shadows.d[k] = sr.d; shadows.c[k] = sr.c; shadows.L[k] = sr.L;
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
                     }
@@ -1837,7 +1850,7 @@ __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const Came
 // the oracle's per-sample summation order).  Level 0 starts the sum: L = (0,0,0) [+ T (x) v].
 // With several lights the in-order light sum of k_light_sum is folded in here.
 __global__ void __launch_bounds__(256) k_pt_gather(const NodeRec* __restrict__ nodes, const PathRec* __restrict__ paths,
-                                                   const ShadowRec* __restrict__ shadows, int nL,
+                                                   const ShadowPlanes shadows, int nL,
                                                    NodeRec* __restrict__ level0, int level, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1846,8 +1859,8 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodeRec* __restrict__ n
     f3 v = mk(nd.cr, nd.cg, nd.cb);
     if (nL > 1 && (nd.kind & 0x100)) {          // Scene::RecursiveShading's col = ((amb + L0) + L1) + ...
         for (int li = 0; li < nL; li++) {
-            const float4 sc = shadows[(size_t)i * nL + li].c;
-            const float lit = shadows[(size_t)i * nL + li].L.w;
+            const float4 sc = shadows.c[(size_t)i * nL + li];
+            const float lit = shadows.L[(size_t)i * nL + li].w;
             v = v + ((sc.w != 0.0f && lit == 1.0f) ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));
         }
     }
@@ -1868,7 +1881,7 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodeRec* __restrict__ n
 // does); with several, the visibility is recorded and k_light_sum adds them in light order.
 template <bool EXHAUSTIVE, bool STATS>
 __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const SceneView sv,
-                                                                       ShadowRec* __restrict__ shadows,
+                                                                       const ShadowPlanes shadows, bool lean,
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount,
                                                                        float* __restrict__ ncol,
@@ -1884,8 +1897,26 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     Stats st = {0, 0, 0, 0};
     if (j < (int)*scount) {
         const int idx = slist[j];
-        const float4 so = shadows[idx].o, sd = shadows[idx].d;
-        const f3 o = mk(so.x, so.y, so.z), d = mk(sd.x, sd.y, sd.z);
+        const float4 so = shadows.o[idx];
+        const f3 o = mk(so.x, so.y, so.z);
+        f3 d;
+        float tmax;
+        if (lean) {     // one point / spot / directional light (node idx, light 0): rebuild d, tmax
+            const LightDev& L = sv.lights[0];
+            if (L.type == RTG_LIGHT_DIRECTIONAL) {
+                d = -ld3(L.dir);
+                tmax = FLT_MAX;
+            } else {
+                const float* pp = npnt + (size_t)idx * nstride;
+                const f3 p = mk(pp[0], pp[1], pp[2]), lp = ld3(L.pos);
+                d = toward(lp, p);
+                tmax = shadow_tmax(o, p, lp, sv.shadow_eps);
+            }
+        } else {
+            const float4 sd = shadows.d[idx];
+            d = mk(sd.x, sd.y, sd.z);
+            tmax = sd.w;
+        }
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
         // Certification bound (closest_hit ANY): for 0 < t <= t_cert the computed
         // norm(p - (o + d t)) stays below the computed norm(p - L) (the point-light test of
@@ -1894,12 +1925,14 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         // Directional / environment queries are blocked by any hit (t_cert = inf).
         float t_cert = 0.0f;
         if (!EXHAUSTIVE && RTG_SHADOW_ANY) {
-            const ShadowRec sr = shadows[idx];
+            const float4 srL = lean ? make_float4(sv.lights[0].pos[0], sv.lights[0].pos[1], sv.lights[0].pos[2], 0.0f)
+                                    : shadows.L[idx];
+            const float mode = shadows.c[idx].w;
             const int i = idx / sv.num_lights;
             const float* pp = npnt + (size_t)i * nstride;
             const f3 p = mk(pp[0], pp[1], pp[2]);
-            const f3 lp = mk(sr.L.x, sr.L.y, sr.L.z);
-            if (sr.c.w == 1.0f) {
+            const f3 lp = mk(srL.x, srL.y, srL.z);
+            if (mode == 1.0f) {
                 const float DL = norm(p - lp);
                 const float po = norm(p - o), dn = norm(d);
                 const float S = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(p.x))),
@@ -1907,16 +1940,16 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 const float num = DL * (1.0f - 1e-5f) - 1e-5f * S - po * (1.0f + 1e-5f);
                 if (num > 0.0f && dn > 0.0f) t_cert = num / (dn * (1.0f + 2e-5f));
                 if (!(t_cert < FLT_MAX)) t_cert = 0.0f;
-            } else if (sr.c.w == 2.0f) {
+            } else if (mode == 2.0f) {
                 t_cert = INFINITY;
             }
         }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, !EXHAUSTIVE && RTG_SHADOW_ANY>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : sd.w,
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, !EXHAUSTIVE && RTG_SHADOW_ANY>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax,
                                                                s_stack + threadIdx.x, kTraceBlock, s_wnode[threadIdx.x >> 6],
                                                                s_wmask[threadIdx.x >> 6], st, t_cert);
         // the query's contribution / mode are re-read rather than kept live across the traversal
         // (register pressure: 128 VGPRs for 4 waves per SIMD)
-        const float* scp = reinterpret_cast<const float*>(&shadows[idx].c);
+        const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
         const float4 sc = make_float4(__builtin_nontemporal_load(scp), __builtin_nontemporal_load(scp + 1),
                                       __builtin_nontemporal_load(scp + 2), __builtin_nontemporal_load(scp + 3));
         const int i = idx / sv.num_lights;
@@ -1927,12 +1960,21 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             blocked = false;
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
-                const float* q = reinterpret_cast<const float*>(shadows + idx);
                 auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
-                const f3 o_ = mk(ld(q + 0), ld(q + 1), ld(q + 2)), d_ = mk(ld(q + 4), ld(q + 5), ld(q + 6));
-                const f3 l_ = mk(ld(q + 12), ld(q + 13), ld(q + 14));
+                const float* qo = reinterpret_cast<const float*>(shadows.o + idx);
+                const f3 o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
                 const float* pp = npnt + (size_t)i * nstride;
                 const f3 p_ = mk(ld(pp), ld(pp + 1), ld(pp + 2));
+                f3 d_, l_;
+                if (lean) {     // mode 1 with one light: a point / spot light
+                    l_ = ld3(sv.lights[0].pos);
+                    d_ = toward(l_, p_);
+                } else {
+                    const float* qd = reinterpret_cast<const float*>(shadows.d + idx);
+                    const float* ql = reinterpret_cast<const float*>(shadows.L + idx);
+                    d_ = mk(ld(qd), ld(qd + 1), ld(qd + 2));
+                    l_ = mk(ld(ql), ld(ql + 1), ld(ql + 2));
+                }
                 f3 hp = o_ + d_ * h.t;
                 if (sc.w == 1.0f) {
                     blocked = norm(p_ - l_) > norm(p_ - hp);
@@ -1951,7 +1993,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             cp[1] = cp[1] + add.y;
             cp[2] = cp[2] + add.z;
         } else {
-            shadows[idx].L.w = blocked ? 0.0f : 1.0f;
+            reinterpret_cast<float*>(shadows.L + idx)[3] = blocked ? 0.0f : 1.0f;
         }
     }
     // NaN queries are rare: one atomic per wave that has any
@@ -1976,7 +2018,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
 }
 
 // Several lights: Scene::RecursiveShading's in-order sum col = ((amb + L0) + L1) + ...
-__global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const ShadowRec* __restrict__ shadows,
+__global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const ShadowPlanes shadows,
                                                    const NodePlanes nodes, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1984,9 +2026,10 @@ __global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const Sha
     if (!(__float_as_int(nc.w) & 0x100)) return;
     f3 col = mk(nc.x, nc.y, nc.z);
     for (int li = 0; li < sv.num_lights; li++) {
-        const ShadowRec sr = shadows[(size_t)i * sv.num_lights + li];
-        const bool lit = sr.c.w != 0.0f && sr.L.w == 1.0f;
-        col = col + (lit ? mk(sr.c.x, sr.c.y, sr.c.z) : mk(0, 0, 0));
+        const size_t k = (size_t)i * sv.num_lights + li;
+        const float4 sc = shadows.c[k];
+        const bool lit = sc.w != 0.0f && shadows.L[k].w == 1.0f;
+        col = col + (lit ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));
     }
     nodes.col[i] = make_float4(col.x, col.y, col.z, nc.w);
 }
@@ -2181,15 +2224,16 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
     if (n <= 0) return;
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
     const NodePlanes np = node_planes(nodes, n);
+    const ShadowPlanes sp = shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1));
     if (sv.full)
-        hipLaunchKernelGGL((k_shade<true, true>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, shadows,
+        hipLaunchKernelGGL((k_shade<true, true>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp,
                            slist, next_rays, next_meta, qcount, n);
     else if (sv.spot)
         hipLaunchKernelGGL((k_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np,
-                           shadows, slist, next_rays, next_meta, qcount, n);
+                           sp, slist, next_rays, next_meta, qcount, n);
     else
         hipLaunchKernelGGL((k_shade<false, false>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np,
-                           shadows, slist, next_rays, next_meta, qcount, n);
+                           sp, slist, next_rays, next_meta, qcount, n);
 }
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
                    int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted) {
@@ -2200,11 +2244,13 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     float* ncol = whitted ? reinterpret_cast<float*>(np.col) : &nodes[0].cr;
     const float* npnt = whitted ? reinterpret_cast<const float*>(np.pnt) : &nodes[0].px;
     const int ns = whitted ? 4 : (int)(sizeof(NodeRec) / sizeof(float));
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, shadows, slist, scount, ncol, npnt, ns, nan_queries, ctr);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, shadows, slist, scount, ncol, npnt, ns, nan_queries, ctr);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, shadows, slist, scount, ncol, npnt, ns, nan_queries, ctr);
+    const ShadowPlanes sp = shadow_planes(shadows, cap);
+    const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, ncol, npnt, ns, nan_queries, ctr);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, ncol, npnt, ns, nan_queries, ctr);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, ncol, npnt, ns, nan_queries, ctr);
     if (sv.num_lights > 1 && whitted)
-        hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, shadows, np, n);
+        hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, sp, np, n);
 }
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
@@ -2214,7 +2260,7 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
     dim3 g(nblk(n, 256)), b(256);
 #define RTG_PT_LAUNCH(F, S, B)                                                                                    \
     hipLaunchKernelGGL((k_pt_shade<F, S, B>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, nodes, \
-                       shadows, slist, next_rays, next_meta, next_paths, qcount, n)
+                       shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1)), slist, next_rays, next_meta, next_paths, qcount, n)
     // textures / area / environment lights need the full variant; BRDFs alone do not
     if (sv.full && !sv.brdf_only) RTG_PT_LAUNCH(true, true, true);
     else if (sv.full) { if (sv.spot) RTG_PT_LAUNCH(false, true, true); else RTG_PT_LAUNCH(false, false, true); }
@@ -2225,7 +2271,8 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
                       int level, int n, hipStream_t st) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, nodes, paths, shadows, nL, level0, level, n);
+    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, nodes, paths,
+                       shadow_planes(const_cast<ShadowRec*>(shadows), (long long)n * (nL > 1 ? nL : 1)), nL, level0, level, n);
 }
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child, hipStream_t st) {
     if (n <= 0) return;

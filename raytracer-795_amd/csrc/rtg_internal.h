@@ -145,6 +145,8 @@ struct SceneView {
     int full;                      // 0: no textures / BRDFs / area or environment lights
     int spot;                      // any spot light (its double-precision cone math is compiled in)
     int brdf_only;                 // full only because of BRDFs (no textures / area / environment)
+    int lean_shadow;               // one point / spot / directional light: a Whitted shadow query
+                                   // stores only origin + contribution (k_shadow rebuilds d, tmax, L)
     // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
     // lights into num_lights)
     const int* top_emit;           // per top-level entry: emitter light index, -1 if not a light
@@ -248,6 +250,20 @@ struct ShadowRec {      // 64 B, nLights per shading node
     float4 c;           // contribution rgb, mode (0 none, 1 distance test, 2 any hit)
     float4 L;           // light point for the distance test, pad
 };
+
+// A level's shadow records as four planes over cap = nodes x lights entries (same 64 cap bytes):
+// k_shadow reads the ray planes before its traversal and the contribution after it, and the
+// lean single-light Whitted path (SceneView::lean_shadow) does not store `d` / `L` at all.
+struct ShadowPlanes {
+    float4* o;      // origin.xyz, time
+    float4* d;      // direction.xyz, tmax
+    float4* c;      // contribution rgb, mode
+    float4* L;      // light point, lit flag (several lights)
+};
+inline ShadowPlanes shadow_planes(ShadowRec* base, long long cap) {
+    float4* b = reinterpret_cast<float4*>(base);
+    return ShadowPlanes{b, b + cap, b + 2 * cap, b + 3 * cap};
+}
 
 struct Counters {
     unsigned long long node_visits, tri_tests;           // closest-hit kernel
