@@ -1481,7 +1481,11 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
             mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
         } else {
             RayRec r = rays[i];
-            mt = meta[i];
+            if (sv.meta_free && level > 0) {   // nothing below level 0 draws random numbers
+                mt.slot = 0; mt.path_lo = 0u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
+            } else {
+                mt = meta[i];
+            }
             o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
             time = r.o_t.w;
         }
@@ -1622,8 +1626,8 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     __syncthreads();
     int idx = (int)((unsigned)s_base + s_wc[w] + coff);
     if (i < n) {
-        if (has0) { next_rays[idx] = c0r; next_meta[idx] = c0m; nd.child0 = idx; idx++; }
-        if (has1) { next_rays[idx] = c1r; next_meta[idx] = c1m; nd.child1 = idx; }
+        if (has0) { next_rays[idx] = c0r; if (!sv.meta_free) next_meta[idx] = c0m; nd.child0 = idx; idx++; }
+        if (has1) { next_rays[idx] = c1r; if (!sv.meta_free) next_meta[idx] = c1m; nd.child1 = idx; }
         nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind | (hit ? kNodeHit : 0)));
         if (hit) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
         if ((nd.kind & 0xFF) != NK_FINAL) nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, 0);

@@ -954,6 +954,9 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.full |= any_brdf;
     sv.spot = 0;
     for (int i = 0; i < d->num_lights; i++) sv.spot |= d->lights[i].type == RTG_LIGHT_SPOT;
+    int any_rough = 0;
+    for (int i = 0; i < d->num_materials; i++) any_rough |= d->materials[i].is_rough != 0;
+    sv.meta_free = !sv.full && !any_rough;
     sv.lean_shadow = d->num_lights == 1 &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);

@@ -145,6 +145,9 @@ struct SceneView {
     int full;                      // 0: no textures / BRDFs / area or environment lights
     int spot;                      // any spot light (its double-precision cone math is compiled in)
     int brdf_only;                 // full only because of BRDFs (no textures / area / environment)
+    int meta_free;                 // Whitted: no RNG below level 0 (no textures / area / environment
+                                   // lights / rough materials): child rays need no RayMeta (their
+                                   // depth is max_depth - level, slot and path are unused)
     int lean_shadow;               // one point / spot / directional light: a Whitted shadow query
                                    // stores only origin + contribution (k_shadow rebuilds d, tmax, L)
     // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
