@@ -211,3 +211,33 @@ def test_full_frame_shards_sum_exactly(gpu):
         for rank in range(4):
             acc += r.render(0, **shard_opts(rank, 4))
     assert np.array_equal(acc.view(np.int32), full.view(np.int32))
+
+
+# One point / spot / directional light takes the lean shadow-record path (k_shadow rebuilds the
+# direction and t bound, SceneView::lean_shadow); a rough mirror keeps the child RayMeta
+# records (SceneView::meta_free off); two lights take the full four-plane records.
+@pytest.mark.parametrize("kind", ["point", "spot", "directional", "two_lights", "rough_mirror"])
+def test_shadow_record_paths_match_oracle(gpu, kind):
+    from rtg import _abi as A
+    from rtg.scene import Light
+    sc = scenegen.bunny5k(64, 48, level=3, spp=2)
+    L = sc.lights[0]
+    if kind == "spot":
+        sc.lights[0] = Light(type=A.LIGHT_SPOT, position=L.position, direction=(-0.4, -1.0, -0.6),
+                             intensity=L.intensity, coverage_deg=50, falloff_deg=25)
+    elif kind == "directional":
+        sc.lights[0] = Light(type=A.LIGHT_DIRECTIONAL, direction=(-0.3, -1.0, -0.5), intensity=(3, 3, 3))
+    elif kind == "two_lights":
+        sc.lights.append(Light(type=A.LIGHT_DIRECTIONAL, direction=(0.5, -1.0, 0.2), intensity=(2, 2, 2)))
+    elif kind == "rough_mirror":
+        sc.materials[1].is_rough, sc.materials[1].roughness = True, 0.15
+    with rtg.Renderer(sc, device=gpu) as r:
+        img = r.render(0)
+        st = r.stats()
+    o = pyoracle.Oracle(sc)
+    ref, _, _, _ = o.render(0)
+    linf, frac, nanm = _cmp(img, ref)
+    print(f"{kind}: Linf={linf:.3g} differing={frac:.2e} shadow={st['shadow_rays']}/{o.ray_counts()['shadow']}")
+    assert nanm == 0
+    assert linf < TOL
+    assert 0 < st["shadow_rays"] <= o.ray_counts()["shadow"]
