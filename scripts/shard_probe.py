@@ -1,0 +1,29 @@
+"""Per-rank frame time of the N-GPU row shards on one GPU (what each rank of bench.py --gpus N
+renders): render_ms of every shard k of N (row_offset k, row_stride N, the bench's row block),
+compact owned rows left in HBM.  usage: python scripts/shard_probe.py [N ...]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracer-795_amd"))
+import torch  # noqa: E402
+import rtg  # noqa: E402
+from rtg import scenegen  # noqa: E402
+from rtg.shard import shard_opts  # noqa: E402
+
+sc = scenegen.dragon1m(1920, 1080, spp=64)
+r = rtg.Renderer(sc, 0)
+out = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
+for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
+    ms = []
+    for k in range(n):
+        kw = dict(shard_opts(k, n), compact_rows=1 if n > 1 else 0)
+        r.render_device(0, out.data_ptr(), **kw)          # warm (buffers sized for this shard)
+        torch.cuda.synchronize()
+        best = 1e9
+        for _ in range(3):
+            r.render_device(0, out.data_ptr(), **kw)
+            torch.cuda.synchronize()
+            best = min(best, r.stats()["render_ms"])
+        ms.append(best)
+    print(f"N={n}: per-rank render_ms max {max(ms):.2f} min {min(ms):.2f}", flush=True)
