@@ -20,7 +20,10 @@ constexpr int kPacketStack = 64;    // wave stack of the packet walk: <= 3 pushe
 #define RTG_TRACE_BLOCK 64
 #endif
 constexpr int kTraceBlock = RTG_TRACE_BLOCK;   // threads per traversal block (LDS stack: 128 B per lane)
-constexpr int kShadeBlock = 512;
+#ifndef RTG_SHADE_BLOCK
+#define RTG_SHADE_BLOCK 512
+#endif
+constexpr int kShadeBlock = RTG_SHADE_BLOCK;   // k_shade (simple variants): one queue atomic per block
 
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:86-127):
 // objects first, then instances.  Read with scalar loads (wave-uniform loop).
