@@ -17,7 +17,8 @@ out = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
 for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
     ms = []
     for k in range(n):
-        kw = dict(shard_opts(k, n), compact_rows=1 if n > 1 else 0)
+        kw = dict(shard_opts(k, n), compact_rows=1 if n > 1 else 0,
+                  max_batch_rays=int(os.environ.get("RTG_BATCH", "0")))
         r.render_device(0, out.data_ptr(), **kw)          # warm (buffers sized for this shard)
         torch.cuda.synchronize()
         best = 1e9
@@ -26,4 +27,4 @@ for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
             torch.cuda.synchronize()
             best = min(best, r.stats()["render_ms"])
         ms.append(best)
-    print(f"N={n}: per-rank render_ms max {max(ms):.2f} min {min(ms):.2f}", flush=True)
+    print(f"batch={os.environ.get('RTG_BATCH', '0')} N={n}: per-rank render_ms max {max(ms):.2f} min {min(ms):.2f}", flush=True)
