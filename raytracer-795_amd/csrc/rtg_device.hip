@@ -1371,11 +1371,25 @@ __global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassD
     meta[i] = mt;
 }
 
+// Render-path hit records: k_shade / k_pt_shade rebuild the hit from (object, primitive) alone
+// (hit_record re-runs the winning test), so the wavefront stores 8 bytes per ray, not the
+// 16-byte HitRec the rtg_trace_closest path returns.
+DEV void store_hit_compact(HitRec* hits, int i, const HitRec& h) {
+    reinterpret_cast<int2*>(hits)[i] = make_int2(h.obj, h.prim);
+}
+DEV HitRec load_hit_compact(const HitRec* hits, int i) {
+    const int2 v = reinterpret_cast<const int2*>(hits)[i];
+    HitRec h;
+    h.obj = v.x; h.prim = v.y; h.t = 0.0f; h.pad = 0;
+    return h;
+}
+
 // GEN: level-0 launch of the Whitted path, the ray is primary_ray(slot i) (no RayRec buffer).
 template <bool EXHAUSTIVE, bool STATS, bool GEN = false>
 __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayRec* __restrict__ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
-                                                       const CameraDev cam, const PassDev ps, uint64_t seed) {
+                                                       const CameraDev cam, const PassDev ps, uint64_t seed,
+                                                       bool compact) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
     __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
@@ -1394,7 +1408,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
         }
         HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock,
                                                   s_wnode[threadIdx.x >> 6], s_wmask[threadIdx.x >> 6], st);
-        hits[i] = h;
+        if (compact) store_hit_compact(hits, i, h);
+        else hits[i] = h;
     }
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
@@ -1472,7 +1487,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     NodeRec nd;
     unsigned long long smask = 0;   // lights whose shadow query must be traced
     if (i < n) {
-        HitRec h = hits[i];
+        const HitRec h = load_hit_compact(hits, i);
         f3 o, d;
         float time;
         RayMeta mt;
@@ -1696,7 +1711,7 @@ __global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const Came
     if (i < n) {
         const RayRec r = rays[i];
         const RayMeta mt = meta[i];
-        const HitRec h = hits[i];
+        const HitRec h = load_hit_compact(hits, i);
         const f3 o = mk(r.o_t.x, r.o_t.y, r.o_t.z), d = mk(r.d.x, r.d.y, r.d.z);
         const float time = r.o_t.w;
         uint32_t pixel, sample;
@@ -2206,20 +2221,20 @@ void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps,
     hipLaunchKernelGGL(k_raygen, dim3(nblk(n, 256)), dim3(256), 0, st, cam, ps, seed, rays, meta, n, sv.max_depth);
 }
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
-                  hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed) {
+                  hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed, bool compact) {
     if (n <= 0) return;
     dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
     const CameraDev cam = gen_cam ? *gen_cam : CameraDev{};
     const PassDev ps = gen_ps ? *gen_ps : PassDev{};
     if (gen_cam) {   // primary rays generated in the kernel (rays unused)
-        if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
-        else if (ctr) hipLaunchKernelGGL((k_trace<false, true, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
-        else hipLaunchKernelGGL((k_trace<false, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
+        if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+        else if (ctr) hipLaunchKernelGGL((k_trace<false, true, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+        else hipLaunchKernelGGL((k_trace<false, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
         return;
     }
-    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
-    else if (ctr) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
-    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed);
+    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+    else if (ctr) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
 }
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,

@@ -1160,7 +1160,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         // Whitted level 0: k_trace / k_shade regenerate the primary rays (no level-0 ray buffer)
         const bool gen = !pt && level == 0;
         launch_trace(sv, gen ? nullptr : Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st,
-                     gen ? &cd : nullptr, gen ? &ps : nullptr, o.seed);
+                     gen ? &cd : nullptr, gen ? &ps : nullptr, o.seed, /*compact=*/true);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
         if (pt)
             launch_pt_shade(sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),

@@ -284,7 +284,7 @@ void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps,
 // gen_cam / gen_ps non-null: level 0 of the Whitted path, rays are generated in the kernel
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
-                  uint64_t seed = 0);
+                  uint64_t seed = 0, bool compact = false);
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta,
                   unsigned long long* qcount, int n, hipStream_t st);
