@@ -26,8 +26,14 @@ namespace rtg {
 #ifndef RTG_SHADOW_ATTR  // 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
-#ifndef RTG_SHADE_ATTR   // occupancy experiments on k_shade (Whitted, non-full variants)
-#define RTG_SHADE_ATTR
+#ifndef RTG_SHADE_ATTR   // k_shade: the full variant (textures / BRDFs / area & environment lights) needs
+                         // > 256 registers; capped at 2 waves per SIMD it spills 236 B/lane and is
+                         // still faster (cornell_dynamic 1080p64: 34.0 -> 29.7 ms); the simple
+                         // variants already fit 4 waves (no-op for them)
+#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#endif
+#ifndef RTG_PT_SHADE_ATTR  // occupancy experiments on k_pt_shade
+#define RTG_PT_SHADE_ATTR
 #endif
 #ifndef RTG_PACKET        // 1: wave-packet walk of the 4-wide tree (scalar node loads, one stack per wave)
 #define RTG_PACKET 0
@@ -1693,7 +1699,7 @@ DEV DielSplit dielectric_split(const SceneView& sv, f3 d, const Ret& ret, const 
 constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour to the sample
 
 template <bool FULL, bool SPOT, bool BRDF>
-__global__ void __launch_bounds__(256) k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+__global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                   uint64_t seed, const RayRec* __restrict__ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
                                                   PathRec* __restrict__ paths, NodeRec* __restrict__ nodes,
