@@ -1476,7 +1476,10 @@ DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialD
     rd = wr;
 }
 
-template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock>
+// TEX (full variant only): object texturing and BRDFs compiled in; a full scene without them
+// (area / environment lights, background texture) runs k_shade<true, *, 256, false>, which has
+// far fewer live registers.
+template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL>
 __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                uint64_t seed,
                                                const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
@@ -1531,7 +1534,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
             }
         } else {
             hit = true;
-            Ret ret = hit_record<FULL>(sv, o, d, time, h);
+            Ret ret = hit_record<FULL && TEX>(sv, o, d, time, h);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading :361-372
@@ -1602,7 +1605,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
-                        light_sample<FULL, SPOT>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
+                        light_sample<FULL, SPOT, FULL && TEX>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         // one light: a query that is not traced is never read (k_light_sum reads
                         // every record when there are several)
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
@@ -2250,9 +2253,12 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
     const NodePlanes np = node_planes(nodes, n);
     const ShadowPlanes sp = shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1));
-    if (sv.full)
+    if (sv.full && sv.tex)
         hipLaunchKernelGGL((k_shade<true, true>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp,
                            slist, next_rays, next_meta, qcount, n);
+    else if (sv.full)
+        hipLaunchKernelGGL((k_shade<true, true, 256, false>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays,
+                           meta, hits, np, sp, slist, next_rays, next_meta, qcount, n);
     else if (sv.spot)
         hipLaunchKernelGGL((k_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np,
                            sp, slist, next_rays, next_meta, qcount, n);

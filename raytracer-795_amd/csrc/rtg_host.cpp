@@ -951,6 +951,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     int any_brdf = 0;
     for (int i = 0; i < d->num_materials; i++) any_brdf |= d->materials[i].brdf != RTG_BRDF_NONE;
     sv.brdf_only = !sv.full && any_brdf;
+    sv.tex = any_brdf;
+    for (int i = 0; i < d->num_objects; i++) sv.tex |= d->objects[i].num_textures > 0;
     sv.full |= any_brdf;
     sv.spot = 0;
     for (int i = 0; i < d->num_lights; i++) sv.spot |= d->lights[i].type == RTG_LIGHT_SPOT;

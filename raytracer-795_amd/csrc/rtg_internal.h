@@ -148,6 +148,7 @@ struct SceneView {
     int full;                      // 0: no textures / BRDFs / area or environment lights
     int spot;                      // any spot light (its double-precision cone math is compiled in)
     int brdf_only;                 // full only because of BRDFs (no textures / area / environment)
+    int tex;                       // any textured object or BRDF material (k_shade's TEX variant)
     int meta_free;                 // Whitted: no RNG below level 0 (no textures / area / environment
                                    // lights / rough materials): child rays need no RayMeta (their
                                    // depth is max_depth - level, slot and path are unused)
