@@ -32,8 +32,10 @@ namespace rtg {
                          // variants already fit 4 waves (no-op for them)
 #define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
-#ifndef RTG_PT_SHADE_ATTR  // occupancy experiments on k_pt_shade
-#define RTG_PT_SHADE_ATTR
+#ifndef RTG_PT_SHADE_ATTR  // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168
+                           // VGPRs, 64 B/lane spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves
+                           // (236 B spill) is slower (594 ms); the full variants keep the default
+#define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? 3 : 1)))
 #endif
 #ifndef RTG_PACKET        // 1: wave-packet walk of the 4-wide tree (scalar node loads, one stack per wave)
 #define RTG_PACKET 0
@@ -1705,7 +1707,7 @@ template <bool FULL, bool SPOT, bool BRDF>
 __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                   uint64_t seed, const RayRec* __restrict__ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
-                                                  PathRec* __restrict__ paths, NodeRec* __restrict__ nodes,
+                                                  PathRec* __restrict__ paths, const NodePlanes nodes,
                                                   const ShadowPlanes shadows, int* __restrict__ slist,
                                                   RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
                                                   PathRec* __restrict__ next_paths, unsigned long long* qcount, int n) {
@@ -1863,7 +1865,9 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
     const int idx = (int)((unsigned)s_base + s_wc[wv] + coff);
     if (i < n) {
         if (has) { next_rays[idx] = cr; next_meta[idx] = cm; next_paths[idx] = cp; nd.child1 = idx; }
-        nodes[i] = nd;
+        nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
+        nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
+        nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, nd.slot);
     }
     unsigned sb = (unsigned)(s_base >> 32) + s_ws[wv];
     for (int li = 0; li < sv.num_lights; li++) {
@@ -1877,15 +1881,16 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
 // L[slot] += T (x) v of every contributing vertex, one level at a time (stream order keeps
 // the oracle's per-sample summation order).  Level 0 starts the sum: L = (0,0,0) [+ T (x) v].
 // With several lights the in-order light sum of k_light_sum is folded in here.
-__global__ void __launch_bounds__(256) k_pt_gather(const NodeRec* __restrict__ nodes, const PathRec* __restrict__ paths,
+__global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const PathRec* __restrict__ paths,
                                                    const ShadowPlanes shadows, int nL,
-                                                   NodeRec* __restrict__ level0, int level, int n) {
+                                                   const NodePlanes level0, int level, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const NodeRec nd = nodes[i];
-    const bool c = (nd.kind & kContrib) != 0;
-    f3 v = mk(nd.cr, nd.cg, nd.cb);
-    if (nL > 1 && (nd.kind & 0x100)) {          // Scene::RecursiveShading's col = ((amb + L0) + L1) + ...
+    const float4 nc = nodes.col[i];
+    const int kind = __float_as_int(nc.w);
+    const bool c = (kind & kContrib) != 0;
+    f3 v = mk(nc.x, nc.y, nc.z);
+    if (nL > 1 && (kind & 0x100)) {          // Scene::RecursiveShading's col = ((amb + L0) + L1) + ...
         for (int li = 0; li < nL; li++) {
             const float4 sc = shadows.c[(size_t)i * nL + li];
             const float lit = shadows.L[(size_t)i * nL + li].w;
@@ -1895,11 +1900,12 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodeRec* __restrict__ n
     if (level == 0) {
         f3 L = mk(0, 0, 0);
         if (c) L = L + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), v);
-        level0[i].cr = L.x; level0[i].cg = L.y; level0[i].cb = L.z;
+        level0.col[i] = make_float4(L.x, L.y, L.z, nc.w);
     } else if (c) {
-        NodeRec& z = level0[nd.slot];
-        const f3 L = mk(z.cr, z.cg, z.cb) + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), v);
-        z.cr = L.x; z.cg = L.y; z.cb = L.z;
+        const int slot = nodes.link[i].w;
+        const float4 z = level0.col[slot];
+        const f3 L = mk(z.x, z.y, z.z) + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), v);
+        level0.col[slot] = make_float4(L.x, L.y, L.z, z.w);
     }
 }
 
@@ -1915,8 +1921,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        float* __restrict__ ncol,
                                                                        const float* __restrict__ npnt, int nstride,
                                                                        unsigned* nan_queries, Counters* ctr) {
-    // node i's colour at ncol + i * nstride, its hit point at npnt + i * nstride (NodePlanes:
-    // stride 4 floats; the path tracer's NodeRec array: stride 12)
+    // node i's colour at ncol + i * nstride, its hit point at npnt + i * nstride (the NodePlanes
+    // colour / point planes: stride 4 floats)
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
     __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
@@ -2130,8 +2136,7 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodeP
 // order.  mode 2: the single sample itself; 1: first chunk (start from 0); 0: continue the
 // running sum in `acc`.
 constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
-// Colours are read at ncol + slot * nstride (the NodePlanes colour plane: stride 4; the path
-// tracer's NodeRec array: stride 12); `resolve` (Whitted only) evaluates non-final level-0 nodes
+// Colours are read from the level-0 NodePlanes colour plane (ncol, stride 4); `resolve` (Whitted only) evaluates non-final level-0 nodes
 // against level 1 first.
 __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv, const float* __restrict__ ncol, int nstride,
                                                     const NodePlanes level0, const NodePlanes level1, bool resolve,
@@ -2272,9 +2277,9 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
     const NodePlanes np = node_planes(nodes, n);
-    float* ncol = whitted ? reinterpret_cast<float*>(np.col) : &nodes[0].cr;
-    const float* npnt = whitted ? reinterpret_cast<const float*>(np.pnt) : &nodes[0].px;
-    const int ns = whitted ? 4 : (int)(sizeof(NodeRec) / sizeof(float));
+    float* ncol = reinterpret_cast<float*>(np.col);
+    const float* npnt = reinterpret_cast<const float*>(np.pnt);
+    const int ns = 4;
     const ShadowPlanes sp = shadow_planes(shadows, cap);
     const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
     if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, ncol, npnt, ns, nan_queries, ctr);
@@ -2290,7 +2295,8 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
     if (n <= 0) return;
     dim3 g(nblk(n, 256)), b(256);
 #define RTG_PT_LAUNCH(F, S, B)                                                                                    \
-    hipLaunchKernelGGL((k_pt_shade<F, S, B>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, nodes, \
+    hipLaunchKernelGGL((k_pt_shade<F, S, B>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, \
+                       node_planes(nodes, n), \
                        shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1)), slist, next_rays, next_meta, next_paths, qcount, n)
     // textures / area / environment lights need the full variant; BRDFs alone do not
     if (sv.full && !sv.brdf_only) RTG_PT_LAUNCH(true, true, true);
@@ -2300,10 +2306,11 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
 #undef RTG_PT_LAUNCH
 }
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
-                      int level, int n, hipStream_t st) {
+                      int n0, int level, int n, hipStream_t st) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, nodes, paths,
-                       shadow_planes(const_cast<ShadowRec*>(shadows), (long long)n * (nL > 1 ? nL : 1)), nL, level0, level, n);
+    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, node_planes(const_cast<NodeRec*>(nodes), n), paths,
+                       shadow_planes(const_cast<ShadowRec*>(shadows), (long long)n * (nL > 1 ? nL : 1)), nL,
+                       node_planes(level0, n0), level, n);
 }
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child, hipStream_t st) {
     if (n <= 0) return;
@@ -2314,10 +2321,10 @@ void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec
                        const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1) {
     if (ps.npass <= 0) return;
     NodeRec* l0 = const_cast<NodeRec*>(level0);
-    const NodePlanes p0 = whitted ? node_planes(l0, n0) : NodePlanes{};
+    const NodePlanes p0 = node_planes(l0, n0);
     const NodePlanes p1 = (whitted && level1) ? node_planes(const_cast<NodeRec*>(level1), n1) : NodePlanes{};
-    const float* ncol = whitted ? reinterpret_cast<const float*>(p0.col) : &l0[0].cr;
-    const int ns = whitted ? 4 : (int)(sizeof(NodeRec) / sizeof(float));
+    const float* ncol = reinterpret_cast<const float*>(p0.col);
+    const int ns = 4;
     hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, ncol, ns, p0, p1,
                        resolve && whitted, acc, ps, nx, mode);
 }

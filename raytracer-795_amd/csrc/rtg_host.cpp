@@ -1186,7 +1186,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt)
             launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), Lc.shadows.as<ShadowRec>(), nL,
-                             ln.levels[0].nodes.as<NodeRec>(), level, n, ln.st);
+                             ln.levels[0].nodes.as<NodeRec>(), ln.counts[0], level, n, ln.st);
         HIP_TRY(hipGetLastError());
         return RTG_OK;
     };

@@ -239,7 +239,8 @@ struct NodeRec {        // 48 B, one per traced ray
 // Whitted path: a level's n node records as three planes in the same 48 n bytes (structure of
 // arrays), so the kernels that only need a node's colour (accumulate, light sums, final nodes in
 // resolve) read 16 B of it, and k_shade stores the point only for hits and the links only for
-// non-final nodes.  The path tracer keeps the NodeRec array (k_pt_shade / k_pt_gather).
+// non-final nodes.  The path tracer uses the same planes (all three stored; link.w = the slot
+// k_pt_gather adds the vertex's contribution to).
 struct NodePlanes {
     float4* col;    // cr, cg, cb, kind (int bits; kNodeHit set for hits)
     float4* pnt;    // px, py, pz, F               (hit nodes only)
@@ -296,10 +297,10 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
                      ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st);
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
-                      int level, int n, hipStream_t st);
+                      int n0, int level, int n, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
-// whitted: level0 / level1 hold NodePlanes over n0 / n1 nodes (else NodeRec arrays, path tracer)
+// level0 / level1 hold NodePlanes over n0 / n1 nodes; whitted: resolve level 0 against level 1
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
                        const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1);
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block, int total,
