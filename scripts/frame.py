@@ -12,6 +12,14 @@ w = os.environ.get("RTG_WORKLOAD", "dragon1m")      # any rtg.scenegen factory
 sc = getattr(scenegen, w)(1920, 1080, spp=int(os.environ.get("RTG_SPP", "256" if w == "cornell_pt" else "64")))
 r = rtg.Renderer(sc, 0)
 stride = int(os.environ.get("RTG_ROW_STRIDE", "1"))     # one multi-GPU rank's row shard
-for _ in range(n):
-    r.render(0, row_offset=0, row_stride=stride, row_block=int(os.environ.get("RTG_ROW_BLOCK", "8")))
+kw = dict(row_offset=0, row_stride=stride, row_block=int(os.environ.get("RTG_ROW_BLOCK", "8")))
+if os.environ.get("RTG_DEVICE_OUT") == "1":              # as bench.py: output left in HBM
+    import torch
+    out = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
+    for _ in range(n):
+        r.render_device(0, out.data_ptr(), compact_rows=1 if stride > 1 else 0, **kw)
+    torch.cuda.synchronize()
+else:
+    for _ in range(n):
+        r.render(0, **kw)
 print("frame ms", round(r.stats()["render_ms"], 1))
