@@ -32,6 +32,15 @@ namespace rtg {
                          // variants already fit 4 waves (no-op for them)
 #define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
+// Non-temporal hints on the queue records (measured on the 1080p64 dragon, 2 runs each, and
+// left off: frame time within ±0.2 ms noise of 47.7 ms — the node / triangle working set stays
+// in L2 + MALL either way)
+#ifndef RTG_NT_RECORDS     // 1: queue-record loads ahead of a traversal are non-temporal
+#define RTG_NT_RECORDS 0
+#endif
+#ifndef RTG_NT_STORES      // 1: k_shade's queue-record stores are non-temporal
+#define RTG_NT_STORES 0
+#endif
 #ifndef RTG_PT_SHADE_ATTR  // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168
                            // VGPRs, 64 B/lane spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves
                            // (236 B spill) is slower (594 ms); the full variants keep the default
@@ -1383,6 +1392,27 @@ __global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassD
 // Render-path hit records: k_shade / k_pt_shade rebuild the hit from (object, primitive) alone
 // (hit_record re-runs the winning test), so the wavefront stores 8 bytes per ray, not the
 // 16-byte HitRec the rtg_trace_closest path returns.
+DEV float4 ld_rec(const float4* p) {
+    if (RTG_NT_RECORDS) {
+        const float* q = reinterpret_cast<const float*>(p);
+        return make_float4(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1),
+                           __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3));
+    }
+    return *p;
+}
+DEV void st_rec(float4* p, float4 v) {
+    if (RTG_NT_STORES) {
+        float* q = reinterpret_cast<float*>(p);
+        __builtin_nontemporal_store(v.x, q); __builtin_nontemporal_store(v.y, q + 1);
+        __builtin_nontemporal_store(v.z, q + 2); __builtin_nontemporal_store(v.w, q + 3);
+    } else {
+        *p = v;
+    }
+}
+DEV void st_rec(int4* p, int4 v) {
+    st_rec(reinterpret_cast<float4*>(p), make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z),
+                                                     __int_as_float(v.w)));
+}
 DEV void store_hit_compact(HitRec* hits, int i, const HitRec& h) {
     reinterpret_cast<int2*>(hits)[i] = make_int2(h.obj, h.prim);
 }
@@ -1411,7 +1441,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
             primary_ray(cam, ps, seed, i, o, d, time);
             tmax = FLT_MAX;
         } else {
-            RayRec r = rays[i];
+            RayRec r;
+            r.o_t = ld_rec(&rays[i].o_t); r.d = ld_rec(&rays[i].d);
             o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
             time = r.o_t.w; tmax = r.d.w;
         }
@@ -1613,9 +1644,9 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                         // every record when there are several)
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
                             const size_t k = (size_t)i * sv.num_lights + li;
-                            shadows.o[k] = sr.o;
-                            shadows.c[k] = sr.c;
-                            if (!sv.lean_shadow) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
+                            st_rec(shadows.o + k, sr.o);
+                            st_rec(shadows.c + k, sr.c);
+                            if (!sv.lean_shadow) { st_rec(shadows.d + k, sr.d); st_rec(shadows.L + k, sr.L); }
                         }
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
@@ -1653,11 +1684,17 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     __syncthreads();
     int idx = (int)((unsigned)s_base + s_wc[w] + coff);
     if (i < n) {
-        if (has0) { next_rays[idx] = c0r; if (!sv.meta_free) next_meta[idx] = c0m; nd.child0 = idx; idx++; }
-        if (has1) { next_rays[idx] = c1r; if (!sv.meta_free) next_meta[idx] = c1m; nd.child1 = idx; }
-        nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind | (hit ? kNodeHit : 0)));
-        if (hit) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
-        if ((nd.kind & 0xFF) != NK_FINAL) nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, 0);
+        auto put_ray = [&](int k, const RayRec& rr, const RayMeta& mm) {
+            st_rec(&next_rays[k].o_t, rr.o_t);
+            st_rec(&next_rays[k].d, rr.d);
+            if (!sv.meta_free) st_rec(reinterpret_cast<int4*>(next_meta + k), make_int4(mm.slot, (int)mm.path_lo,
+                                                                                         (int)mm.path_hi, mm.depth));
+        };
+        if (has0) { put_ray(idx, c0r, c0m); nd.child0 = idx; idx++; }
+        if (has1) { put_ray(idx, c1r, c1m); nd.child1 = idx; }
+        st_rec(nodes.col + i, make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind | (hit ? kNodeHit : 0))));
+        if (hit) st_rec(nodes.pnt + i, make_float4(nd.px, nd.py, nd.pz, nd.F));
+        if ((nd.kind & 0xFF) != NK_FINAL) st_rec(nodes.link + i, make_int4(nd.child0, nd.child1, nd.material, 0));
     }
     unsigned sb = (unsigned)(s_base >> 32) + s_ws[w];
     for (int li = 0; li < sv.num_lights; li++) {
@@ -1932,7 +1969,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     Stats st = {0, 0, 0, 0};
     if (j < (int)*scount) {
         const int idx = slist[j];
-        const float4 so = shadows.o[idx];
+        const float4 so = ld_rec(shadows.o + idx);
         const f3 o = mk(so.x, so.y, so.z);
         f3 d;
         float tmax;
@@ -1942,13 +1979,13 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 d = -ld3(L.dir);
                 tmax = FLT_MAX;
             } else {
-                const float* pp = npnt + (size_t)idx * nstride;
-                const f3 p = mk(pp[0], pp[1], pp[2]), lp = ld3(L.pos);
+                const float4 pf = ld_rec(reinterpret_cast<const float4*>(npnt + (size_t)idx * nstride));
+                const f3 p = mk(pf.x, pf.y, pf.z), lp = ld3(L.pos);
                 d = toward(lp, p);
                 tmax = shadow_tmax(o, p, lp, sv.shadow_eps);
             }
         } else {
-            const float4 sd = shadows.d[idx];
+            const float4 sd = ld_rec(shadows.d + idx);
             d = mk(sd.x, sd.y, sd.z);
             tmax = sd.w;
         }
