@@ -1758,11 +1758,19 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
     NodeRec nd;
     unsigned long long smask = 0;
     if (i < n) {
-        const RayRec r = rays[i];
-        const RayMeta mt = meta[i];
+        f3 o, d;
+        float time;
+        RayMeta mt;
+        if (rays == nullptr) {          // level 0 without a ray buffer: regenerate (k_raygen's record)
+            primary_ray(cam, ps, seed, i, o, d, time);
+            mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
+        } else {
+            const RayRec r = rays[i];
+            mt = meta[i];
+            o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
+            time = r.o_t.w;
+        }
         const HitRec h = load_hit_compact(hits, i);
-        const f3 o = mk(r.o_t.x, r.o_t.y, r.o_t.z), d = mk(r.d.x, r.d.y, r.d.z);
-        const float time = r.o_t.w;
         uint32_t pixel, sample;
         int x, y;
         slot_pixel(cam, ps, mt.slot, pixel, sample, x, y);

@@ -1159,13 +1159,14 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             return rc2;
         unsigned long long* qc = ln.qcnt.as<unsigned long long>() + level;
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
-        // Whitted level 0: k_trace / k_shade regenerate the primary rays (no level-0 ray buffer)
-        const bool gen = !pt && level == 0;
+        // level 0: k_trace / k_shade / k_pt_shade regenerate the primary rays (no level-0 ray buffer)
+        const bool gen = level == 0;
         launch_trace(sv, gen ? nullptr : Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st,
                      gen ? &cd : nullptr, gen ? &ps : nullptr, o.seed, /*compact=*/true);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
         if (pt)
-            launch_pt_shade(sv, cd, level, ps, o.seed, Lc.rays.as<RayRec>(), Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
+            launch_pt_shade(sv, cd, level, ps, o.seed, gen ? nullptr : Lc.rays.as<RayRec>(),
+                            gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                             Lc.paths.as<PathRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                             Ln.rays.as<RayRec>(), Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st);
         else
@@ -1200,12 +1201,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         ln.counts.assign(1, n0);
         ln.level = 0;
         if ((int)ln.levels.size() < 1) ln.levels.resize(1);
-        Level& L0 = ln.levels[0];
-        if (pt) {   // the Whitted path generates its primary rays inside level 0's trace / shade
-            if ((rc2 = L0.rays.grow(sizeof(RayRec) * (size_t)n0)) || (rc2 = L0.meta.grow(sizeof(RayMeta) * (size_t)n0)))
-                return rc2;
-            launch_raygen(sv, cd, ps, o.seed, L0.rays.as<RayRec>(), L0.meta.as<RayMeta>(), n0, ln.st);
-        }
+        // no k_raygen: both integrators generate their primary rays inside level 0's kernels
         stt.primary_rays += (uint64_t)n0;
         ln.busy = true;
         return enqueue_level(ln);
