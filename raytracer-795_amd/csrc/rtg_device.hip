@@ -1320,9 +1320,9 @@ DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f
 }
 
 // ------------------------------------------------------------------ kernels
-// Primary ray of sample slot i of the pass.  k_raygen stores it; the Whitted path's level-0
-// k_trace / k_shade recompute it from the slot instead (same function, so bit-identical),
-// which saves the 48-byte RayRec + RayMeta store and its two re-reads per primary ray.
+// Primary ray of sample slot i of the pass (Camera::getPrimaryRay / getSampleRay).  Level 0's
+// k_trace / k_shade / k_pt_shade compute it from the slot (same function, so bit-identical)
+// instead of storing a 48-byte RayRec + RayMeta per primary ray and re-reading it twice.
 DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int i, f3& o_out, f3& d_out,
                      float& time_out) {
     uint32_t pixel, sample;
@@ -1372,23 +1372,6 @@ DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int
     o_out = o; d_out = d; time_out = time;
 }
 
-__global__ void __launch_bounds__(256) k_raygen(const CameraDev cam, const PassDev ps, uint64_t seed,
-                                                RayRec* __restrict__ rays, RayMeta* __restrict__ meta, int n,
-                                                int max_depth) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    f3 o, d;
-    float time;
-    primary_ray(cam, ps, seed, i, o, d, time);
-    RayRec r;
-    r.o_t = make_float4(o.x, o.y, o.z, time);
-    r.d = make_float4(d.x, d.y, d.z, FLT_MAX);
-    rays[i] = r;
-    RayMeta mt;
-    mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = max_depth;
-    meta[i] = mt;
-}
-
 // Render-path hit records: k_shade / k_pt_shade rebuild the hit from (object, primitive) alone
 // (hit_record re-runs the winning test), so the wavefront stores 8 bytes per ray, not the
 // 16-byte HitRec the rtg_trace_closest path returns.
@@ -1423,7 +1406,7 @@ DEV HitRec load_hit_compact(const HitRec* hits, int i) {
     return h;
 }
 
-// GEN: level-0 launch of the Whitted path, the ray is primary_ray(slot i) (no RayRec buffer).
+// GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no RayRec buffer).
 template <bool EXHAUSTIVE, bool STATS, bool GEN = false>
 __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayRec* __restrict__ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
@@ -1534,7 +1517,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
         f3 o, d;
         float time;
         RayMeta mt;
-        if (rays == nullptr) {          // level 0 without a ray buffer: regenerate (k_raygen's record)
+        if (rays == nullptr) {          // level 0 without a ray buffer: generate the primary ray and its meta
             primary_ray(cam, ps, seed, i, o, d, time);
             mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
         } else {
@@ -1761,7 +1744,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
         f3 o, d;
         float time;
         RayMeta mt;
-        if (rays == nullptr) {          // level 0 without a ray buffer: regenerate (k_raygen's record)
+        if (rays == nullptr) {          // level 0 without a ray buffer: generate the primary ray and its meta
             primary_ray(cam, ps, seed, i, o, d, time);
             mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
         } else {
@@ -2284,11 +2267,6 @@ __global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const R
 // ------------------------------------------------------------------ launchers
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 
-void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps, uint64_t seed, RayRec* rays,
-                   RayMeta* meta, int n, hipStream_t st) {
-    if (n <= 0) return;
-    hipLaunchKernelGGL(k_raygen, dim3(nblk(n, 256)), dim3(256), 0, st, cam, ps, seed, rays, meta, n, sv.max_depth);
-}
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
                   hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed, bool compact) {
     if (n <= 0) return;

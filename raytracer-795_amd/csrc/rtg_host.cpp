@@ -1201,7 +1201,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         ln.counts.assign(1, n0);
         ln.level = 0;
         if ((int)ln.levels.size() < 1) ln.levels.resize(1);
-        // no k_raygen: both integrators generate their primary rays inside level 0's kernels
+        // both integrators generate their primary rays inside level 0's kernels (primary_ray)
         stt.primary_rays += (uint64_t)n0;
         ln.busy = true;
         return enqueue_level(ln);

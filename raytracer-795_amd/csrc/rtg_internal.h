@@ -281,9 +281,7 @@ struct Counters {
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
 struct LevelBuffers;
-void launch_raygen(const SceneView& sv, const CameraDev& cam, const PassDev& ps, uint64_t seed, RayRec* rays,
-                   RayMeta* meta, int n, hipStream_t st);
-// gen_cam / gen_ps non-null: level 0 of the Whitted path, rays are generated in the kernel
+// gen_cam / gen_ps non-null: level 0 (either integrator), rays are generated in the kernel
 void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
                   uint64_t seed = 0, bool compact = false);
