@@ -17,42 +17,16 @@
 namespace rtg {
 
 #define DEV __device__ __forceinline__
-#ifndef RTG_BVH4
-#define RTG_BVH4 1       // 1: 4-wide collapsed BVH walk (BVH2 walk as overflow fallback); 0: BVH2 only
-#endif
-#ifndef RTG_TRACE_ATTR
-#define RTG_TRACE_ATTR   // occupancy experiments: -DRTG_TRACE_ATTR='__attribute__((amdgpu_waves_per_eu(5)))'
-#endif
-#ifndef RTG_SHADOW_ATTR  // 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
+// k_shadow: 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
-#endif
-#ifndef RTG_SHADE_ATTR   // k_shade: the full variant (textures / BRDFs / area & environment lights) needs
-                         // > 256 registers; capped at 2 waves per SIMD it spills 236 B/lane and is
-                         // still faster (cornell_dynamic 1080p64: 34.0 -> 29.7 ms); the simple
-                         // variants already fit 4 waves (no-op for them)
+// k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
+// capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
+// 34.0 -> 29.7 ms); the simple variants already fit 4 waves (no-op for them)
 #define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
-#endif
-// Non-temporal hints on the queue records (measured on the 1080p64 dragon, 2 runs each, and
-// left off: frame time within ±0.2 ms noise of 47.7 ms — the node / triangle working set stays
-// in L2 + MALL either way)
-#ifndef RTG_NT_RECORDS     // 1: queue-record loads ahead of a traversal are non-temporal
-#define RTG_NT_RECORDS 0
-#endif
-#ifndef RTG_NT_STORES      // 1: k_shade's queue-record stores are non-temporal
-#define RTG_NT_STORES 0
-#endif
-#ifndef RTG_PT_SHADE_ATTR  // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168
-                           // VGPRs, 64 B/lane spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves
-                           // (236 B spill) is slower (594 ms); the full variants keep the default
+// k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
+// spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); the full
+// variants keep the default
 #define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? 3 : 1)))
-#endif
-#ifndef RTG_PACKET        // 1: wave-packet walk of the 4-wide tree (scalar node loads, one stack per wave)
-#define RTG_PACKET 0
-#endif
-#ifndef RTG_SHADOW_ANY    // 1: certified early exit for blocked shadow queries (closest_hit ANY).  Off: on
-#define RTG_SHADOW_ANY 0  // dragon1m it saves 5% of the steps but costs 12 VGPRs (35.3 vs 32.6 ms);
-                          // cornell_pt with object-light (mode 3) certification: 629 vs 553 ms
-#endif
 constexpr double PI_D = 3.14159265358979323846;
 
 // ------------------------------------------------------------------ vectors (Eigen order)
@@ -286,40 +260,25 @@ DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d
     d2 = xform(T.inv, d, 0.0f);
 }
 
-// steps: node steps of this lane; iters: loop iterations its wave ran for it (packet walk:
-// one per node the packet visits; per-lane walk: = steps, the wave runs max over lanes)
-struct Stats { unsigned nodes, tris, steps, iters; };
+// steps: node steps of this lane (the wave runs the max over its lanes)
+struct Stats { unsigned nodes, tris, steps; };
 
 // ------------------------------------------------------------------ closest hit
-// BVHMethods::FindIntersection (src/Helper.cpp:72-134) with the per-object nearest
+// BVHMethods::FindIntersection (src/Helper.cpp:18-80) with the per-object nearest
 // candidate of BVH::FindIntersectionWithBVH (src/BVH.cpp:137-210).  The reference visits
 // both children of every node whose box the infinite line crosses; its result is the
 // candidate of minimal Euclidean distance, ties -> rightmost leaf, then lowest index in
 // the leaf.  This ordered traversal computes the same total order and prunes subtrees
 // whose distance lower bound exceeds the current best (EXHAUSTIVE disables pruning).
 // `tmax`: hits with gett() >= tmax are irrelevant to the caller (shadow queries).
-//
-// ANY (shadow queries): `t_cert` > 0 is a parameter bound such that any object whose winning
-// candidate has 0 < gett() <= t_cert already decides the query as blocked (k_shadow derives it
-// from the light distance with rounding margins).  Inside a mesh, once a candidate c with
-// t_c (1 + 1e-4) <= t_cert is accepted, the object's winner has distance <= |c| and hence
-// t <= t_cert; the only way the object could still contribute nothing is a winner behind the
-// origin (gett <= 0, the src/BVH.cpp:159-173 quirk), which needs t <= t0w.  So the rest of
-// the object is walked with the window shrunk to [tlo, t0w]; if the winner seen then has
-// gett > 0 the query returns blocked (out.pad = 1), otherwise the object is walked again
-// without certification (exact closest-hit semantics).
-template <bool EXHAUSTIVE, bool STATS, bool ANY = false>
-DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride,
-                       int* wst_node, unsigned long long* wst_mask, Stats& st, float t_cert = 0.0f) {
+template <bool EXHAUSTIVE, bool STATS>
+DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
     float nearest = tmax;
     const float eps = sv.int_eps;
     for (int i = 0; i < sv.num_tops; i++) {
-#ifdef RTG_DBG_ONLYOBJ
-        if (i != RTG_DBG_ONLYOBJ) continue;
-#endif
         const TopObject& T = sv.tops[i];
         const Geometry& g = sv.geoms[T.geom];
         f3 o2, d2;
@@ -361,402 +320,238 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     if (!(boundD == boundD)) boundD = FLT_MAX;
                 }
             }
-            // gett() of a candidate with t <= t0w may come out <= 0 (error of p = o + d t in the
-            // first nonzero direction component); certification needs this to be excluded.
-            const float t0w = (8.0f * 5.9604645e-8f) * fabsf(oa) / fabsf(da) + 1e-30f;
-            bool allow_cert = ANY && t_cert > 0.0f && da != 0.0f && t0w < INFINITY;
-            for (;;) {
-                bool cert = false;
-                found = false; bprim = -1; bp = mk(0, 0, 0);
-                const float pad = g.prune_pad;
-                float best_d = FLT_MAX;
-                int best_leaf = -1;
-                // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
-                // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
-                // skipped when its box, expanded by `pad`, meets the line only outside that window.
-                const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
-                const float tlo = -(fabsf(eps) + 1e-6f);
-                const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
-                const float inv_dn = __builtin_amdgcn_rcpf(dnorm);   // 1 ulp: inside the 2e-5 margins of thi
-                float thi = INFINITY;
-                if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
-                const float tm_global = thi;
-                float tcap = tm_global;     // thi never exceeds this (shrinks to t0w once certified)
-                // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
-                auto test_prim = [&](const TriGeom& tg, int k, int start) {
-                    if (STATS) st.tris++;
-                    Cand c = tri_test(tg, o2, d2, eps);
-                    if (c.ok) {
-                        float dist = norm(c.p - o2);
-                        if (dist < FLT_MAX &&
-                            (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
-                            best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
-                            if (!EXHAUSTIVE) thi = fminf(tcap, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                        }
-                        if (ANY && allow_cert && !cert && c.t > 2.0f * t0w && c.t * (1.0f + 1e-4f) <= t_cert) {
-                            cert = true;
-                            tcap = t0w;
-                            thi = fminf(thi, t0w);
-                        }
+            const float pad = g.prune_pad;
+            float best_d = FLT_MAX;
+            int best_leaf = -1;
+            // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
+            // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
+            // skipped when its box, expanded by `pad`, meets the line only outside that window.
+            const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
+            const float tlo = -(fabsf(eps) + 1e-6f);
+            const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+            const float inv_dn = __builtin_amdgcn_rcpf(dnorm);   // 1 ulp: inside the 2e-5 margins of thi
+            float thi = INFINITY;
+            if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
+            const float thi0 = thi;     // thi never exceeds the window of the best hit so far
+            // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
+            auto test_prim = [&](const TriGeom& tg, int k, int start) {
+                if (STATS) st.tris++;
+                Cand c = tri_test(tg, o2, d2, eps);
+                if (c.ok) {
+                    float dist = norm(c.p - o2);
+                    if (dist < FLT_MAX &&
+                        (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
+                        best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                        if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                     }
-                };
-                // one child box: reachability (interior, exact predicate) + window pruning + entry key
-                auto child = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool interior,
-                                 float& key) -> bool {
-                    key = 0.0f;
-                    if (!EXHAUSTIVE && fast) {
-                        float ax = (mnx - o2.x) * inv.x, bx = (mxx - o2.x) * inv.x;
-                        float ay = (mny - o2.y) * inv.y, by = (mxy - o2.y) * inv.y;
-                        float az = (mnz - o2.z) * inv.z, bz = (mxz - o2.z) * inv.z;
-                        float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                        float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                        float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                        float lo = le - e - padt, hi = sl + e + padt;
-                        key = lo;
-                        if (hi < lo || hi < tlo || lo > thi) return false;
-                        if (!interior) return true;
-                        if (sl < le - e) return false;
-                        if (sl >= le + e) return true;
-                        return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
-                    }
-                    if (!interior) return true;
-                    return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
-                };
-                if (g.node_base < 0) {
-                    for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
-                        test_prim(sv.tris[k], k, g.root_leaf_start);
-                } else {                // root box already hit (root_ok)
-                    // Leaf children are resolved as soon as they are reached.
-                    auto leaf = [&](int start, int count) {
-#ifndef RTG_DBG_NOLEAF
-                        for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
-#endif
-                    };
-                    // BVH2 walk (ordered, pruned): the reference tree node by node.
-                    auto walk2 = [&]() {
-                        int sp = 0;
-                        int cur = g.node_base;
-                        while (true) {
-                            if (STATS) { st.nodes += 2; st.steps++; }   // one 64-B node = two 32-B child records
-                            const Node nd = sv.nodes[cur];
-                            const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
-                            float lk = 0.0f, rk = 0.0f;
-                            bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
-                            bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
-                            bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
-                            if (lleaf && rleaf && rk < lk) {
-                                leaf(rref, rcnt);
-                                if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
-                                lok = rok = false;
-                            } else {
-                                if (lleaf) { leaf(lref, lcnt); lok = false; }
-                                if (rleaf) {
-                                    if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
-                                    rok = false;
-                                }
-                            }
-                            if (!EXHAUSTIVE) {
-                                lok = lok && !(lk > thi);
-                                rok = rok && !(rk > thi);
-                            }
-                            if (lok && rok) {
-                                int nearc = lref, farc = rref;
-                                if (rk < lk) { nearc = rref; farc = lref; }
-                                stack[sp * sstride] = farc;
-                                sp++;
-                                cur = nearc;
-                            } else if (lok) {
-                                cur = lref;
-                            } else if (rok) {
-                                cur = rref;
-                            } else {
-                                if (sp == 0) break;
-                                sp--;
-                                cur = stack[sp * sstride];
-                            }
-                        }
-                    };
-#if RTG_BVH4
-                    // 4-wide walk over the collapsed tree (fast reciprocal path only; exhaustive
-                    // traversal and rays with a zero / denormal / huge direction component use the
-                    // exact BVH2 walk).  Slots of a collapsed child c need c's box hit too.  The
-                    // exact slab predicate is monotone under box containment here (no zero direction
-                    // component), so a slot whose own box -- or whose pair sibling's box -- is
-                    // certainly hit implies c's hit; interior slots are themselves box-tested; only a
-                    // leaf slot without such a witness tests the pair union (= c's range box)
-                    // explicitly.  A stack that would overflow (> kStackDepth entries: up to 3
-                    // pushes per level) restarts the object on the BVH2 walk, whose depth bound
-                    // fits; candidates already found stay valid.
-                    bool use2 = EXHAUSTIVE || !fast;
-#if RTG_PACKET
-                    // Packet walk: the wave traverses the collapsed tree together.  Rays of one wave
-                    // are the samples of one pixel (or of an 8x8 tile at 1 spp), so they visit nearly
-                    // the same nodes: the node index and its 128-B record are wave-uniform (scalar
-                    // loads into SGPRs), the stack is one per wave (LDS), and every lane applies its
-                    // own exact box predicate and parameter window -- a child is pushed with the mask
-                    // of the lanes that reach it, a leaf is tested by the lanes that reach it.  Each
-                    // lane therefore tests exactly the leaves the per-ray walk would reach (minus
-                    // window-pruned ones), and the result is order independent.
-                    {
-                        const unsigned long long pk = __ballot(!use2);
-                        if (pk) {
-                            const int lane = __lane_id();
-                            int psp = 0;
-                            int cur = __builtin_amdgcn_readfirstlane(g.node4_base);
-                            unsigned long long m = pk;
-                            while (true) {
-                                const bool in = (m >> lane) & 1ull;
-                                if (STATS) st.iters++;
-                                if (STATS && in) { st.nodes += 4; st.steps++; }
-                                const Node4 nd = sv.nodes4[cur];
-                                const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
-                                const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
-                                const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
-                                const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
-                                const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
-                                const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
-                                const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
-                                const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
-                                float key[4];
-                                int okm = 0, surem = 0, gate_mask = 0;
-#pragma unroll
-                                for (int j = 0; j < 4; j++) {
-                                    const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
-                                    const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
-                                    const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
-                                    const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                                    const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                                    const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                                    const float lo = le - e - padt, hi = sl + e + padt;
-                                    key[j] = lo;
-                                    const bool valid = inf[j] >= 0;
-                                    const bool isleaf = (inf[j] & kSlotCount) != 0;
-                                    const bool win = !(hi < lo || hi < tlo || lo > thi);
-                                    const bool miss = sl < le - e;
-                                    const bool sure = sl >= le + e;
-                                    const bool ok = in & valid & win & (isleaf | !miss);
-                                    okm |= ok << j;
-                                    surem |= sure << j;
-                                    gate_mask |= (ok & !isleaf & !sure) << j;
-                                }
-                                while (gate_mask) {          // exact tests of uncertain interior slots (rare)
-                                    const int j = __builtin_ctz(gate_mask);
-                                    gate_mask &= gate_mask - 1;
-                                    const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
-                                    const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
-                                    const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
-                                    const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
-                                    const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
-                                    const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
-                                    if (box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2)) surem |= 1 << j;
-                                    else okm &= ~(1 << j);
-                                }
-#pragma unroll
-                                for (int q = 0; q < 4; q += 2) {   // collapsed-child gates (pair union box)
-                                    const int g0 = inf[q], g1 = inf[q + 1];
-                                    const bool gated = ((g0 >= 0) & ((g0 & kSlotGate) != 0)) | ((g1 >= 0) & ((g1 & kSlotGate) != 0));
-                                    const int lm = (((g0 & kSlotCount) != 0) & (g0 >= 0)) | ((((g1 & kSlotCount) != 0) & (g1 >= 0)) << 1);
-                                    const int pm = 3 << q;
-                                    if (gated && (okm & (lm << q)) && !(surem & pm)) {
-                                        const bool b0 = g0 >= 0, b1 = g1 >= 0;
-                                        const float ux = b0 && b1 ? fminf(lx[q], lx[q + 1]) : (b0 ? lx[q] : lx[q + 1]);
-                                        const float uy = b0 && b1 ? fminf(ly[q], ly[q + 1]) : (b0 ? ly[q] : ly[q + 1]);
-                                        const float uz = b0 && b1 ? fminf(lz[q], lz[q + 1]) : (b0 ? lz[q] : lz[q + 1]);
-                                        const float vx = b0 && b1 ? fmaxf(hx[q], hx[q + 1]) : (b0 ? hx[q] : hx[q + 1]);
-                                        const float vy = b0 && b1 ? fmaxf(hy[q], hy[q + 1]) : (b0 ? hy[q] : hy[q + 1]);
-                                        const float vz = b0 && b1 ? fmaxf(hz[q], hz[q + 1]) : (b0 ? hz[q] : hz[q + 1]);
-                                        if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) okm &= ~pm;
-                                    }
-                                }
-                                // leaf slots: the lanes that reach them (and whose window still admits
-                                // them) test the primitives; the triangle records are wave-uniform
-#pragma unroll
-                                for (int j = 0; j < 4; j++) {
-                                    const int cnt = inf[j] & kSlotCount;
-                                    if (inf[j] < 0 || cnt == 0) continue;
-                                    const bool me = ((okm >> j) & 1) && !(key[j] > thi);
-                                    if (!__ballot(me)) continue;
-                                    const int start = rf[j];
-                                    for (int k = start; k < start + cnt; k++) {
-                                        const TriGeom tg = sv.tris[k];
-                                        if (me) test_prim(tg, k, start);
-                                    }
-                                }
-                                // interior slots: masks of the lanes that reach them (window-pruned),
-                                // ordered by the entry key of their first lane, pushed far first
-                                float k4[4];
-                                int r4[4];
-                                unsigned long long m4[4];
-#pragma unroll
-                                for (int j = 0; j < 4; j++) {
-                                    const bool interior = inf[j] >= 0 && (inf[j] & kSlotCount) == 0;
-                                    const bool me = ((okm >> j) & 1) && !(key[j] > thi);
-                                    const unsigned long long mj = interior ? __ballot(me) : 0ull;
-                                    m4[j] = mj;
-                                    r4[j] = rf[j];
-                                    k4[j] = mj ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                                                     __builtin_bit_cast(int, key[j]), (int)__builtin_ctzll(mj)))
-                                               : INFINITY;
-                                }
-                                auto ce = [&](int a, int b) {
-                                    const bool sw = k4[b] < k4[a] || (m4[a] == 0ull && m4[b] != 0ull);
-                                    const float ka = k4[a], kb = k4[b];
-                                    const int ra = r4[a], rb = r4[b];
-                                    const unsigned long long ma = m4[a], mb = m4[b];
-                                    k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
-                                    r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
-                                    m4[a] = sw ? mb : ma; m4[b] = sw ? ma : mb;
-                                };
-                                ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-#pragma unroll
-                                for (int j = 3; j >= 1; j--)
-                                    if (m4[j]) { wst_node[psp] = r4[j]; wst_mask[psp] = m4[j]; psp++; }
-                                if (m4[0]) {
-                                    cur = r4[0];
-                                    m = m4[0];
-                                } else {
-                                    if (psp == 0) break;
-                                    psp--;
-                                    cur = __builtin_amdgcn_readfirstlane(wst_node[psp]);
-                                    m = wst_mask[psp];
-                                    m = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
-                                        (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
-                                }
-                            }
-                        }
-                    }
-#else
-                    if (!use2) {
-                        int sp = 0;
-                        int cur = g.node4_base;
-                        while (true) {
-                            if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
-                            const Node4 nd = sv.nodes4[cur];
-                            const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
-                            const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
-                            const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
-                            const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
-                            const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
-                            const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
-                            const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
-                            const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
-                            // branch-free slot tests: ok (reachable and inside the window), sure (box
-                            // certainly hit), gate (interior slot in the uncertain band)
-                            float key[4];
-                            int okm = 0, surem = 0, gate_mask = 0, leafm = 0;
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
-                                const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
-                                const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
-                                const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                                const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                                const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                                const float lo = le - e - padt, hi = sl + e + padt;
-                                key[j] = lo;
-                                const bool valid = inf[j] >= 0;
-                                const bool isleaf = (inf[j] & kSlotCount) != 0;
-                                const bool win = !(hi < lo || hi < tlo || lo > thi);
-                                const bool miss = sl < le - e;
-                                const bool sure = sl >= le + e;
-                                const bool ok = valid & win & (isleaf | !miss);
-                                okm |= ok << j;
-                                surem |= sure << j;
-                                gate_mask |= (ok & !isleaf & !sure) << j;
-                                leafm |= (valid & isleaf) << j;
-                            }
-                            // own exact tests of uncertain interior slots (rare)
-                            while (gate_mask) {
-                                const int j = __builtin_ctz(gate_mask);
-                                gate_mask &= gate_mask - 1;
-                                const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
-                                const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
-                                const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
-                                const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
-                                const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
-                                const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
-                                if (box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2)) surem |= 1 << j;
-                                else okm &= ~(1 << j);
-                            }
-                            // collapsed-child gates (pair union box), once per pair: needed only for a
-                            // reachable leaf slot when neither slot of the pair is certainly hit
-#pragma unroll
-                            for (int q = 0; q < 4; q += 2) {
-                                const int g0 = inf[q], g1 = inf[q + 1];
-                                const bool gated = ((g0 >= 0) & ((g0 & kSlotGate) != 0)) | ((g1 >= 0) & ((g1 & kSlotGate) != 0));
-                                const int pm = 3 << q;
-                                if (gated && (okm & leafm & pm) && !(surem & pm)) {
-                                    const bool b0 = g0 >= 0, b1 = g1 >= 0;
-                                    const float ux = b0 && b1 ? fminf(lx[q], lx[q + 1]) : (b0 ? lx[q] : lx[q + 1]);
-                                    const float uy = b0 && b1 ? fminf(ly[q], ly[q + 1]) : (b0 ? ly[q] : ly[q + 1]);
-                                    const float uz = b0 && b1 ? fminf(lz[q], lz[q + 1]) : (b0 ? lz[q] : lz[q + 1]);
-                                    const float vx = b0 && b1 ? fmaxf(hx[q], hx[q + 1]) : (b0 ? hx[q] : hx[q + 1]);
-                                    const float vy = b0 && b1 ? fmaxf(hy[q], hy[q + 1]) : (b0 ? hy[q] : hy[q + 1]);
-                                    const float vz = b0 && b1 ? fmaxf(hz[q], hz[q + 1]) : (b0 ? hz[q] : hz[q + 1]);
-                                    if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) okm &= ~pm;
-                                }
-                            }
-                            // interior candidates first, so the node's boxes are dead during leaf tests
-                            float k4[4];
-                            int r4[4];
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const bool take = ((okm >> j) & 1) && !((leafm >> j) & 1);
-                                k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
-                                r4[j] = take ? rf[j] : -1;
-                            }
-                            int leaf_mask = okm & leafm;
-                            // leaves now, one code site (thi may shrink between them)
-                            while (leaf_mask) {
-                                const int j = __builtin_ctz(leaf_mask);
-                                leaf_mask &= leaf_mask - 1;
-                                const float kj = j == 0 ? key[0] : j == 1 ? key[1] : j == 2 ? key[2] : key[3];
-                                if (kj > thi) continue;
-                                const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
-                                const int info = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
-                                leaf(start, info & kSlotCount);
-                            }
-#pragma unroll
-                            for (int j = 0; j < 4; j++)
-                                if (k4[j] > thi) { k4[j] = INFINITY; r4[j] = -1; }
-                            // interior slots, nearest first: sort (key, ref), push the others farthest first
-                            auto ce = [&](int a, int b) {
-                                const bool sw = k4[b] < k4[a];
-                                const float ka = k4[a], kb = k4[b];
-                                const int ra = r4[a], rb = r4[b];
-                                k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
-                                r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
-                            };
-                            ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-                            const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
-                            if (sp + npush > kStackDepth) { use2 = true; break; }
-                            if (r4[3] >= 0) { stack[sp * sstride] = r4[3]; sp++; }
-                            if (r4[2] >= 0) { stack[sp * sstride] = r4[2]; sp++; }
-                            if (r4[1] >= 0) { stack[sp * sstride] = r4[1]; sp++; }
-                            if (r4[0] >= 0) {
-                                cur = r4[0];
-                            } else {
-                                if (sp == 0) break;
-                                sp--;
-                                cur = stack[sp * sstride];
-                            }
-                        }
-                    }
-#endif
-                    if (use2) walk2();
-#else
-                    walk2();
-#endif
                 }
-                if (!(ANY && cert)) break;
-                const float tw = gett(o2, d2, bp);
-                if (tw > 0) { out.obj = i; out.prim = bprim; out.t = tw; out.pad = 1; return out; }
-                allow_cert = false;     // winner behind the origin: walk the object again, exactly
+            };
+            // one child box: reachability (interior, exact predicate) + window pruning + entry key
+            auto child = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool interior,
+                             float& key) -> bool {
+                key = 0.0f;
+                if (!EXHAUSTIVE && fast) {
+                    float ax = (mnx - o2.x) * inv.x, bx = (mxx - o2.x) * inv.x;
+                    float ay = (mny - o2.y) * inv.y, by = (mxy - o2.y) * inv.y;
+                    float az = (mnz - o2.z) * inv.z, bz = (mxz - o2.z) * inv.z;
+                    float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                    float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                    float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                    float lo = le - e - padt, hi = sl + e + padt;
+                    key = lo;
+                    if (hi < lo || hi < tlo || lo > thi) return false;
+                    if (!interior) return true;
+                    if (sl < le - e) return false;
+                    if (sl >= le + e) return true;
+                    return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+                }
+                if (!interior) return true;
+                return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+            };
+            if (g.node_base < 0) {
+                for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
+                    test_prim(sv.tris[k], k, g.root_leaf_start);
+            } else {                // root box already hit (root_ok)
+                // Leaf children are resolved as soon as they are reached.
+                auto leaf = [&](int start, int count) {
+                    for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
+                };
+                // BVH2 walk (ordered, pruned): the reference tree node by node.
+                auto walk2 = [&]() {
+                    int sp = 0;
+                    int cur = g.node_base;
+                    while (true) {
+                        if (STATS) { st.nodes += 2; st.steps++; }   // one 64-B node = two 32-B child records
+                        const Node nd = sv.nodes[cur];
+                        const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
+                        float lk = 0.0f, rk = 0.0f;
+                        bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
+                        bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
+                        bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
+                        if (lleaf && rleaf && rk < lk) {
+                            leaf(rref, rcnt);
+                            if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
+                            lok = rok = false;
+                        } else {
+                            if (lleaf) { leaf(lref, lcnt); lok = false; }
+                            if (rleaf) {
+                                if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
+                                rok = false;
+                            }
+                        }
+                        if (!EXHAUSTIVE) {
+                            lok = lok && !(lk > thi);
+                            rok = rok && !(rk > thi);
+                        }
+                        if (lok && rok) {
+                            int nearc = lref, farc = rref;
+                            if (rk < lk) { nearc = rref; farc = lref; }
+                            stack[sp * sstride] = farc;
+                            sp++;
+                            cur = nearc;
+                        } else if (lok) {
+                            cur = lref;
+                        } else if (rok) {
+                            cur = rref;
+                        } else {
+                            if (sp == 0) break;
+                            sp--;
+                            cur = stack[sp * sstride];
+                        }
+                    }
+                };
+                // 4-wide walk over the collapsed tree (fast reciprocal path only; exhaustive
+                // traversal and rays with a zero / denormal / huge direction component use the
+                // exact BVH2 walk).  Slots of a collapsed child c need c's box hit too.  The
+                // exact slab predicate is monotone under box containment here (no zero direction
+                // component), so a slot whose own box -- or whose pair sibling's box -- is
+                // certainly hit implies c's hit; interior slots are themselves box-tested; only a
+                // leaf slot without such a witness tests the pair union (= c's range box)
+                // explicitly.  A stack that would overflow (> kStackDepth entries: up to 3
+                // pushes per level) restarts the object on the BVH2 walk, whose depth bound
+                // fits; candidates already found stay valid.
+                bool use2 = EXHAUSTIVE || !fast;
+                if (!use2) {
+                    int sp = 0;
+                    int cur = g.node4_base;
+                    while (true) {
+                        if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
+                        const Node4 nd = sv.nodes4[cur];
+                        const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
+                        const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
+                        const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
+                        const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
+                        const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
+                        const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
+                        const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
+                        const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
+                        // branch-free slot tests: ok (reachable and inside the window), sure (box
+                        // certainly hit), gate (interior slot in the uncertain band)
+                        float key[4];
+                        int okm = 0, surem = 0, gate_mask = 0, leafm = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
+                            const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
+                            const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
+                            const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                            const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                            const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                            const float lo = le - e - padt, hi = sl + e + padt;
+                            key[j] = lo;
+                            const bool valid = inf[j] >= 0;
+                            const bool isleaf = (inf[j] & kSlotCount) != 0;
+                            const bool win = !(hi < lo || hi < tlo || lo > thi);
+                            const bool miss = sl < le - e;
+                            const bool sure = sl >= le + e;
+                            const bool ok = valid & win & (isleaf | !miss);
+                            okm |= ok << j;
+                            surem |= sure << j;
+                            gate_mask |= (ok & !isleaf & !sure) << j;
+                            leafm |= (valid & isleaf) << j;
+                        }
+                        // own exact tests of uncertain interior slots (rare)
+                        while (gate_mask) {
+                            const int j = __builtin_ctz(gate_mask);
+                            gate_mask &= gate_mask - 1;
+                            const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
+                            const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
+                            const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
+                            const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
+                            const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
+                            const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
+                            if (box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2)) surem |= 1 << j;
+                            else okm &= ~(1 << j);
+                        }
+                        // collapsed-child gates (pair union box), once per pair: needed only for a
+                        // reachable leaf slot when neither slot of the pair is certainly hit
+#pragma unroll
+                        for (int q = 0; q < 4; q += 2) {
+                            const int g0 = inf[q], g1 = inf[q + 1];
+                            const bool gated = ((g0 >= 0) & ((g0 & kSlotGate) != 0)) | ((g1 >= 0) & ((g1 & kSlotGate) != 0));
+                            const int pm = 3 << q;
+                            if (gated && (okm & leafm & pm) && !(surem & pm)) {
+                                const bool b0 = g0 >= 0, b1 = g1 >= 0;
+                                const float ux = b0 && b1 ? fminf(lx[q], lx[q + 1]) : (b0 ? lx[q] : lx[q + 1]);
+                                const float uy = b0 && b1 ? fminf(ly[q], ly[q + 1]) : (b0 ? ly[q] : ly[q + 1]);
+                                const float uz = b0 && b1 ? fminf(lz[q], lz[q + 1]) : (b0 ? lz[q] : lz[q + 1]);
+                                const float vx = b0 && b1 ? fmaxf(hx[q], hx[q + 1]) : (b0 ? hx[q] : hx[q + 1]);
+                                const float vy = b0 && b1 ? fmaxf(hy[q], hy[q + 1]) : (b0 ? hy[q] : hy[q + 1]);
+                                const float vz = b0 && b1 ? fmaxf(hz[q], hz[q + 1]) : (b0 ? hz[q] : hz[q + 1]);
+                                if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) okm &= ~pm;
+                            }
+                        }
+                        // interior candidates first, so the node's boxes are dead during leaf tests
+                        float k4[4];
+                        int r4[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const bool take = ((okm >> j) & 1) && !((leafm >> j) & 1);
+                            k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
+                            r4[j] = take ? rf[j] : -1;
+                        }
+                        int leaf_mask = okm & leafm;
+                        // leaves now, one code site (thi may shrink between them)
+                        while (leaf_mask) {
+                            const int j = __builtin_ctz(leaf_mask);
+                            leaf_mask &= leaf_mask - 1;
+                            const float kj = j == 0 ? key[0] : j == 1 ? key[1] : j == 2 ? key[2] : key[3];
+                            if (kj > thi) continue;
+                            const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
+                            const int info = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
+                            leaf(start, info & kSlotCount);
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (k4[j] > thi) { k4[j] = INFINITY; r4[j] = -1; }
+                        // interior slots, nearest first: sort (key, ref), push the others farthest first
+                        auto ce = [&](int a, int b) {
+                            const bool sw = k4[b] < k4[a];
+                            const float ka = k4[a], kb = k4[b];
+                            const int ra = r4[a], rb = r4[b];
+                            k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
+                            r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
+                        };
+                        ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+                        const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
+                        if (sp + npush > kStackDepth) { use2 = true; break; }
+                        if (r4[3] >= 0) { stack[sp * sstride] = r4[3]; sp++; }
+                        if (r4[2] >= 0) { stack[sp * sstride] = r4[2]; sp++; }
+                        if (r4[1] >= 0) { stack[sp * sstride] = r4[1]; sp++; }
+                        if (r4[0] >= 0) {
+                            cur = r4[0];
+                        } else {
+                            if (sp == 0) break;
+                            sp--;
+                            cur = stack[sp * sstride];
+                        }
+                    }
+                }
+                if (use2) walk2();
             }
         }
         if (found) {
             float t = gett(o2, d2, bp);
-            if (ANY && t > 0 && t <= t_cert) { out.obj = i; out.prim = bprim; out.t = t; out.pad = 1; return out; }
             if (t < nearest && t > 0) {
                 nearest = t;
                 out.obj = i; out.prim = bprim; out.t = t;
@@ -1375,27 +1170,6 @@ DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int
 // Render-path hit records: k_shade / k_pt_shade rebuild the hit from (object, primitive) alone
 // (hit_record re-runs the winning test), so the wavefront stores 8 bytes per ray, not the
 // 16-byte HitRec the rtg_trace_closest path returns.
-DEV float4 ld_rec(const float4* p) {
-    if (RTG_NT_RECORDS) {
-        const float* q = reinterpret_cast<const float*>(p);
-        return make_float4(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1),
-                           __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3));
-    }
-    return *p;
-}
-DEV void st_rec(float4* p, float4 v) {
-    if (RTG_NT_STORES) {
-        float* q = reinterpret_cast<float*>(p);
-        __builtin_nontemporal_store(v.x, q); __builtin_nontemporal_store(v.y, q + 1);
-        __builtin_nontemporal_store(v.z, q + 2); __builtin_nontemporal_store(v.w, q + 3);
-    } else {
-        *p = v;
-    }
-}
-DEV void st_rec(int4* p, int4 v) {
-    st_rec(reinterpret_cast<float4*>(p), make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z),
-                                                     __int_as_float(v.w)));
-}
 DEV void store_hit_compact(HitRec* hits, int i, const HitRec& h) {
     reinterpret_cast<int2*>(hits)[i] = make_int2(h.obj, h.prim);
 }
@@ -1408,15 +1182,13 @@ DEV HitRec load_hit_compact(const HitRec* hits, int i) {
 
 // GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no RayRec buffer).
 template <bool EXHAUSTIVE, bool STATS, bool GEN = false>
-__global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayRec* __restrict__ rays,
+__global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayRec* __restrict__ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
                                                        const CameraDev cam, const PassDev ps, uint64_t seed,
                                                        bool compact) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
-    __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
-    __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Stats st = {0, 0, 0, 0};
+    Stats st = {0, 0, 0};
     if (i < n) {
         f3 o, d;
         float time, tmax;
@@ -1424,19 +1196,17 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
             primary_ray(cam, ps, seed, i, o, d, time);
             tmax = FLT_MAX;
         } else {
-            RayRec r;
-            r.o_t = ld_rec(&rays[i].o_t); r.d = ld_rec(&rays[i].d);
+            const RayRec r = rays[i];
             o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
             time = r.o_t.w; tmax = r.d.w;
         }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock,
-                                                  s_wnode[threadIdx.x >> 6], s_wmask[threadIdx.x >> 6], st);
+        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st);
         if (compact) store_hit_compact(hits, i, h);
         else hits[i] = h;
     }
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
-        unsigned mx = RTG_PACKET ? st.iters : st.steps;
+        unsigned mx = st.steps;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
@@ -1450,21 +1220,6 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
             atomicAdd(&ctr->trace_steps, ns);
         }
     }
-}
-
-// Wave-aggregated append of 0..2 records per lane (ballot + mbcnt prefix, one atomic per wave).
-DEV int wave_append(int cnt, unsigned* counter) {
-    unsigned long long m1 = __ballot(cnt >= 1);
-    unsigned long long m2 = __ballot(cnt >= 2);
-    unsigned long long lt = __lanemask_lt();
-    int off = __popcll(m1 & lt) + __popcll(m2 & lt);
-    int total = __popcll(m1) + __popcll(m2);
-    int base = 0;
-    int lane = __lane_id();
-    int leader = __ffsll((long long)__ballot(1)) - 1;
-    if (lane == leader && total > 0) base = (int)atomicAdd(counter, (unsigned)total);
-    base = __shfl(base, leader);
-    return base + off;
 }
 
 DEV RayRec make_ray(f3 o, f3 d, float time) {
@@ -1627,9 +1382,9 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                         // every record when there are several)
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
                             const size_t k = (size_t)i * sv.num_lights + li;
-                            st_rec(shadows.o + k, sr.o);
-                            st_rec(shadows.c + k, sr.c);
-                            if (!sv.lean_shadow) { st_rec(shadows.d + k, sr.d); st_rec(shadows.L + k, sr.L); }
+                            shadows.o[k] = sr.o;
+                            shadows.c[k] = sr.c;
+                            if (!sv.lean_shadow) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
                         }
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
@@ -1668,16 +1423,14 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     int idx = (int)((unsigned)s_base + s_wc[w] + coff);
     if (i < n) {
         auto put_ray = [&](int k, const RayRec& rr, const RayMeta& mm) {
-            st_rec(&next_rays[k].o_t, rr.o_t);
-            st_rec(&next_rays[k].d, rr.d);
-            if (!sv.meta_free) st_rec(reinterpret_cast<int4*>(next_meta + k), make_int4(mm.slot, (int)mm.path_lo,
-                                                                                         (int)mm.path_hi, mm.depth));
+            next_rays[k] = rr;
+            if (!sv.meta_free) next_meta[k] = mm;
         };
         if (has0) { put_ray(idx, c0r, c0m); nd.child0 = idx; idx++; }
         if (has1) { put_ray(idx, c1r, c1m); nd.child1 = idx; }
-        st_rec(nodes.col + i, make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind | (hit ? kNodeHit : 0))));
-        if (hit) st_rec(nodes.pnt + i, make_float4(nd.px, nd.py, nd.pz, nd.F));
-        if ((nd.kind & 0xFF) != NK_FINAL) st_rec(nodes.link + i, make_int4(nd.child0, nd.child1, nd.material, 0));
+        nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind | (hit ? kNodeHit : 0)));
+        if (hit) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
+        if ((nd.kind & 0xFF) != NK_FINAL) nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, 0);
     }
     unsigned sb = (unsigned)(s_base >> 32) + s_ws[w];
     for (int li = 0; li < sv.num_lights; li++) {
@@ -1938,29 +1691,26 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const
     }
 }
 
-// Shadow queries + in-order light sum of Scene::BasicShading (src/Scene.cpp:374-398).
+// Shadow queries + in-order light sum of Scene::BasicShading (src/Scene.cpp:243-267).
 // One thread per traced shadow query (compacted by k_shade).  With one light the result is
-// added to the node colour here (col + c or col + 0, as Scene::RecursiveShading's light loop
+// added to the node colour here (col + c or col + 0, as Scene::BasicShading's light loop
 // does); with several, the visibility is recorded and k_light_sum adds them in light order.
+// Each query is a full closest-hit FindIntersection, as Light::IsShadow does
+// (src/Light.cpp:188-205): the distance test below decides blocking.
 template <bool EXHAUSTIVE, bool STATS>
 __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const SceneView sv,
                                                                        const ShadowPlanes shadows, bool lean,
                                                                        const int* __restrict__ slist,
-                                                                       const unsigned* scount,
-                                                                       float* __restrict__ ncol,
-                                                                       const float* __restrict__ npnt, int nstride,
+                                                                       const unsigned* scount, const NodePlanes nodes,
                                                                        unsigned* nan_queries, Counters* ctr) {
-    // node i's colour at ncol + i * nstride, its hit point at npnt + i * nstride (the NodePlanes
-    // colour / point planes: stride 4 floats)
     __shared__ int s_stack[kStackDepth * kTraceBlock];
-    __shared__ int s_wnode[kTraceBlock / 64][kPacketStack];
-    __shared__ unsigned long long s_wmask[kTraceBlock / 64][kPacketStack];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
-    Stats st = {0, 0, 0, 0};
+    Stats st = {0, 0, 0};
     if (j < (int)*scount) {
         const int idx = slist[j];
-        const float4 so = ld_rec(shadows.o + idx);
+        const int i = idx / sv.num_lights;      // shading node of the query
+        const float4 so = shadows.o[idx];
         const f3 o = mk(so.x, so.y, so.z);
         f3 d;
         float tmax;
@@ -1970,72 +1720,33 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 d = -ld3(L.dir);
                 tmax = FLT_MAX;
             } else {
-                const float4 pf = ld_rec(reinterpret_cast<const float4*>(npnt + (size_t)idx * nstride));
+                const float4 pf = nodes.pnt[i];
                 const f3 p = mk(pf.x, pf.y, pf.z), lp = ld3(L.pos);
                 d = toward(lp, p);
                 tmax = shadow_tmax(o, p, lp, sv.shadow_eps);
             }
         } else {
-            const float4 sd = ld_rec(shadows.d + idx);
+            const float4 sd = shadows.d[idx];
             d = mk(sd.x, sd.y, sd.z);
             tmax = sd.w;
         }
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
-        // Certification bound (closest_hit ANY): for 0 < t <= t_cert the computed
-        // norm(p - (o + d t)) stays below the computed norm(p - L) (the point-light test of
-        // PointLight::IsShadow, src/Light.cpp:188-205): |p - hp| <= |p - o| + t|d| plus rounding
-        // of hp, of the difference and of the norm, all inside the 1e-5 relative margins.
-        // Directional / environment queries are blocked by any hit (t_cert = inf).
-        float t_cert = 0.0f;
-        if (!EXHAUSTIVE && RTG_SHADOW_ANY) {
-            const float4 srL = lean ? make_float4(sv.lights[0].pos[0], sv.lights[0].pos[1], sv.lights[0].pos[2], 0.0f)
-                                    : shadows.L[idx];
-            const float mode = shadows.c[idx].w;
-            const int i = idx / sv.num_lights;
-            const float* pp = npnt + (size_t)i * nstride;
-            const f3 p = mk(pp[0], pp[1], pp[2]);
-            const f3 lp = mk(srL.x, srL.y, srL.z);
-            if (mode == 1.0f) {
-                const float DL = norm(p - lp);
-                const float po = norm(p - o), dn = norm(d);
-                const float S = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(p.x))),
-                                      fmaxf(fabsf(p.y), fabsf(p.z)));
-                const float num = DL * (1.0f - 1e-5f) - 1e-5f * S - po * (1.0f + 1e-5f);
-                if (num > 0.0f && dn > 0.0f) t_cert = num / (dn * (1.0f + 2e-5f));
-                if (!(t_cert < FLT_MAX)) t_cert = 0.0f;
-            } else if (mode == 3.0f) {   // object light: blocked iff |p - hp| < dl - (eps + 1e-4 dl)
-                const float dl = norm(p - lp);
-                const float DL = dl - (sv.shadow_eps + 1e-4f * dl);
-                const float po = norm(p - o), dn = norm(d);
-                const float S = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(p.x))),
-                                      fmaxf(fabsf(p.y), fabsf(p.z)));
-                const float num = DL * (1.0f - 1e-5f) - 1e-5f * S - po * (1.0f + 1e-5f);
-                if (num > 0.0f && dn > 0.0f) t_cert = num / (dn * (1.0f + 2e-5f));
-                if (!(t_cert < FLT_MAX)) t_cert = 0.0f;
-            } else if (mode == 2.0f) {
-                t_cert = INFINITY;
-            }
-        }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, !EXHAUSTIVE && RTG_SHADOW_ANY>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax,
-                                                               s_stack + threadIdx.x, kTraceBlock, s_wnode[threadIdx.x >> 6],
-                                                               s_wmask[threadIdx.x >> 6], st, t_cert);
+        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x,
+                                                  kTraceBlock, st);
         // the query's contribution / mode are re-read rather than kept live across the traversal
         // (register pressure: 128 VGPRs for 4 waves per SIMD)
         const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
         const float4 sc = make_float4(__builtin_nontemporal_load(scp), __builtin_nontemporal_load(scp + 1),
                                       __builtin_nontemporal_load(scp + 2), __builtin_nontemporal_load(scp + 3));
-        const int i = idx / sv.num_lights;
         bool blocked;
-        if (h.pad == 1) {
-            blocked = true;         // certified by closest_hit (ANY)
-        } else if (sc.w == 1.0f || sc.w == 3.0f) {
+        if (sc.w == 1.0f || sc.w == 3.0f) {
             blocked = false;
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
                 auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
                 const float* qo = reinterpret_cast<const float*>(shadows.o + idx);
                 const f3 o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
-                const float* pp = npnt + (size_t)i * nstride;
+                const float* pp = reinterpret_cast<const float*>(nodes.pnt + i);
                 const f3 p_ = mk(ld(pp), ld(pp + 1), ld(pp + 2));
                 f3 d_, l_;
                 if (lean) {     // mode 1 with one light: a point / spot light
@@ -2048,7 +1759,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                     l_ = mk(ld(ql), ld(ql + 1), ld(ql + 2));
                 }
                 f3 hp = o_ + d_ * h.t;
-                if (sc.w == 1.0f) {
+                if (sc.w == 1.0f) {             // PointLight::IsShadow: |p - L| > |p - hit|
                     blocked = norm(p_ - l_) > norm(p_ - hp);
                 } else {   // object light (hw7, Page7.md:143-147): an occluder nearer than the sample
                     const float dl = norm(p_ - l_);
@@ -2056,11 +1767,11 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 }
             }
         } else {
-            blocked = h.obj >= 0;
+            blocked = h.obj >= 0;               // directional / environment: any hit
         }
         if (sv.num_lights == 1) {
             f3 add = blocked ? mk(0, 0, 0) : mk(sc.x, sc.y, sc.z);
-            float* cp = ncol + (size_t)i * nstride;
+            float* cp = reinterpret_cast<float*>(nodes.col + i);
             cp[0] = cp[0] + add.x;
             cp[1] = cp[1] + add.y;
             cp[2] = cp[2] + add.z;
@@ -2073,7 +1784,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     if (nm && (threadIdx.x & 63) == 0) atomicAdd(nan_queries, (unsigned)__popcll(nm));
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
-        unsigned mx = RTG_PACKET ? st.iters : st.steps;
+        unsigned mx = st.steps;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
@@ -2174,9 +1885,9 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodeP
 // order.  mode 2: the single sample itself; 1: first chunk (start from 0); 0: continue the
 // running sum in `acc`.
 constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
-// Colours are read from the level-0 NodePlanes colour plane (ncol, stride 4); `resolve` (Whitted only) evaluates non-final level-0 nodes
-// against level 1 first.
-__global__ void __launch_bounds__(256) k_accumulate(const SceneView sv, const float* __restrict__ ncol, int nstride,
+// Colours are read from the level-0 NodePlanes colour plane; `resolve` (Whitted only) evaluates
+// non-final level-0 nodes against level 1 first.
+__global__ void __launch_bounds__(256) k_accumulate(const SceneView sv,
                                                     const NodePlanes level0, const NodePlanes level1, bool resolve,
                                                     float* __restrict__ acc, const PassDev ps, int nx, int mode) {
     __shared__ float sr[kAccPix * kAccStride], sg[kAccPix * kAccStride], sb[kAccPix * kAccStride];
@@ -2198,16 +1909,11 @@ __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv, const fl
             const int q = e / cs, s = e - q * cs;
             const size_t slot = (size_t)(p0 + q) * ps.ns + s0 + s;
             f3 c;
-            if (nstride == 4) {
-                const float4 nc = level0.col[slot];
-                if (resolve && (__float_as_int(nc.w) & 0xFF) != NK_FINAL)   // level 0 of the bottom-up pass
-                    c = resolve_node(sv, nc, (int)slot, level0, level1);
-                else
-                    c = mk(nc.x, nc.y, nc.z);
-            } else {
-                const float* cp = ncol + slot * nstride;
-                c = mk(cp[0], cp[1], cp[2]);
-            }
+            const float4 nc = level0.col[slot];
+            if (resolve && (__float_as_int(nc.w) & 0xFF) != NK_FINAL)   // level 0 of the bottom-up pass
+                c = resolve_node(sv, nc, (int)slot, level0, level1);
+            else
+                c = mk(nc.x, nc.y, nc.z);
             sr[q * kAccStride + s] = c.x;
             sg[q * kAccStride + s] = c.y;
             sb[q * kAccStride + s] = c.z;
@@ -2310,14 +2016,11 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
     const NodePlanes np = node_planes(nodes, n);
-    float* ncol = reinterpret_cast<float*>(np.col);
-    const float* npnt = reinterpret_cast<const float*>(np.pnt);
-    const int ns = 4;
     const ShadowPlanes sp = shadow_planes(shadows, cap);
     const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, ncol, npnt, ns, nan_queries, ctr);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, ncol, npnt, ns, nan_queries, ctr);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, ncol, npnt, ns, nan_queries, ctr);
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
     if (sv.num_lights > 1 && whitted)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, sp, np, n);
 }
@@ -2356,9 +2059,7 @@ void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec
     NodeRec* l0 = const_cast<NodeRec*>(level0);
     const NodePlanes p0 = node_planes(l0, n0);
     const NodePlanes p1 = (whitted && level1) ? node_planes(const_cast<NodeRec*>(level1), n1) : NodePlanes{};
-    const float* ncol = reinterpret_cast<const float*>(p0.col);
-    const int ns = 4;
-    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, ncol, ns, p0, p1,
+    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, p0, p1,
                        resolve && whitted, acc, ps, nx, mode);
 }
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block,

@@ -14,16 +14,9 @@
 namespace rtg {
 
 constexpr int kMaxLights = 64;      // per-node shadow slots are statically strided
-constexpr int kStackDepth = 32;
-constexpr int kPacketStack = 64;    // wave stack of the packet walk: <= 3 pushes per 4-wide level, <= 16 levels     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
-#ifndef RTG_TRACE_BLOCK
-#define RTG_TRACE_BLOCK 64
-#endif
-constexpr int kTraceBlock = RTG_TRACE_BLOCK;   // threads per traversal block (LDS stack: 128 B per lane)
-#ifndef RTG_SHADE_BLOCK
-#define RTG_SHADE_BLOCK 512
-#endif
-constexpr int kShadeBlock = RTG_SHADE_BLOCK;   // k_shade (simple variants): one queue atomic per block
+constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
+constexpr int kTraceBlock = 64;     // threads per traversal block (LDS stack: 128 B per lane)
+constexpr int kShadeBlock = 512;    // k_shade (simple variants): one queue atomic per block
 
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:86-127):
 // objects first, then instances.  Read with scalar loads (wave-uniform loop).

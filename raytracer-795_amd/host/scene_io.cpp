@@ -1026,21 +1026,23 @@ int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t 
         if (!name || !rgb || nx < 1 || ny < 1) return fail(RTG_ERR_INVALID, "bad image");
         FILE* f = fopen(name, "wb");
         if (!f) return fail(RTG_ERR_INVALID, std::string("cannot write ") + name);
-        if (is_png(name)) {                      // Image::SavePng (src/Image.cpp:222-263): P3 text
+        if (is_png(name)) {                      // Image::SavePng (src/Image.cpp:62-103): P3 text
             fprintf(f, "P3\n%d %d\n255\n", nx, ny);
             std::string row;
             for (int y = 0; y < ny; y++) {
                 row.clear();
                 for (int x = 0; x < nx * 3; x++) {
                     float v = rgb[(size_t)y * nx * 3 + x];
-                    if (v > 255) v = 255;
-                    const int u = (v == v && v > 0) ? ((int)truncf(v) & 0xFF) : 0;
+                    if (v > 255) v = 255;        // src/Image.cpp:64-68
+                    // (unsigned char)_data[i] (src/Image.cpp:96) as x86-64 gcc compiles it: cvttss2si to a
+                    // 32-bit int, low byte kept (-1 -> 255, -300 -> 212); NaN / out-of-range -> 0x80000000 -> 0
+                    const int u = (v >= -2147483648.0f) ? ((int)v & 0xFF) : 0;
                     row += std::to_string(u);
                     row += (x + 1 < nx * 3) ? " " : " \n";
                 }
                 fputs(row.c_str(), f);
             }
-        } else {                                 // ExrLibrary::SaveExr (src/Helper.cpp:415-466): HALF B,G,R
+        } else {                                 // ExrLibrary::SaveExr (src/Helper.cpp:361-412): HALF B,G,R
             std::string h;
             auto i32 = [&](int32_t v) { h.append((const char*)&v, 4); };
             auto attr = [&](const char* n, const char* t, const std::string& data) {

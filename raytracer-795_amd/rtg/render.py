@@ -159,13 +159,16 @@ def _is_png(name: str) -> bool:
 
 
 def ppm_p3_bytes(rgb: np.ndarray) -> bytes:
-    """Image::SavePng (src/Image.cpp:222-263): values > 255 clamped, (unsigned char) cast,
+    """Image::SavePng (src/Image.cpp:62-103): values > 255 clamped, (unsigned char) cast,
     P3 text with a trailing space after every value and a newline per row."""
     h, w, _ = rgb.shape
     v = np.asarray(rgb, np.float32).copy()
     v[v > 255] = 255
-    # (unsigned char)float: truncation toward zero; negative/NaN is UB in C, mapped to 0
-    u8 = np.where(np.isfinite(v) & (v > 0), np.trunc(v), 0).astype(np.int64) & 0xFF
+    # (unsigned char)_data[i] (src/Image.cpp:96) as x86-64 gcc compiles it: cvttss2si to a 32-bit
+    # int (truncation toward zero), low byte kept: -1 -> 255, -255.5 -> 1, -300 -> 212; NaN and
+    # values below -2^31 give 0x80000000 -> 0
+    ok = v >= np.float32(-2147483648.0)
+    u8 = np.where(ok, np.trunc(np.where(ok, v, 0)), 0).astype(np.int64) & 0xFF
     lines = [f"P3\n{w} {h}\n255\n"]
     for y in range(h):
         lines.append(" ".join(str(int(x)) for x in u8[y].reshape(-1)) + " \n")

@@ -122,8 +122,48 @@ def test_ply_quad_split_and_offsets(tmp_path):
 
 def test_image_writers():
     assert _is_png("out.png") and _is_png("a.png.exr") and not _is_png("out.exr")
-    img = np.array([[[300.0, 12.7, -1.0]]], np.float32)
+    img = np.array([[[300.0, 12.7, -0.5]]], np.float32)
     assert ppm_p3_bytes(img) == b"P3\n1 1\n255\n255 12 0 \n"
     exr = exr_half_bytes(np.zeros((2, 3, 3), np.float32))
     assert exr[:4] == b"\x76\x2f\x31\x01"
     assert len(exr) > 2 * 3 * 3 * 2
+
+
+# (unsigned char)_data[i] of src/Image.cpp:96 on x86-64 gcc: cvttss2si to int32, low byte kept
+PPM_CASES = [(-1.0, 255), (-255.5, 1), (-300.0, 212), (-0.5, 0), (-0.0, 0), (float("nan"), 0),
+             (-float("inf"), 0), (float("inf"), 255), (300.0, 255), (12.7, 12), (-3e9, 0),
+             (-2147483648.0, 0), (255.9, 255), (-2147483520.0, 128), (-65535.0, 1)]
+
+
+def test_ppm_negative_pixels_keep_the_low_byte():
+    vals = [v for v, _ in PPM_CASES]
+    img = np.array(vals, np.float32).reshape(1, len(vals) // 3, 3)
+    body = ppm_p3_bytes(img).decode().split("\n")[3].split()
+    assert [int(x) for x in body] == [u for _, u in PPM_CASES]
+
+
+def test_ppm_cast_matches_compiled_x86_cast(tmp_path):
+    """Pin the expected bytes on the host compiler itself: the reference's clamp + cast
+    (src/Image.cpp:64-68, 96) compiled by gcc, fed the same floats."""
+    import shutil
+    import subprocess
+    import platform
+    if shutil.which("gcc") is None or platform.machine() != "x86_64":
+        pytest.skip("needs gcc on x86-64")
+    src = tmp_path / "cast.c"
+    src.write_text("""#include <stdio.h>
+#include <stdlib.h>
+int main(int argc, char** argv) {
+    for (int i = 1; i < argc; i++) {
+        volatile float v = strtof(argv[i], 0);
+        if (v > 255) v = 255;
+        printf("%d ", (unsigned char)v);
+    }
+    return 0;
+}
+""")
+    exe = tmp_path / "cast"
+    subprocess.run(["gcc", "-O3", "-std=c11", "-o", str(exe), str(src)], check=True)
+    args = ["nan" if v != v else repr(float(v)) for v, _ in PPM_CASES]
+    out = subprocess.run([str(exe)] + args, check=True, capture_output=True, text=True).stdout.split()
+    assert [int(x) for x in out] == [u for _, u in PPM_CASES]
