@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 4
+#define RTG_ABI_VERSION 5
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -230,6 +230,20 @@ typedef struct rtg_render_opts {
     int32_t compact_rows;    /* 1: the output holds only the owned rows, in image order
                                 (rows_owned*nx*3 floats; rows_owned = rtg_shard_rows()), for a
                                 gather of the shards instead of a full-frame reduce */
+    /* In-process multi-GPU fan-out (rtg_render / rtg_render_device; SURVEY.md §8(b) Threading,
+       the GPU counterpart of renderScene's 8 std::threads, src/Scene.cpp:340-356).  0/1: the
+       scene's device only.  N > 1: the frame is cut into N shards of row blocks (row_block, 0 = 4;
+       shard r owns the rows with (y / row_block) % N == r), one host thread per device renders
+       one shard on a replica of the scene (device-to-device copies of the scene's buffers), and
+       the shards' rows are gathered onto the scene's device with RCCL point-to-point transfers
+       (ncclCommInitAll over the devices; librccl.so.1 is loaded on first use).  row_offset /
+       row_stride / compact_rows must be 0. */
+    int32_t num_devices;
+    const int32_t* devices;  /* NULL: the scene's device followed by the next num_devices-1 device
+                                indices (mod rtg_device_count()); else num_devices indices, devices[0]
+                                = the scene's device.  A device listed twice takes no RCCL
+                                communicator: its shard is copied with hipMemcpyPeer (rehearsal of
+                                the N-shard path on fewer GPUs; results are identical). */
 } rtg_render_opts;
 
 /* Number of image rows y < ny with (y / row_block) % row_stride == row_offset. */
@@ -255,6 +269,10 @@ typedef struct rtg_render_stats {
     uint64_t shadow_steps;
     uint64_t trace_lane_slots;     /* collect_stats: sum over waves of 64 x the wave's longest walk */
     uint64_t shadow_lane_slots;    /*   (SIMD efficiency = trace_steps / trace_lane_slots) */
+    double shade_ms;         /* collect_timing: summed device time of the shading launches */
+    int32_t shade_launches;
+    int32_t devices;         /* devices that rendered the frame (num_devices fan-out or ranks: 1 here) */
+    double gather_ms;        /* multi-GPU: host wall time from the last shard's end to the gathered frame */
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */
@@ -315,6 +333,23 @@ int32_t rtg_render(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_rende
 int32_t rtg_render_device(rtg_scene* scene, const rtg_camera_desc* cam,
                           const rtg_render_opts* opts, float* rgb_out_device, void* stream);
 int32_t rtg_last_render_stats(const rtg_scene* scene, rtg_render_stats* out);
+
+/* ---- multi-process multi-GPU (one process per GPU) ------------------------
+   The same shard + RCCL gather as rtg_render_opts.num_devices, for callers that run one process
+   (rank) per GPU, e.g. under torch.distributed.run: rank 0 makes an id with rtg_comm_unique_id,
+   hands the RTG_COMM_ID_BYTES bytes to every rank (any side channel), and each rank calls
+   rtg_comm_init_rank (ncclCommInitRank).  rtg_render_ranked renders this rank's row-block shard
+   (row_offset = rank, row_stride = nranks, row_block = opts->row_block or 4) and gathers the
+   shards' rows into `frame_device` (ny*nx*3 floats on rank 0's device; may be NULL on other
+   ranks).  Every rank must call it for the same camera.  Synchronous on return. */
+#define RTG_COMM_ID_BYTES 128
+typedef struct rtg_comm rtg_comm;
+int32_t rtg_comm_unique_id(uint8_t id[RTG_COMM_ID_BYTES]);
+int32_t rtg_comm_init_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
+                           rtg_comm** out);
+int32_t rtg_comm_destroy(rtg_comm* comm);
+int32_t rtg_render_ranked(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_opts* opts, rtg_comm* comm,
+                          float* frame_device, void* stream);
 
 /* hw5 tone mapping (pages/Page5.md:47-53 describes a global operator; src/ has none): the
    Photographic TMO of DESIGN.md §11, from a camera's <Tonemap> (<TMO>Photographic</TMO>

@@ -49,6 +49,11 @@ int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t 
 /* Parse, build on `device`, render every camera with Philox seed `seed`, save each image
    (under out_dir if not NULL/empty, else at its <ImageName>). */
 int32_t rtgh_render_scene(const char* xml_path, int32_t device, uint64_t seed, const char* out_dir);
+/* Same, every camera rendered on num_devices GPUs (device, device+1, ...): row-block shards,
+   one host thread per GPU, RCCL gather of the rows (rtg_render_opts.num_devices / devices; with
+   num_devices = 1 the one GPU is a one-rank RCCL job).  num_devices = 0: rtgh_render_scene. */
+int32_t rtgh_render_scene_multi(const char* xml_path, int32_t device, int32_t num_devices, uint64_t seed,
+                                const char* out_dir);
 
 #ifdef __cplusplus
 }

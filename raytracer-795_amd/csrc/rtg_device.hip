@@ -1946,6 +1946,21 @@ __global__ void __launch_bounds__(256) k_finalize(const float* __restrict__ acc,
     out[3 * pix] = r; out[3 * pix + 1] = g; out[3 * pix + 2] = b;
 }
 
+// Multi-GPU gather: frame row y comes from the shard that owns it, at that shard's compact row
+// index (the rows of every shard are stacked in `recv` in rank order).
+__global__ void __launch_bounds__(256) k_place_rows(const float* __restrict__ recv, float* __restrict__ frame, int nx,
+                                                    int ny, int nranks, int block, const ShardPrefix pre) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // one float4 of a row
+    const int row4 = (3 * nx + 3) / 4;
+    if (e >= (long long)row4 * ny) return;
+    const int y = (int)(e / row4), c = (int)(e - (long long)y * row4) * 4;
+    const int r = (y / block) % nranks;
+    const int k = shard_owned_index(y, r, nranks, block);
+    const float* src = recv + ((size_t)(pre.rows[r] + k) * nx) * 3;
+    float* dst = frame + ((size_t)y * nx) * 3;
+    for (int q = c; q < c + 4 && q < 3 * nx; q++) dst[q] = src[q];
+}
+
 __global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const RayRec* __restrict__ rays,
                                                      const HitRec* __restrict__ hits, rtg_hit* __restrict__ out,
                                                      const int* __restrict__ orig_prim, int n) {
@@ -2068,6 +2083,13 @@ void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offse
     if (n <= 0) return;
     hipLaunchKernelGGL(k_finalize, dim3(nblk(n, 256)), dim3(256), 0, st, acc, out, nx, ny, row_offset, row_stride,
                        row_block, total);
+}
+void launch_place_rows(const float* recv, float* frame, int nx, int ny, int nranks, int block, const ShardPrefix& pre,
+                       hipStream_t st) {
+    const long long n = (long long)((3 * nx + 3) / 4) * ny;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_place_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, recv, frame, nx, ny, nranks,
+                       block, pre);
 }
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st) {

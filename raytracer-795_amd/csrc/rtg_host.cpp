@@ -347,6 +347,7 @@ int build_node4(const std::vector<HNode>& hn, int n, int prim_base, std::vector<
 struct DBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    size_t used = 0;         // bytes holding data (upload); replicas copy this many
     int grow(size_t need) {
         if (need <= bytes) return RTG_OK;
         if (p) (void)hipFree(p);
@@ -360,7 +361,7 @@ struct DBuf {
         return RTG_OK;
     }
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
-    void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
+    void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; used = 0; }
 };
 
 template <class T>
@@ -369,6 +370,7 @@ int upload(DBuf& b, const std::vector<T>& v) {
     int rc = b.grow(n);
     if (rc) return rc;
     if (!v.empty()) HIP_TRY(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    b.used = v.size() * sizeof(T);
     return RTG_OK;
 }
 
@@ -386,7 +388,7 @@ struct Level {
 struct Lane {
     hipStream_t st = nullptr;
     hipEvent_t ev_count = nullptr;          // recorded after the level count copy
-    hipEvent_t ev_t[4] = {};                // trace start/end, shadow start/end (collect_timing)
+    hipEvent_t ev_t[5] = {};                // trace start, trace end, shade end, shadow start, shadow end
     unsigned long long* h_count = nullptr;  // pinned host slot
     DBuf qcnt;                              // 64 x u64 per pass (level -> next rays | shadow entries << 32)
     std::vector<Level> levels;
@@ -436,6 +438,8 @@ struct rtg_scene {
     int bvh_builder = RTG_BVH_AUTO;
     double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
     int bvh_gpu_objects = 0;                 // objects whose BVH the GPU built
+    bool replica = false;                    // device copy made by scene_replicate (no host-side structures)
+    rtg::MultiState* multi = nullptr;        // num_devices fan-out: replicas, RCCL communicators (rtg_multi.cpp)
 };
 
 // Exceptions (std::bad_alloc from host containers, ...) never cross the C ABI.
@@ -522,11 +526,39 @@ static int validate(const rtg_scene_desc* d) {
     return RTG_OK;
 }
 
+// The scene's device buffers, in one list (release, replication).
+static std::vector<DBuf*> scene_buffers(rtg_scene* s) {
+    return {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices,
+            &s->d_vnormals, &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights,
+            &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf};
+}
+
+// Point the kernels' SceneView at this scene's device buffers.
+static void bind_view(rtg_scene* s) {
+    SceneView& sv = s->sv;
+    sv.tops = s->d_tops.as<TopObject>();
+    sv.geoms = s->d_geoms.as<Geometry>();
+    sv.nodes = s->d_nodes.as<Node>();
+    sv.nodes4 = s->d_nodes4.as<Node4>();
+    sv.tris = s->d_tris.as<TriGeom>();
+    sv.prim_idx = s->d_primidx.as<int4>();
+    sv.vertices = s->d_vertices.as<float>();
+    sv.vnormals = s->d_vnormals.as<float>();
+    sv.texcoords = s->d_texcoords.as<float>();
+    sv.materials = s->d_materials.as<MaterialDev>();
+    sv.textures = s->d_textures.as<TextureDev>();
+    sv.texels = s->d_texels.as<float>();
+    sv.lights = s->d_lights.as<LightDev>();
+    sv.top_emit = s->d_topemit.as<int>();
+    sv.emit_tris = s->d_etris.as<float>();
+    sv.emit_cdf = s->d_ecdf.as<float>();
+}
+
 static void scene_free(rtg_scene* s) {
-    DBuf* bufs[] = {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices, &s->d_vnormals,
-                    &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights, &s->d_origprim,
-                    &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_acc, &s->d_counters, &s->d_stats};
-    for (DBuf* b : bufs) b->release();
+    multi_free(s->multi);
+    s->multi = nullptr;
+    for (DBuf* b : scene_buffers(s)) b->release();
+    s->d_acc.release(); s->d_counters.release(); s->d_stats.release();
     for (Lane& l : s->lanes) l.destroy();
     s->lanes.clear();
 }
@@ -918,23 +950,12 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         return rc;
 
     SceneView& sv = s->sv;
-    sv.tops = s->d_tops.as<TopObject>(); sv.num_tops = (int)tops.size(); sv.num_objects = d->num_objects;
-    sv.geoms = s->d_geoms.as<Geometry>();
-    sv.nodes = s->d_nodes.as<Node>();
-    sv.nodes4 = s->d_nodes4.as<Node4>();
-    sv.tris = s->d_tris.as<TriGeom>();
-    sv.prim_idx = s->d_primidx.as<int4>();
-    sv.vertices = s->d_vertices.as<float>();
-    sv.vnormals = s->d_vnormals.as<float>();
-    sv.texcoords = s->d_texcoords.as<float>();
+    bind_view(s);
+    sv.num_tops = (int)tops.size(); sv.num_objects = d->num_objects;
     sv.num_texcoords = d->num_texcoords;
-    sv.materials = s->d_materials.as<MaterialDev>(); sv.num_materials = d->num_materials;
-    sv.textures = s->d_textures.as<TextureDev>(); sv.num_textures = d->num_textures;
-    sv.texels = s->d_texels.as<float>();
-    sv.lights = s->d_lights.as<LightDev>(); sv.num_lights = d->num_lights;
-    sv.top_emit = s->d_topemit.as<int>();
-    sv.emit_tris = s->d_etris.as<float>();
-    sv.emit_cdf = s->d_ecdf.as<float>();
+    sv.num_materials = d->num_materials;
+    sv.num_textures = d->num_textures;
+    sv.num_lights = d->num_lights;
     sv.num_emit = s->num_emit;
     sv.pt_flags = 0;
     sv.max_depth = d->max_recursion_depth;
@@ -1040,6 +1061,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     if (cam->nx < 1 || cam->ny < 1 || cam->num_samples < 1) return fail(RTG_ERR_INVALID, "bad camera");
     rtg_render_opts o{};
     if (opts) o = *opts;
+    if (o.num_devices > 1 || o.devices) return fail(RTG_ERR_INVALID, "num_devices / devices need rtg_render / rtg_render_device");
     int stride = o.row_stride > 1 ? o.row_stride : 1;
     int off = o.row_offset;
     if (off < 0 || off >= stride) return fail(RTG_ERR_INVALID, "row_offset out of range");
@@ -1174,16 +1196,17 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                          gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                          Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), Ln.rays.as<RayRec>(),
                          Ln.meta.as<RayMeta>(), qc, n, ln.st);
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
         // the next level's size is known once shade is done: read it back now, so the host can
         // enqueue that level while this level's shadow queries still run (no host round trip
         // between the levels on the stream)
         HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
         HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
-        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
         launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
                       Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt);
-        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt)
             launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), Lc.shadows.as<ShadowRec>(), nL,
@@ -1252,13 +1275,16 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const unsigned next = (unsigned)q;
         shadow_listed += q >> 32;
         if (timing) {
-            float a = 0.0f, b = 0.0f;
+            float a = 0.0f, b = 0.0f, c = 0.0f;
             HIP_TRY(hipEventElapsedTime(&a, ln.ev_t[0], ln.ev_t[1]));
+            HIP_TRY(hipEventElapsedTime(&c, ln.ev_t[1], ln.ev_t[2]));
             stt.trace_ms += a;
             stt.trace_launches++;
+            stt.shade_ms += c;
+            stt.shade_launches++;
             if (nL > 0) {
-                HIP_TRY(hipEventSynchronize(ln.ev_t[3]));   // the count arrives before the shadow pass ends
-                HIP_TRY(hipEventElapsedTime(&b, ln.ev_t[2], ln.ev_t[3]));
+                HIP_TRY(hipEventSynchronize(ln.ev_t[4]));   // the count arrives before the shadow pass ends
+                HIP_TRY(hipEventElapsedTime(&b, ln.ev_t[3], ln.ev_t[4]));
                 stt.shadow_ms += b;
                 stt.shadow_launches++;
             }
@@ -1310,9 +1336,61 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     stt.shadow_steps = ctr.shadow_steps;
     stt.trace_lane_slots = ctr.trace_lane_slots;
     stt.shadow_lane_slots = ctr.shadow_lane_slots;
+    stt.devices = 1;
     s->stats = stt;
     return RTG_OK;
 }
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ hooks for rtg_multi.cpp
+namespace rtg {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+int scene_device(const rtg_scene* s) { return s->device; }
+int scene_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* o, float* out_dev, hipStream_t st) {
+    return render_impl(s, cam, o, out_dev, st);
+}
+rtg_render_stats scene_stats(const rtg_scene* s) { return s->stats; }
+void scene_set_stats(rtg_scene* s, const rtg_render_stats& st) { s->stats = st; }
+MultiState*& scene_multi(rtg_scene* s) { return s->multi; }
+
+// A render-only copy of `src` on `device`: every device buffer copied device to device
+// (hipMemcpyPeer), the kernels' view re-pointed.  No host-side structures (introspection) and
+// its own render workspace, so one host thread per replica can render concurrently.
+int scene_replicate(rtg_scene* src, int device, rtg_scene** out) {
+    *out = nullptr;
+    rtg_scene* r = new (std::nothrow) rtg_scene();
+    if (!r) return fail(RTG_ERR_OOM, "host allocation");
+    r->device = device;
+    r->replica = true;
+    r->num_objects = src->num_objects; r->num_instances = src->num_instances; r->num_vertices = src->num_vertices;
+    r->num_emit = src->num_emit;
+    r->num_lanes = src->num_lanes;
+    r->sv = src->sv;
+    const std::vector<DBuf*> from = scene_buffers(src), to = scene_buffers(r);
+    int rc = RTG_OK;
+    if (hipSetDevice(device) != hipSuccess) rc = fail(RTG_ERR_NO_DEVICE, "replica device");
+    for (size_t i = 0; i < from.size() && rc == RTG_OK; i++) {
+        const size_t n = from[i]->used;
+        rc = to[i]->grow(std::max<size_t>(n, 1));
+        if (rc == RTG_OK && n) {
+            const hipError_t e = hipMemcpyPeer(to[i]->p, device, from[i]->p, src->device, n);
+            if (e != hipSuccess) rc = fail(RTG_ERR_HIP, std::string("scene replica copy: ") + hipGetErrorString(e));
+        }
+        to[i]->used = n;
+    }
+    if (rc != RTG_OK) {
+        scene_free(r);
+        delete r;
+        return rc;
+    }
+    bind_view(r);
+    *out = r;
+    return RTG_OK;
+}
+}  // namespace rtg
+
+extern "C" {
 
 int32_t rtg_render_device(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, float* rgb_out_device,
                           void* stream) {
@@ -1320,6 +1398,7 @@ int32_t rtg_render_device(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
         if (!s || !cam || !rgb_out_device) return fail(RTG_ERR_INVALID, "null argument");
         if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot render");
         HIP_TRY(hipSetDevice(s->device));
+        if (opts && (opts->num_devices > 1 || opts->devices)) return render_multi(s, cam, opts, rgb_out_device, (hipStream_t)stream);
         return render_impl(s, cam, opts, rgb_out_device, (hipStream_t)stream);
     });
 }
@@ -1343,7 +1422,8 @@ int32_t rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_op
         size_t bytes = sizeof(float) * 3 * (size_t)cam->nx * std::max(out_rows, 1);
         float* d_out = nullptr;
         HIP_TRY(hipMalloc(&d_out, bytes));
-        int rc = render_impl(s, cam, opts, d_out, nullptr);
+        int rc = (opts && (opts->num_devices > 1 || opts->devices)) ? render_multi(s, cam, opts, d_out, nullptr)
+                                                 : render_impl(s, cam, opts, d_out, nullptr);
         if (rc == RTG_OK) {
             hipError_t e = hipMemcpy(rgb_out, d_out, bytes, hipMemcpyDeviceToHost);
             if (e != hipSuccess) rc = fail(RTG_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));

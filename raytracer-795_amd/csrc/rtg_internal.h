@@ -299,6 +299,26 @@ void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offse
 void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st);
 
+// Multi-GPU rows gather: shard r's compact rows start at row prefix[r] of `recv`; every frame
+// row y is copied from its owning shard ((y / block) % nranks).  nranks <= kMaxRanks.
+constexpr int kMaxRanks = 64;
+struct ShardPrefix { int rows[kMaxRanks + 1]; };
+void launch_place_rows(const float* recv, float* frame, int nx, int ny, int nranks, int block, const ShardPrefix& pre,
+                       hipStream_t st);
+
+// Hooks between the C ABI's single-device driver (rtg_host.cpp) and the multi-GPU fan-out
+// (rtg_multi.cpp).  rtg_scene is the opaque ABI handle (defined in rtg_host.cpp).
+struct MultiState;
+void multi_free(MultiState* m);
+int set_error(int code, const std::string& msg);           // sets rtg_last_error() of this thread
+int scene_device(const rtg_scene* s);
+int scene_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* o, float* out_dev, hipStream_t st);
+rtg_render_stats scene_stats(const rtg_scene* s);
+void scene_set_stats(rtg_scene* s, const rtg_render_stats& st);
+MultiState*& scene_multi(rtg_scene* s);
+int scene_replicate(rtg_scene* src, int device, rtg_scene** out);
+int render_multi(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* o, float* out_dev, hipStream_t st);
+
 // Photographic tone mapping (rtg_tonemap.hip); hdr / out are device arrays.
 int tonemap_white_index(int n, float burn_percent);
 int tonemap_device(const float* hdr, int nx, int ny, const rtg_tonemap_desc& tm, float* out, hipStream_t st,

@@ -1089,7 +1089,19 @@ int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t 
 
 // Scene::renderScene (src/Scene.cpp:425-494): precompute once, render and save every camera.
 int32_t rtgh_render_scene(const char* xml_path, int32_t device, uint64_t seed, const char* out_dir) {
+    return rtgh_render_scene_multi(xml_path, device, 0, seed, out_dir);
+}
+
+int32_t rtgh_render_scene_multi(const char* xml_path, int32_t device, int32_t num_devices, uint64_t seed,
+                                const char* out_dir) {
     return guarded([&]() -> int32_t {
+        if (num_devices < 0 || num_devices > 64) return fail(RTG_ERR_INVALID, "num_devices");
+        // num_devices >= 1: the multi-GPU path (rtg_render_opts.devices = device, device+1, ...),
+        // even for one GPU (one RCCL rank); 0: the single-device render
+        const int visible = rtg_device_count();
+        if (num_devices > visible) return fail(RTG_ERR_NO_DEVICE, "more devices requested than visible");
+        std::vector<int32_t> devs(num_devices);
+        for (int r = 0; r < num_devices; r++) devs[r] = (device + r) % std::max(visible, 1);
         rtgh_scene* sc = nullptr;
         int rc = rtgh_parse_xml(xml_path, &sc);
         if (rc) return rc;
@@ -1102,6 +1114,8 @@ int32_t rtgh_render_scene(const char* xml_path, int32_t device, uint64_t seed, c
             std::vector<float> rgb((size_t)c.d.nx * c.d.ny * 3);
             rtg_render_opts o{};
             o.seed = seed;
+            o.num_devices = num_devices;   // row-block shards, one host thread per GPU, RCCL gather
+            o.devices = num_devices > 0 ? devs.data() : nullptr;
             rc = rtg_render(gpu, &c.d, &o, rgb.data());
             if (rc) { g_err = rtg_last_error(); break; }
             std::string name = c.image_name;
@@ -1127,7 +1141,8 @@ int32_t rtgh_render_scene(const char* xml_path, int32_t device, uint64_t seed, c
             }
             rtg_render_stats st{};
             rtg_last_render_stats(gpu, &st);
-            printf("%s: %.1f ms, %.1f Mray/s\n", name.c_str(), st.render_ms, st.total_rays / (st.render_ms * 1e3));
+            printf("%s: %.1f ms, %.1f Mray/s, %d GPU%s\n", name.c_str(), st.render_ms, st.total_rays / (st.render_ms * 1e3),
+                   st.devices, st.devices == 1 ? "" : "s");
         }
         rtg_scene_destroy(gpu);
         rtgh_free(sc);

@@ -6,8 +6,8 @@ mirror of the reference's Parser / Scene::renderScene() / Image interface.
 """
 from . import _abi
 from ._abi import RtgError, load_library
-from .render import Renderer, render_scene, save_image, tonemap
+from .render import Comm, Renderer, render_scene, save_image, tonemap
 from .scene import Camera, Instance, Light, Material, Object, Scene, Texture, parse_xml, write_xml
 
-__all__ = ["RtgError", "load_library", "Renderer", "render_scene", "save_image", "tonemap", "Camera", "Instance", "Light",
+__all__ = ["RtgError", "load_library", "Comm", "Renderer", "render_scene", "save_image", "tonemap", "Camera", "Instance", "Light",
            "Material", "Object", "Scene", "Texture", "parse_xml", "write_xml", "_abi"]

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 4
+RTG_ABI_VERSION = 5
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -107,7 +107,7 @@ class RenderOpts(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("row_offset", C.c_int32), ("row_stride", C.c_int32),
                 ("traversal", C.c_int32), ("max_batch_rays", C.c_int32), ("collect_stats", C.c_int32),
                 ("collect_timing", C.c_int32), ("streams", C.c_int32), ("row_block", C.c_int32),
-                ("compact_rows", C.c_int32)]
+                ("compact_rows", C.c_int32), ("num_devices", C.c_int32), ("devices", C.POINTER(C.c_int32))]
 
 
 class RenderStats(C.Structure):
@@ -117,7 +117,11 @@ class RenderStats(C.Structure):
                 ("shadow_node_visits", C.c_uint64), ("shadow_tri_tests", C.c_uint64), ("trace_ms", C.c_double),
                 ("shadow_ms", C.c_double), ("trace_launches", C.c_int32), ("shadow_launches", C.c_int32),
                 ("trace_steps", C.c_uint64), ("shadow_steps", C.c_uint64),
-                ("trace_lane_slots", C.c_uint64), ("shadow_lane_slots", C.c_uint64)]
+                ("trace_lane_slots", C.c_uint64), ("shadow_lane_slots", C.c_uint64),
+                ("shade_ms", C.c_double), ("shade_launches", C.c_int32), ("devices", C.c_int32),
+                ("gather_ms", C.c_double)]
+
+RTG_COMM_ID_BYTES = 128
 
 
 class Ray(C.Structure):
@@ -170,6 +174,11 @@ EXPORTS = {
     "rtg_scene_object_bvh": (C.c_int32, [C.c_void_p, C.c_int32, PI, PI, PI, PI, PF]),
     "rtg_scene_object_matrices": (C.c_int32, [C.c_void_p, C.c_int32, PF, PF]),
     "rtg_scene_vertex_normals": (C.c_int32, [C.c_void_p, PF]),
+    "rtg_comm_unique_id": (C.c_int32, [C.c_void_p]),
+    "rtg_comm_init_rank": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "rtg_comm_destroy": (C.c_int32, [C.c_void_p]),
+    "rtg_render_ranked": (C.c_int32, [C.c_void_p, C.POINTER(CameraDesc), C.POINTER(RenderOpts), C.c_void_p,
+                                      C.c_void_p, C.c_void_p]),
 }
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))

@@ -39,6 +39,8 @@ def load():
         lib.rtgh_save_image.restype = C.c_int32
         lib.rtgh_render_scene.argtypes = [C.c_char_p, C.c_int32, C.c_uint64, C.c_char_p]
         lib.rtgh_render_scene.restype = C.c_int32
+        lib.rtgh_render_scene_multi.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_uint64, C.c_char_p]
+        lib.rtgh_render_scene_multi.restype = C.c_int32
         lib.rtgh_read_image.argtypes = [C.c_char_p, C.POINTER(A.PF), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         lib.rtgh_read_image.restype = C.c_int32
         lib.rtgh_free_image.argtypes = [A.PF]
@@ -110,9 +112,11 @@ def save_image(name: str, rgb: np.ndarray):
     _check(lib.rtgh_save_image(name.encode(), a.ctypes.data_as(A.PF), a.shape[1], a.shape[0]))
 
 
-def render_scene(xml_path: str, device: int = 0, seed: int = 0x5EED2026, out_dir: str | None = None):
+def render_scene(xml_path: str, device: int = 0, seed: int = 0x5EED2026, out_dir: str | None = None,
+                 num_devices: int = 1):
     lib = load()
-    _check(lib.rtgh_render_scene(xml_path.encode(), device, seed, out_dir.encode() if out_dir else None))
+    _check(lib.rtgh_render_scene_multi(xml_path.encode(), device, num_devices, seed,
+                                       out_dir.encode() if out_dir else None))
 
 
 def _struct(s) -> dict:

@@ -53,7 +53,7 @@ class Renderer:
 
     @staticmethod
     def opts(seed=DEFAULT_SEED, row_offset=0, row_stride=1, traversal=0, max_batch_rays=0, collect_stats=0,
-             collect_timing=0, streams=0, row_block=1, compact_rows=0):
+             collect_timing=0, streams=0, row_block=1, compact_rows=0, num_devices=0, devices=None):
         o = A.RenderOpts()
         o.seed = seed
         o.row_offset, o.row_stride, o.row_block = row_offset, row_stride, row_block
@@ -63,6 +63,11 @@ class Renderer:
         o.collect_timing = collect_timing
         o.streams = streams
         o.compact_rows = compact_rows
+        o.num_devices = num_devices
+        if devices is not None:
+            arr = (C.c_int32 * len(devices))(*devices)
+            o.devices = C.cast(arr, C.POINTER(C.c_int32))
+            o._devices_keepalive = arr
         return o
 
     def render(self, camera: Camera | int = 0, **kw) -> np.ndarray:
@@ -82,6 +87,15 @@ class Renderer:
         o = self.opts(**kw)
         A.check(self.lib.rtg_render_device(self.handle, C.byref(cd), C.byref(o), C.c_void_p(out_ptr),
                                            C.c_void_p(stream)), self.lib)
+
+    def render_ranked(self, camera: Camera | int, comm: "Comm", frame_ptr: int, stream: int = 0, **kw):
+        """One rank of a one-process-per-GPU render (rtg_render_ranked): this rank's row-block shard,
+        gathered over RCCL into `frame_ptr` (device memory, rank 0; other ranks may pass 0)."""
+        cam = self.scene.cameras[camera] if isinstance(camera, int) else camera
+        cd = cam.desc()
+        o = self.opts(**kw)
+        A.check(self.lib.rtg_render_ranked(self.handle, C.byref(cd), C.byref(o), comm.handle,
+                                           C.c_void_p(frame_ptr or None), C.c_void_p(stream)), self.lib)
 
     def stats(self) -> dict:
         s = A.RenderStats()
@@ -233,6 +247,38 @@ def tonemapped_name(name: str) -> str:
     """Where a camera's tone-mapped image goes: its ImageName with the extension set to .png."""
     stem, _ = os.path.splitext(name)
     return stem + ".png"
+
+
+class Comm:
+    """An RCCL communicator of librtg (rtg_comm_init_rank) for rtg_render_ranked."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = A.load_library()
+        buf = (C.c_uint8 * A.RTG_COMM_ID_BYTES)()
+        A.check(lib.rtg_comm_unique_id(buf), lib)
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
+        self.lib = A.load_library()
+        if len(uid) != A.RTG_COMM_ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        buf = (C.c_uint8 * A.RTG_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        A.check(self.lib.rtg_comm_init_rank(buf, int(nranks), int(rank), int(device), C.byref(h)), self.lib)
+        self.handle = h
+        self.rank, self.nranks, self.device = rank, nranks, device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.rtg_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def render_scene(scene: Scene, out_dir: str | None = None, device: int = 0, seed: int = DEFAULT_SEED) -> list:

@@ -1,0 +1,60 @@
+"""Per-kernel PMC counters of a gpu_round.sh run -> one CSV + one JSON summary.
+
+usage: python scripts/pmc_counters.py <prof_dir> <out.csv> <out.json> [workload]
+
+Every counter pass (p1..pN) is a separate `rocprofv3 --pmc <set> --kernel-trace` run of
+`bench.py --steps 1 --warmup 0 --no-cpu` with RTG_STREAMS=1.  For each kernel and counter the
+CSV holds the number of dispatches, the sum over them and the mean per dispatch; the JSON holds
+the per-dispatch means that bench.py divides by its live HIP-event launch times (the roofline
+ceilings of DESIGN.md §4).  FETCH_SIZE / WRITE_SIZE are in KB; the gfx950 correction
+(MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of wide reads) is applied in the
+JSON's `hbm_bytes` (= 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def kname(k):
+    k = k.split("(")[0].replace("void ", "")
+    # k_trace<false, false, true> (level 0) and <false, false, false> (secondary levels): one
+    # combined entry as well, the kernel bench.py times as `k_trace<false,false,*>`
+    return k
+
+
+def main():
+    d, out_csv, out_json = sys.argv[1:4]
+    workload = sys.argv[4] if len(sys.argv) > 4 else "dragon1m"
+    tot = collections.defaultdict(float)
+    cnt = collections.defaultdict(int)
+    for f in sorted(glob.glob(f"{d}/p*/**/*counter_collection.csv", recursive=True)):
+        for r in csv.DictReader(open(f)):
+            k = kname(r["Kernel_Name"])
+            c = r["Counter_Name"]
+            v = float(r["Counter_Value"])
+            for key in {k, "rtg::k_trace<false, false, *>"} if k.startswith("rtg::k_trace<false, false") else {k}:
+                tot[(key, c)] += v
+                cnt[(key, c)] += 1
+    rows = sorted(tot)
+    with open(out_csv, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["kernel", "counter", "dispatches", "sum", "per_dispatch"])
+        for k, c in rows:
+            w.writerow([k, c, cnt[(k, c)], f"{tot[(k, c)]:.6g}", f"{tot[(k, c)] / cnt[(k, c)]:.6g}"])
+    summ = collections.defaultdict(dict)
+    for k, c in rows:
+        summ[k][c] = tot[(k, c)] / cnt[(k, c)]
+        summ[k]["dispatches_" + c] = cnt[(k, c)]
+    for k, m in summ.items():
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            m["hbm_bytes"] = 2.0 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024
+    json.dump({"source": os.path.basename(os.path.normpath(d)), "workload": workload,
+               "command": "RTG_STREAMS=1 rocprofv3 --pmc <set> --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu",
+               "kernels": summ}, open(out_json, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

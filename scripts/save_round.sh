@@ -1,0 +1,29 @@
+#!/bin/bash
+# Copy the judged evidence of a gpu_round.sh run into profiles/ (tracked):
+#   <tag>_bench.json            the bench.py line
+#   <tag>_kernel_stats.{csv,txt} rocprofv3 --kernel-trace --stats of bench.py (RTG_STREAMS=1)
+#   <tag>_counters.csv          per-kernel PMC counters (dispatches, sum, per-dispatch mean)
+#   counters_current.json       the per-dispatch means bench.py's rooflines divide by live launch times
+set -e
+TAG=$1
+WL=${2:-dragon1m}
+D=gpurun_out/prof_$TAG
+cp $D/bench.json profiles/${TAG}_bench.json
+python3 - "$D/kt/kt_kernel_stats.csv" > profiles/${TAG}_kernel_stats.txt <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+print(f"{'kernel':48s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>9s} {'pct':>6s}")
+for r in rows:
+    print(f"{r['Name'].split('(')[0].replace('void ', '')[:48]:48s} {r['Calls']:>6s} "
+          f"{float(r['TotalDurationNs'])/1e6:10.2f} {float(r['AverageNs'])/1e3:9.1f} {float(r['Percentage']):6.2f}")
+# combined closest-hit line (GEN=true level-0 + GEN=false secondary launches): the kernel whose
+# average bench.py's roofline.avg_launch_ms measures
+ks = [r for r in rows if r['Name'].replace('void ', '').startswith('rtg::k_trace<false, false')]
+if ks:
+    c = sum(int(r['Calls']) for r in ks); t = sum(float(r['TotalDurationNs']) for r in ks)
+    print(f"{'rtg::k_trace<false, false, *> (combined)':48s} {c:6d} {t/1e6:10.2f} {t/c/1e3:9.1f}")
+PY
+cp $D/kt/kt_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
+python3 scripts/pmc_counters.py $D profiles/${TAG}_counters.csv profiles/${TAG}_counters.json $WL
+cp profiles/${TAG}_counters.json profiles/counters_current.json
+echo saved $TAG

@@ -206,7 +206,7 @@ def test_host_library_exports_every_declared_symbol():
     hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rtg_host.h")
     decl = set(re.findall(r"^\s*(?:int32_t|const char\*|void|const rtg_scene_desc\*)\s+(rtgh_\w+)\s*\(",
                           open(hdr).read(), re.M))
-    assert len(decl) == 11
+    assert len(decl) == 12
     out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], capture_output=True, text=True, check=True)
     syms = set(re.findall(r"\sT\s(rtgh_\w+)", out.stdout))
     assert decl <= syms, decl - syms
