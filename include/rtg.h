@@ -3,28 +3,28 @@
  * (badiba/raytracer-795).  Plain C, plain pointers and sizes, no C++/torch types.
  *
  * Drop-in seam:
- *   reference  void Scene::renderScene(void)                       src/Scene.h:89, src/Scene.cpp:425-494
- *   reference  ReturnVal BVHMethods::FindIntersection(ray,objs,inst) src/Helper.h:25, src/Helper.cpp:72-134
+ *   reference  void Scene::renderScene(void)                       src/Scene.h:89, src/Scene.cpp:294-363
+ *   reference  ReturnVal BVHMethods::FindIntersection(ray,objs,inst) src/Helper.h:25, src/Helper.cpp:18-80
  *
  *   rtg_scene_create()  replaces the precompute half of renderScene()
  *                        (Perlin table, ComputeObjectTransformations, smooth normals,
- *                        per-object BVH construction: src/Scene.cpp:427-458)
+ *                        per-object BVH construction: src/Scene.cpp:296-323)
  *   rtg_render()        replaces the per-camera pixel loop of renderScene()
  *                        (8 std::threads of ThreadedRendering -> Single/MultiSample ->
- *                        Shading: src/Scene.cpp:461-488, 400-423, 496-542) and writes
+ *                        Shading: src/Scene.cpp:329-362, 269-292, 365-411) and writes
  *                        the float RGB framebuffer the reference keeps in Image::_data
- *                        (src/Image.cpp:176-184) — [y][x][c], 0..255 scale, unclamped.
+ *                        (src/Image.cpp:16-24) — [y][x][c], 0..255 scale, unclamped.
  *   rtg_trace_closest() replaces BVHMethods::FindIntersection for a batch of rays
  *                        (closest-hit with the reference's object/instance rules).
  *
  * The scene descriptor is exactly what the reference Parser leaves in the global
- * Scene after `new Scene(xml)` (src/Scene.cpp:586-634, src/Parser.h): raw vertices,
+ * Scene after `new Scene(xml)` (src/Scene.cpp:455-504, src/Parser.h): raw vertices,
  * texture coordinates, objects with their transformation-reference lists, instances,
  * materials, textures (decoded texels), lights in the reference's light order, scalars.
  * All indices keep the reference's conventions: vertex / material / texture indices
- * are 1-based positions (materials[matIndex-1], src/Scene.cpp:506; vertices[idx-1],
- * src/Shape.cpp:232), transformation ids are 1-based positions into the per-kind lists
- * (src/Helper.cpp:212).
+ * are 1-based positions (materials[matIndex-1], src/Scene.cpp:375; vertices[idx-1],
+ * src/Shape.cpp:300-302), transformation ids are 1-based positions into the per-kind lists
+ * (src/Helper.cpp:158).
  *
  * Every function returns RTG_OK (0) or a negative rtg_status; rtg_last_error() returns
  * a thread-local message.  Nothing throws or aborts.  The library copies all inputs to
@@ -51,7 +51,7 @@ typedef enum rtg_status {
     RTG_ERR_UNSUPPORTED = -5
 } rtg_status;
 
-/* ---- enums mirror src/defs.h:8-11, src/Material.h:8-9, src/Light.h:12, src/Transformation.h:8 ---- */
+/* ---- enums mirror src/defs.h:8-11, src/Material.h:7-8, src/Light.h:12, src/Transformation.h:7 ---- */
 typedef enum rtg_object_type { RTG_OBJ_SPHERE = 0, RTG_OBJ_TRIANGLE = 1, RTG_OBJ_MESH = 2 } rtg_object_type;
 typedef enum rtg_xform_type {
     RTG_XF_TRANSLATION = 1, RTG_XF_SCALING = 2, RTG_XF_ROTATION = 3, RTG_XF_COMPOSITE = 4
@@ -59,7 +59,7 @@ typedef enum rtg_xform_type {
 typedef enum rtg_material_type {
     RTG_MAT_NORMAL = 0, RTG_MAT_MIRROR = 1, RTG_MAT_CONDUCTOR = 2, RTG_MAT_DIELECTRIC = 3
 } rtg_material_type;
-/* BRDFType order of src/Material.h:9 */
+/* BRDFType order of src/Material.h:8 */
 typedef enum rtg_brdf_type {
     RTG_BRDF_NONE = 0, RTG_BRDF_OBP = 1, RTG_BRDF_MBP = 2, RTG_BRDF_MBPN = 3, RTG_BRDF_OP = 4,
     RTG_BRDF_MP = 5, RTG_BRDF_MPN = 6, RTG_BRDF_TS = 7, RTG_BRDF_TSF = 8
@@ -80,7 +80,7 @@ typedef enum rtg_light_type {
     RTG_LIGHT_ENVIRONMENT = 4
 } rtg_light_type;
 
-/* One entry of an object's <Transformations> list, e.g. "t1 s2 r1" (src/Parser.h:763-791).
+/* One entry of an object's <Transformations> list, e.g. "t1 s2 r1" (src/Parser.h:769-796).
    index is the 1-based position in the list of that kind. */
 typedef struct rtg_xform_ref { int32_t type; int32_t index; } rtg_xform_ref;
 
@@ -102,7 +102,7 @@ typedef struct rtg_object_desc {
     int32_t v[3];            /* 1-based vertex indices */
     /* mesh */
     int32_t face_first;      /* range in rtg_scene_desc.faces (triples of 1-based vertex indices,
-                                vertexOffset already added: src/Parser.h:1112-1139) */
+                                vertexOffset already added: src/Parser.h:1109-1149) */
     int32_t face_count;
     /* object light (hw7 <LightSphere> / <LightMesh>, pages/Page7.md:7-13; no reference code):
        is_light = 1 makes the object an emitter of `radiance` from both sides.  Only the path
@@ -115,14 +115,14 @@ typedef struct rtg_object_desc {
 typedef struct rtg_instance_desc {
     int32_t base_object;     /* 0-based index into objects (a Mesh) */
     int32_t id;
-    int32_t material;        /* 1-based; overrides the base mesh material (src/Helper.cpp:122) */
-    int32_t reset_transform; /* src/Helper.cpp:270-272 */
+    int32_t material;        /* 1-based; overrides the base mesh material (src/Helper.cpp:68) */
+    int32_t reset_transform; /* src/Helper.cpp:216-218 */
     int32_t xform_first;
     int32_t xform_count;
     float blur[3];
 } rtg_instance_desc;
 
-typedef struct rtg_material_desc {   /* src/Material.h:11-34, src/Parser.h:304-472 */
+typedef struct rtg_material_desc {   /* src/Material.h:10-33, src/Parser.h:304-474 */
     int32_t type;            /* rtg_material_type */
     int32_t brdf;            /* rtg_brdf_type */
     int32_t phong_exp;
@@ -170,7 +170,7 @@ typedef struct rtg_scene_desc {
     float background[3];
     float ambient_light[3];
     int32_t background_texture;    /* 0-based texture index with decal replace_background, -1 none
-                                      (last such texture, src/Scene.cpp:625-631) */
+                                      (last such texture, src/Scene.cpp:494-500) */
     int32_t environment_light;     /* 0-based light index, -1 none (src/Parser.h:1302-1313) */
 
     const float* vertices;   int32_t num_vertices;    /* xyz triples */
@@ -188,7 +188,7 @@ typedef struct rtg_scene_desc {
     const rtg_light_desc* lights;       int32_t num_lights;
 } rtg_scene_desc;
 
-typedef struct rtg_camera_desc {     /* src/Camera.h:351-399; FovY/GazePoint already resolved */
+typedef struct rtg_camera_desc {     /* src/Camera.h:19-67; FovY/GazePoint already resolved */
     float position[3];
     float gaze[3];
     float up[3];
@@ -231,7 +231,7 @@ typedef struct rtg_render_opts {
                                 (rows_owned*nx*3 floats; rows_owned = rtg_shard_rows()), for a
                                 gather of the shards instead of a full-frame reduce */
     /* In-process multi-GPU fan-out (rtg_render / rtg_render_device; SURVEY.md §8(b) Threading,
-       the GPU counterpart of renderScene's 8 std::threads, src/Scene.cpp:340-356).  0/1: the
+       the GPU counterpart of the 8 std::threads of renderScene, src/Scene.cpp:294-363).  0/1: the
        scene's device only.  N > 1: the frame is cut into N shards of row blocks (row_block, 0 = 4;
        shard r owns the rows with (y / row_block) % N == r), one host thread per device renders
        one shard on a replica of the scene (device-to-device copies of the scene's buffers), and
@@ -286,9 +286,9 @@ typedef struct rtg_hit {             /* what FindIntersection leaves in ReturnVa
     int32_t object;          /* top-level index: [0,num_objects) objects, then instances */
     int32_t prim;            /* primitive index in the object's original (parse) order */
     int32_t material;        /* 1-based material (instance override applied) */
-    float t;                 /* gett() distance along the world ray (src/Helper.cpp:95) */
+    float t;                 /* gett() distance along the world ray (src/Helper.cpp:41) */
     float point[3];          /* world hit point = ray.getPoint(t) */
-    float normal[3];         /* world normal after TransformNormal (src/Helper.cpp:129-131) */
+    float normal[3];         /* world normal after TransformNormal (src/Helper.cpp:75-77) */
 } rtg_hit;
 
 typedef struct rtg_scene rtg_scene;
@@ -386,7 +386,7 @@ int32_t rtg_scene_object_bvh(const rtg_scene* scene, int32_t object, int32_t* nu
    inverse-transpose, glm column-major, 16 floats each. */
 int32_t rtg_scene_object_matrices(const rtg_scene* scene, int32_t top_object, float* inverse16,
                                   float* inverse_transpose16);
-/* Smooth vertex normals after renderScene's precompute (src/Scene.cpp:433-449): 3*num_vertices. */
+/* Smooth vertex normals after the precompute of renderScene (src/Scene.cpp:294-318): 3*num_vertices. */
 int32_t rtg_scene_vertex_normals(const rtg_scene* scene, float* normals);
 
 #ifdef __cplusplus

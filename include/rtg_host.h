@@ -4,13 +4,13 @@
  * scene file goes from XML to images without Python (`rtg_cli scene.xml`, the reference's
  * `./raytracer scene.xml`, src/main.cpp:7-14).
  *
- *   rtgh_parse_xml      replaces  new Scene(xml) -> Parser::Parse* (src/Scene.cpp:586-634,
+ *   rtgh_parse_xml      replaces  new Scene(xml) -> Parser::Parse* (src/Scene.cpp:455-504,
  *                                 src/Parser.h:17-1315) and yields the rtg_scene_desc that
  *                                 rtg_scene_create consumes, plus the cameras
- *   rtgh_save_image     replaces  Image::saveImage (src/Image.cpp:186-263: P3 text when the
+ *   rtgh_save_image     replaces  Image::saveImage (src/Image.cpp:26-107: P3 text when the
  *                                 name contains ".png", else OpenEXR HALF via
- *                                 src/Helper.cpp:415-466)
- *   rtgh_render_scene   replaces  Scene::renderScene (src/Scene.cpp:425-494) end to end
+ *                                 src/Helper.cpp:361-412)
+ *   rtgh_render_scene   replaces  Scene::renderScene (src/Scene.cpp:294-363) end to end
  */
 #ifndef RTG_HOST_H_
 #define RTG_HOST_H_

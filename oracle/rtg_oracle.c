@@ -19,11 +19,11 @@
  *    (float)f64(x) — the correctly rounded value; the reference's glibc float functions
  *    agree with it to <= 1 ulp.  pow(float,int) is a double pow, as in the reference.
  *  - Undefined behaviour is given a fixed meaning: a miss's hit point is (0,0,0)
- *    (src/Helper.cpp:75 `ReturnVal nearestRet = {}` leaves Eigen storage uninitialised);
+ *    (src/Helper.cpp:21 `ReturnVal nearestRet = {}` leaves Eigen storage uninitialised);
  *    Ray::gett falling off its end returns NaN (src/Ray.cpp:21-36); stand-alone
  *    triangles/spheres have textureOffset 0; out-of-range texcoords read (0,0).
  *  - RNG: the reference draws from std::mt19937 seeded by std::random_device (racing
- *    threads, src/Scene.cpp:633, Camera.cpp:59-60, Light.cpp:661-666).  This restatement
+ *    threads, src/Scene.cpp:502-503, Camera.cpp:59-60, Light.cpp:523-528, 555-556).  This restatement
  *    replaces every draw by a counter-based Philox4x32-10 value keyed by
  *    (seed, pixel, sample, ray-tree node, purpose, light, iteration), mapped to float the
  *    way libstdc++'s generate_canonical<float,24> maps one 32-bit draw.
@@ -420,12 +420,12 @@ static const float PERLIN_TABLE[16][3] = {
     {1, 1, 0}, {-1, 1, 0}, {1, -1, 0}, {-1, -1, 0}, {1, 0, 1}, {-1, 0, 1}, {1, 0, -1}, {-1, 0, -1},
     {0, 1, 1}, {0, -1, 1}, {0, 1, -1}, {0, -1, -1}, {1, 1, 0}, {-1, 1, 0}, {0, -1, 1}, {0, -1, -1}};
 static const int PERLIN_SHUFFLED[16] = {12, 7, 15, 6, 11, 0, 4, 9, 13, 3, 14, 8, 2, 5, 1, 10};
-static int perlin_P(int i) { int idx = i % 16; if (idx < 0) idx += 16; return PERLIN_SHUFFLED[idx]; } /* :86-97 */
-static float perlin_weight(float x) {                                   /* :27-30 */
+static int perlin_P(int i) { int idx = i % 16; if (idx < 0) idx += 16; return PERLIN_SHUFFLED[idx]; } /* Perlin.cpp:86-97 */
+static float perlin_weight(float x) {                                   /* Perlin.cpp:27-30 */
     double xd = (double)fabsf(x);
     return (float)((((-6) * pow(xd, 5)) + (15 * pow(xd, 4))) - (10 * pow(xd, 3)) + 1);
 }
-static float perlin_compute(v3 p, float scale, int nc) {                /* :52-84 */
+static float perlin_compute(v3 p, float scale, int nc) {                /* Perlin.cpp:52-84 */
     v3 pt = vmul(p, scale);
     int ii = (int)floorf(pt.x), jj = (int)floorf(pt.y), kk = (int)floorf(pt.z);
     float value = 0;
@@ -443,7 +443,7 @@ static float perlin_compute(v3 p, float scale, int nc) {                /* :52-8
     else if (nc == RTG_NC_ABSVAL) value = fabsf(value);
     return value;
 }
-static v3 perlin_gradient(v3 p, float scale, int nc) {                  /* :36-50 */
+static v3 perlin_gradient(v3 p, float scale, int nc) {                  /* Perlin.cpp:36-50 */
     const float eps = 0.001f;
     v3 xe = p, ye = p, ze = p;
     xe.x += eps; ye.y += eps; ze.z += eps;
@@ -455,7 +455,7 @@ static v3 perlin_gradient(v3 p, float scale, int nc) {                  /* :36-5
 }
 
 /* ------------------------------------------------------------------ geometry helpers */
-/* GeometryHelpers::GetAbsSmallestIndex / GetOrthonormalUVector, src/Helper.cpp:322-343 */
+/* GeometryHelpers::GetAbsSmallestIndex / GetOrthonormalUVector, src/Helper.cpp:322-342 */
 static v3 ortho_u(v3 v) {
     float a0 = fabsf(v.x), a1 = fabsf(v.y), a2 = fabsf(v.z);
     int idx = 2;
@@ -471,7 +471,7 @@ static v3 m_xform(const mat4* m, v3 v, float w) {
     m_mulv(m, in, out);
     return V(out[0], out[1], out[2]);
 }
-/* Transforming::TransformRay, src/Helper.cpp:164-187 */
+/* Transforming::TransformRay, src/Helper.cpp:110-133 */
 static Ray transform_ray(const Ray* ray, const mat4* M, v3 blur) {
     v3 b = V(blur.x * ray->time, blur.y * ray->time, blur.z * ray->time);
     v3 o = ray->origin;
@@ -482,7 +482,7 @@ static Ray transform_ray(const Ray* ray, const mat4* M, v3 blur) {
     r.direction = m_xform(M, ray->direction, 0.0f);
     return r;
 }
-/* Transforming::TransformNormal, src/Helper.cpp:154-162 (w = 1) */
+/* Transforming::TransformNormal, src/Helper.cpp:100-108 (w = 1) */
 static v3 transform_normal(v3 n, const mat4* IT) { return vnormalized(m_xform(IT, n, 1.0f)); }
 
 /* ------------------------------------------------------------------ primitive intersection */
@@ -500,7 +500,7 @@ static v2 texcoord(const struct orc_scene* s, int idx) {
     return s->texcoords[idx];
 }
 
-/* Sphere::TextureComputation, src/Shape.cpp:516-619 (object-space point/normal) */
+/* Sphere::TextureComputation, src/Shape.cpp:400-503 (object-space point/normal) */
 static void sphere_texture(const struct orc_scene* s, const Obj* o, v3 c, float Rr, RetVal* ret) {
     ret->dm = RTG_DECAL_NONE;
     for (int i = 0; i < o->ntex; i++) {
@@ -552,7 +552,7 @@ static void sphere_texture(const struct orc_scene* s, const Obj* o, v3 c, float 
     }
 }
 
-/* Triangle::TextureComputation, src/Shape.cpp:621-732 */
+/* Triangle::TextureComputation, src/Shape.cpp:505-616 */
 static void triangle_texture(const struct orc_scene* s, const Obj* o, const int* vi, v3 e1, v3 e2,
                              float beta, float gamma, RetVal* ret) {
     ret->dm = RTG_DECAL_NONE;
@@ -608,7 +608,7 @@ static void triangle_texture(const struct orc_scene* s, const Obj* o, const int*
     }
 }
 
-/* Triangle::bvhIntersect, src/Shape.cpp:413-461 */
+/* Triangle::bvhIntersect, src/Shape.cpp:297-345 */
 static RetVal triangle_intersect(const struct orc_scene* s, const Obj* o, int k, const Ray* ray) {
     const int* vi = o->pv + 3 * k;
     v3 a = s->vertices[vi[0] - 1], b = s->vertices[vi[1] - 1], c = s->vertices[vi[2] - 1];
@@ -636,7 +636,7 @@ static RetVal triangle_intersect(const struct orc_scene* s, const Obj* o, int k,
     return ret;
 }
 
-/* Sphere::bvhIntersect, src/Shape.cpp:463-514 */
+/* Sphere::bvhIntersect, src/Shape.cpp:347-398 */
 static RetVal sphere_intersect(const struct orc_scene* s, const Obj* o, int k, const Ray* ray) {
     v3 d = ray->direction, og = ray->origin, c = s->vertices[o->pv[3 * k] - 1];
     float Rr = o->R;
@@ -684,20 +684,20 @@ static float maxOfTwo(float a, float b) { return (a >= b) ? a : b; }
 typedef struct { struct orc_scene* s; Obj* o; int* prims; int nn, cap; } Builder;
 
 static v3 prim_center(const struct orc_scene* s, const Obj* o, int face) {
-    if (o->type == RTG_OBJ_SPHERE) return s->vertices[o->pv[0] - 1];   /* Shape.cpp:180-183 */
-    const int* vi = o->pv + 3 * face;                                   /* Shape.cpp:296-306 */
+    if (o->type == RTG_OBJ_SPHERE) return s->vertices[o->pv[0] - 1];   /* Shape.cpp:64-67 */
+    const int* vi = o->pv + 3 * face;                                   /* Shape.cpp:180-190 */
     v3 a = s->vertices[vi[0] - 1], b = s->vertices[vi[1] - 1], c = s->vertices[vi[2] - 1];
     return V(((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f);
 }
 static void prim_box(const struct orc_scene* s, const Obj* o, int face, v3* mn, v3* mx) {
-    if (o->type == RTG_OBJ_SPHERE) {                                    /* Shape.cpp:171-178 */
+    if (o->type == RTG_OBJ_SPHERE) {                                    /* Shape.cpp:55-62 */
         v3 c = s->vertices[o->pv[0] - 1];
         float Rr = o->R;
         *mn = V(c.x - Rr, c.y - Rr, c.z - Rr);
         *mx = V(c.x + Rr, c.y + Rr, c.z + Rr);
         return;
     }
-    const int* vi = o->pv + 3 * face;                                   /* Shape.cpp:278-294 */
+    const int* vi = o->pv + 3 * face;                                   /* Shape.cpp:162-178 */
     v3 a = s->vertices[vi[0] - 1], b = s->vertices[vi[1] - 1], c = s->vertices[vi[2] - 1];
     *mn = V(minOfThree(a.x, b.x, c.x), minOfThree(a.y, b.y, c.y), minOfThree(a.z, b.z, c.z));
     *mx = V(maxOfThree(a.x, b.x, c.x), maxOfThree(a.y, b.y, c.y), maxOfThree(a.z, b.z, c.z));
@@ -713,7 +713,7 @@ static int new_node(Builder* B) {
     }
     return B->nn++;
 }
-/* BVH::ConstructionHelper, src/BVH.cpp:64-110 ; FindMedian :117-135 ; ComputeBoundingBox :268-283 */
+/* BVH::ConstructionHelper, src/BVH.cpp:64-110 ; FindMedian BVH.cpp:117-135 ; ComputeBoundingBox BVH.cpp:268-283 */
 static int construct(Builder* B, int start, int end, int splitType, int depth) {
     if (start == end - 1 || depth >= 30) {
         int n = new_node(B);
@@ -817,7 +817,7 @@ static RetVal bvh_find(const struct orc_scene* s, const Obj* o, const Ray* ray, 
     return ret_empty();
 }
 
-/* BVHMethods::FindIntersection, src/Helper.cpp:72-134 */
+/* BVHMethods::FindIntersection, src/Helper.cpp:18-80 */
 static RetVal find_intersection(const struct orc_scene* s, const Ray* ray) {
     RetVal nearest = ret_empty();
     float nearestDistance = FLT_MAX;
@@ -865,7 +865,7 @@ static RetVal find_intersection(const struct orc_scene* s, const Ray* ray) {
 static const rtg_material_desc* MAT(const struct orc_scene* s, int matIndex) { return &s->mats[matIndex - 1]; }
 static v3 mv(const float f[3]) { return V(f[0], f[1], f[2]); }
 
-/* Light::Fresnel / Scene::ConductorFresnel, src/Light.cpp:156-166, src/Scene.cpp:266-277 */
+/* Scene::ConductorFresnel, src/Scene.cpp:135-146 (the same formula as Light::Fresnel, src/Light.cpp:18-28) */
 static float conductor_fresnel(float n_t, float k_t, v3 ray, v3 normal) {
     float cos_t = -vdot(ray, normal);
     float twoNtCost = (2 * n_t) * cos_t;
@@ -875,7 +875,7 @@ static float conductor_fresnel(float n_t, float k_t, v3 ray, v3 normal) {
     float rp = ((ntk * cosSquared - twoNtCost) + 1) / ((ntk * cosSquared + twoNtCost) + 1);
     return 0.5f * (rs + rp);
 }
-/* Light::GeometryTS :187-198, DistributionTS :150-154 */
+/* Light::GeometryTS Light.cpp:49-60, DistributionTS Light.cpp:12-16 */
 static float geometry_ts(v3 wi, v3 wo, v3 wh, v3 n) {
     float left = (2.0f * vdot(n, wh)) * vdot(n, wo);
     left = left / vdot(wo, wh);
@@ -889,7 +889,7 @@ static float distribution_ts(float cosAlpha, int phongExp) {
     x = (float)((double)x * pow((double)cosAlpha, phongExp));
     return x;
 }
-/* Light::TermBRDF, src/Light.cpp:200-293 */
+/* Light::TermBRDF, src/Light.cpp:62-155 */
 static v3 term_brdf(v3 wi, v3 wo, const RetVal* ret, const rtg_material_desc* m) {
     v3 n = ret->normal, kd = mv(m->diffuse), ks = mv(m->specular);
     int p = m->phong_exp;
@@ -948,13 +948,13 @@ static v3 term_brdf(v3 wi, v3 wo, const RetVal* ret, const rtg_material_desc* m)
         return V(0, 0, 0);
     }
 }
-/* Light::BRDF :295-300 */
+/* Light::BRDF Light.cpp:157-162 */
 static v3 brdf(v3 wi, v3 wo, const RetVal* ret, v3 radiance, const rtg_material_desc* m) {
     v3 t = term_brdf(wi, wo, ret, m);
     float cosAngle = fmax0(vdot(wi, ret->normal));
     return vmul(vcw(radiance, t), cosAngle);
 }
-/* Diffuse kd selection shared by all lights (e.g. PointLight::Diffuse :344-361) */
+/* Diffuse kd selection shared by all lights (e.g. PointLight::Diffuse Light.cpp:206-223) */
 static v3 diffuse_term(v3 LC, const RetVal* ret, const rtg_material_desc* m, float alpha) {
     if (ret->dm == RTG_DECAL_REPLACE_KD)
         return vcw(LC, vmul(vdivs(ret->textureColor, ret->textureNormalizer), alpha));
@@ -978,7 +978,7 @@ static RetVal trace(Ctx* cx, const Ray* r, int kind) {
     return find_intersection(cx->s, r);
 }
 
-/* distance-compared shadow test of Point/Spot/Area lights, e.g. PointLight::IsShadow :326-342 */
+/* distance-compared shadow test of Point/Spot/Area lights, e.g. PointLight::IsShadow Light.cpp:188-204 */
 static int shadow_towards(Ctx* cx, const Ray* prime, const RetVal* ret, v3 L) {
     struct orc_scene* s = cx->s;
     v3 dir = vsub(L, ret->point);
@@ -994,7 +994,7 @@ static int shadow_dir(Ctx* cx, const Ray* prime, const RetVal* ret, v3 dir) {
     return nr.full;
 }
 
-/* EnvironmentLight::ComputeLightContribution :701-713 */
+/* EnvironmentLight::ComputeLightContribution Light.cpp:563-575 */
 static v3 env_radiance(const struct orc_scene* s, const Lgt* L, v3 direction) {
     float theta = f_acos(direction.y);
     float phi = f_atan2(direction.z, direction.x);
@@ -1010,7 +1010,7 @@ static v3 light_shading(Ctx* cx, int li, const Ray* prime, const RetVal* ret, co
     const Lgt* L = &s->lights[li];
     v3 wo = vneg(prime->direction);
     switch (L->type) {
-    case RTG_LIGHT_POINT: {                                   /* PointLight::BasicShading :376-388 */
+    case RTG_LIGHT_POINT: {                                   /* PointLight::BasicShading Light.cpp:238-250 */
         if (shadow_towards(cx, prime, ret, L->pos)) return V(0, 0, 0);
         float dist = vnorm(vsub(ret->point, L->pos));
         v3 LC = vdivs(L->inten, dist * dist);
@@ -1019,14 +1019,14 @@ static v3 light_shading(Ctx* cx, int li, const Ray* prime, const RetVal* ret, co
         float alpha = fmax0(vdot(ret->normal, wi));
         return vadd(diffuse_term(LC, ret, m, alpha), specular_term(LC, wo, wi, ret, m));
     }
-    case RTG_LIGHT_DIRECTIONAL: {                             /* DirectionalLight::BasicShading :447-459 */
+    case RTG_LIGHT_DIRECTIONAL: {                             /* DirectionalLight::BasicShading Light.cpp:309-321 */
         v3 wi = vneg(L->dir);
         if (shadow_dir(cx, prime, ret, wi)) return V(0, 0, 0);
         if (m->brdf != RTG_BRDF_NONE) return brdf(wi, wo, ret, L->inten, m);
         float alpha = fmax0(vdot(ret->normal, wi));
         return vadd(diffuse_term(L->inten, ret, m, alpha), specular_term(L->inten, wo, wi, ret, m));
     }
-    case RTG_LIGHT_SPOT: {                                    /* SpotLight::BasicShading :547-574 */
+    case RTG_LIGHT_SPOT: {                                    /* SpotLight::BasicShading Light.cpp:409-436 */
         if (shadow_towards(cx, prime, ret, L->pos)) return V(0, 0, 0);
         v3 dtp = vnormalized(vsub(ret->point, L->pos));
         float angle = f_acos(vdot(dtp, L->dir));
@@ -1042,16 +1042,16 @@ static v3 light_shading(Ctx* cx, int li, const Ray* prime, const RetVal* ret, co
         }
         if (angle < L->fall) return c;
         float cf = f_cos(L->fall), cc = f_cos(L->coverage);
-        float fo = (float)pow((cos((double)angle) - (double)cc) / (double)(cf - cc), 4);   /* FallOf :481-486 */
+        float fo = (float)pow((cos((double)angle) - (double)cc) / (double)(cf - cc), 4);   /* FallOf Light.cpp:343-348 */
         return vmul(c, fo);
     }
-    case RTG_LIGHT_AREA: {                                    /* AreaLight::BasicShading :660-683 */
+    case RTG_LIGHT_AREA: {                                    /* AreaLight::BasicShading Light.cpp:522-545 */
         float xi[4];
         rng4(cx->rng.seed, cx->rng.pixel, cx->rng.sample, path, RNG_AREA, (uint32_t)li, 0, xi);
         float uChi = xi[0] - 0.5f, vChi = xi[1] - 0.5f;
         v3 sample = vadd(vadd(L->pos, vmul(vmul(L->u, L->size), uChi)), vmul(vmul(L->v, L->size), vChi));
         if (shadow_towards(cx, prime, ret, sample)) return V(0, 0, 0);
-        /* FindAreaFactor :595-601 */
+        /* FindAreaFactor Light.cpp:457-463 */
         v3 pms = vsub(ret->point, sample);
         float cosTheta = fabsf(vdot(vnormalized(pms), L->normal));
         float dSq = vnorm(pms);
@@ -1062,7 +1062,7 @@ static v3 light_shading(Ctx* cx, int li, const Ray* prime, const RetVal* ret, co
         float alpha = fmax0(vdot(ret->normal, wi));
         return vadd(diffuse_term(LC, ret, m, alpha), specular_term(LC, wo, wi, ret, m));
     }
-    case RTG_LIGHT_ENVIRONMENT: {                             /* EnvironmentLight::BasicShading :766-798 */
+    case RTG_LIGHT_ENVIRONMENT: {                             /* EnvironmentLight::BasicShading Light.cpp:628-660 */
         v3 n = ret->normal;
         v3 u = ortho_u(n);
         v3 w = vcross(n, u);
@@ -1086,7 +1086,7 @@ static v3 light_shading(Ctx* cx, int li, const Ray* prime, const RetVal* ret, co
     return V(0, 0, 0);
 }
 
-/* Scene::BasicShading :374-398 with Scene::ambient :153-161 */
+/* Scene::BasicShading Scene.cpp:243-267 with Scene::ambient Scene.cpp:22-30 */
 static v3 basic_shading(Ctx* cx, const Ray* ray, const RetVal* ret, const rtg_material_desc* m, uint64_t path) {
     struct orc_scene* s = cx->s;
     v3 raw = vadd(V(0, 0, 0), vcw(s->ambientLight, mv(m->ambient)));
@@ -1097,7 +1097,7 @@ static v3 basic_shading(Ctx* cx, const Ray* ray, const RetVal* ret, const rtg_ma
 /* ------------------------------------------------------------------ integrator (src/Scene.cpp) */
 typedef struct { Ray ray; RetVal ret; } ShadeComp;
 
-/* Scene::MirrorReflectance :163-186 (path = node whose reflection this is) */
+/* Scene::MirrorReflectance Scene.cpp:32-55 (path = node whose reflection this is) */
 static ShadeComp mirror_reflectance(Ctx* cx, const Ray* ray, const RetVal* ret, const rtg_material_desc* m,
                                     uint64_t path) {
     struct orc_scene* s = cx->s;
@@ -1119,11 +1119,11 @@ static ShadeComp mirror_reflectance(Ctx* cx, const Ray* ray, const RetVal* ret, 
     return sc;
 }
 
-static v3 nan_check(v3 c) { return visnan(c) ? V(0, 0, 0) : c; }   /* :352-359 */
+static v3 nan_check(v3 c) { return visnan(c) ? V(0, 0, 0) : c; }   /* Scene.cpp:221-228 */
 
 static v3 recursive_shading(Ctx* cx, const Ray* ray, const RetVal* ret, int depth, uint64_t path);
 
-/* Scene::DielectricRefraction :188-249 + FresnelReflectance :251-259 + BeerLaw :261-264 */
+/* Scene::DielectricRefraction Scene.cpp:57-118 + FresnelReflectance Scene.cpp:120-128 + BeerLaw Scene.cpp:130-133 */
 static v3 dielectric(Ctx* cx, const Ray* ray, const RetVal* ret, const rtg_material_desc* m, int depth, uint64_t path) {
     struct orc_scene* s = cx->s;
     float dp = vdot(ray->direction, ret->normal);
@@ -1179,7 +1179,7 @@ static v3 dielectric(Ctx* cx, const Ray* ray, const RetVal* ret, const rtg_mater
     return vadd(outside, refl);
 }
 
-/* Scene::RecursiveShading :279-350 */
+/* Scene::RecursiveShading Scene.cpp:148-219 */
 static v3 recursive_shading(Ctx* cx, const Ray* ray, const RetVal* ret, int depth, uint64_t path) {
     if (!ret->full) return V(0, 0, 0);
     const rtg_material_desc* m = MAT(cx->s, ret->matIndex);
@@ -1200,13 +1200,13 @@ static v3 recursive_shading(Ctx* cx, const Ray* ray, const RetVal* ret, int dept
     return vadd(basic_shading(cx, ray, ret, m, path), rc);
 }
 
-/* Scene::Shading :361-372 */
+/* Scene::Shading Scene.cpp:230-241 */
 static v3 shading(Ctx* cx, const Ray* ray, const RetVal* ret) {
     if (ret->dm == RTG_DECAL_REPLACE_ALL) return ret->textureColor;
     return recursive_shading(cx, ray, ret, cx->s->maxDepth, 1);
 }
 
-/* Scene::GetBackgroundColor :544-566 */
+/* Scene::GetBackgroundColor Scene.cpp:413-435 */
 static v3 background(const struct orc_scene* s, int row, int col, int nx, int ny, const Ray* ray) {
     if (s->envLight != -1) {
         const Lgt* L = &s->lights[s->envLight];
@@ -1333,7 +1333,7 @@ static v3 pt_sample(Ctx* cx, Ray ray, int flags, v3 bg) {
         }
         if (b == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) { L = vadd(L, vcw(T, ret.textureColor)); break; }
         const rtg_material_desc* m = MAT(s, ret.matIndex);
-        /* dielectric geometry (Scene::DielectricRefraction :188-249) */
+        /* dielectric geometry (Scene::DielectricRefraction Scene.cpp:57-118) */
         int entering = 1, isTir = 0;
         float F = 0.0f;
         v3 tdir = V(0, 0, 0), torg = V(0, 0, 0);
@@ -1385,7 +1385,7 @@ static v3 pt_sample(Ctx* cx, Ray ray, int flags, v3 bg) {
             next = R(torg, tdir, ray.time);
             nmedium = entering ? ret.matIndex : 0;
         } else {
-            /* mirror / conductor / dielectric reflection: Scene::MirrorReflectance :163-186 */
+            /* mirror / conductor / dielectric reflection: Scene::MirrorReflectance Scene.cpp:32-55 */
             v3 wo = vneg(ray.direction);
             float n_wo = vdot(ret.normal, wo);
             v3 wr = vadd(vneg(wo), vmul(vmul(ret.normal, 2), n_wo));
@@ -1425,7 +1425,7 @@ typedef struct {
     int dof; float focus, aperture;
 } Cam;
 
-static void cam_init(Cam* c, const rtg_camera_desc* d) {          /* Camera::Camera :7-61 */
+static void cam_init(Cam* c, const rtg_camera_desc* d) {          /* Camera::Camera Camera.cpp:7-61 */
     int i = 1;
     c->sampleCount = 1;
     while (i < 1000) { if (i * i >= d->num_samples) { c->sampleCount = i; break; } i++; }
@@ -1446,7 +1446,7 @@ static void cam_init(Cam* c, const rtg_camera_desc* d) {          /* Camera::Cam
     c->total = d->num_samples;
     c->dof = d->is_dof; c->focus = d->focus_distance; c->aperture = d->aperture_size;
 }
-static Ray cam_primary(const Cam* c, int col, int row) {          /* getPrimaryRay :63-72 */
+static Ray cam_primary(const Cam* c, int col, int row) {          /* getPrimaryRay Camera.cpp:63-72 */
     float u = c->l + ((c->r - c->l) * (col + 0.5f)) * c->nxDA;
     float v = c->t - ((c->t - c->b) * (row + 0.5f)) * c->nyDA;
     v3 m = vadd(c->pos, vmul(c->gaze, c->dist));
@@ -1455,7 +1455,7 @@ static Ray cam_primary(const Cam* c, int col, int row) {          /* getPrimaryR
     v3 d = vsub(m, c->pos);
     return R(c->pos, vdivs(d, vnorm(d)), 0);
 }
-static v3 cam_lb(const Cam* c, int row, int col) {                /* PixelLBCorner :84-92 */
+static v3 cam_lb(const Cam* c, int row, int col) {                /* PixelLBCorner Camera.cpp:84-92 */
     float u = c->l + (float)col * c->pw;
     float v = c->t - (float)(row + 1) * c->ph;
     v3 m = vadd(c->pos, vmul(c->gaze, c->dist));
@@ -1463,14 +1463,14 @@ static v3 cam_lb(const Cam* c, int row, int col) {                /* PixelLBCorn
     m = vadd(m, vmul(c->up, v));
     return m;
 }
-static Ray cam_sample(const Cam* c, v3 lb, int si, const float xi[4]) {   /* getSampleRay :94-113 */
+static Ray cam_sample(const Cam* c, v3 lb, int si, const float xi[4]) {   /* getSampleRay Camera.cpp:94-113 */
     int i = si % c->sampleCount, j = si / c->sampleCount;
     v3 m = lb;
     m = vadd(m, vmul(c->right, ((float)i + xi[0]) * c->sw));
     m = vadd(m, vmul(c->up, ((float)j + xi[1]) * c->sh));
     v3 d = vsub(m, c->pos);
     Ray ray = R(c->pos, vdivs(d, vnorm(d)), 0);
-    if (c->dof) {                                                   /* AddDepthOfField :119-139 */
+    if (c->dof) {                                                   /* AddDepthOfField Camera.cpp:119-139 */
         float xa = xi[2] - 0.5f, xb = xi[3] - 0.5f;
         v3 q = c->pos;
         q = vadd(q, vmul(c->right, c->aperture * xa));
@@ -1485,7 +1485,7 @@ static Ray cam_sample(const Cam* c, v3 lb, int si, const float xi[4]) {   /* get
 }
 
 /* ------------------------------------------------------------------ scene construction */
-static mat4 compose(const rtg_scene_desc* d, int first, int count) {   /* Helper.cpp:200-231 */
+static mat4 compose(const rtg_scene_desc* d, int first, int count) {   /* Helper.cpp:146-183 */
     mat4 M = m_identity();
     for (int j = count - 1; j >= 0; j--) {
         const rtg_xform_ref* x = &d->xform_refs[first + j];
@@ -1558,11 +1558,11 @@ int orc_scene_create(const rtg_scene_desc* d, orc_scene** out) {
         L->type = l->type; L->pos = mv(l->position); L->inten = mv(l->intensity); L->tex = l->texture;
         L->size = l->size;
         if (l->type == RTG_LIGHT_DIRECTIONAL || l->type == RTG_LIGHT_SPOT) L->dir = vnormalized(mv(l->direction));
-        if (l->type == RTG_LIGHT_SPOT) {                             /* SpotLight ctor :465-474 */
+        if (l->type == RTG_LIGHT_SPOT) {                             /* SpotLight ctor Light.cpp:327-336 */
             L->coverage = (float)((double)(l->coverage_deg * 0.5f) * (PI_D / 180.0f));
             L->fall = (float)((double)(l->falloff_deg * 0.5f) * (PI_D / 180.0f));
         }
-        if (l->type == RTG_LIGHT_AREA) {                             /* AreaLight ctor :580-593 */
+        if (l->type == RTG_LIGHT_AREA) {                             /* AreaLight ctor Light.cpp:442-455 */
             L->normal = vnormalized(mv(l->direction));
             L->u = ortho_u(L->normal);
             L->v = vcross(L->normal, L->u);
@@ -1602,7 +1602,7 @@ int orc_scene_create(const rtg_scene_desc* d, orc_scene** out) {
         in->base = id->base_object; in->matIndex = id->material; in->reset = id->reset_transform;
         in->blur = mv(id->blur);
         in->model = compose(d, id->xform_first, id->xform_count);
-        if (!in->reset) in->model = m_mul(&in->model, &s->objs[in->base].model);   /* Helper.cpp:270-272 */
+        if (!in->reset) in->model = m_mul(&in->model, &s->objs[in->base].model);   /* Helper.cpp:216-218 */
         in->inv = m_inverse(&in->model);
         in->invT = m_inverse_transpose(&in->model);
     }
@@ -1644,7 +1644,7 @@ int orc_scene_create(const rtg_scene_desc* d, orc_scene** out) {
             E->area = acc;
         }
     }
-    /* smooth vertex normals, src/Scene.cpp:433-449, Shape.cpp:378-406 */
+    /* smooth vertex normals, src/Scene.cpp:302-318, Shape.cpp:262-290 */
     s->vnormals = (v3*)calloc(s->nv ? s->nv : 1, sizeof(v3));
     for (int i = 0; i < s->nobj; i++) {
         Obj* o = &s->objs[i];
@@ -1658,7 +1658,7 @@ int orc_scene_create(const rtg_scene_desc* d, orc_scene** out) {
         }
     }
     for (int i = 0; i < s->nv; i++) s->vnormals[i] = vnormalized(s->vnormals[i]);
-    /* BVH per object (Scene.cpp:451-454; BVH(Shape*) BVH.cpp:53-62) */
+    /* BVH per object (Scene.cpp:320-323; BVH(Shape*) BVH.cpp:53-62) */
     for (int i = 0; i < s->nobj; i++) {
         Obj* o = &s->objs[i];
         int n = o->nprims;
@@ -1709,7 +1709,7 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
             uint32_t pixel = (uint32_t)(y * nx + x);
             cx.rng.pixel = pixel;
             v3 color;
-            if (cam.total > 1) {                          /* Scene::MultiSample :517-542 */
+            if (cam.total > 1) {                          /* Scene::MultiSample Scene.cpp:386-411 */
                 v3 lb = cam_lb(&cam, y, x);
                 color = V(0, 0, 0);
                 for (int i = 0; i < cam.total; i++) {
@@ -1727,7 +1727,7 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
                     else color = vadd(color, background(s, y, x, nx, ny, &r));
                 }
                 color = vdivs(color, (float)cam.total);
-            } else {                                      /* Scene::SingleSample :496-515 (row=x, col=y) */
+            } else {                                      /* Scene::SingleSample Scene.cpp:365-384 (row=x, col=y) */
                 cx.rng.sample = 0;
                 Ray r = cam_primary(&cam, x, y);
                 if (pathT) {

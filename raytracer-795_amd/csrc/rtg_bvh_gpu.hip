@@ -141,7 +141,7 @@ __global__ void k_scatter(int n, const int* __restrict__ segid, int S, const Seg
 // Children of every segment: counts of nodes and of interior (next-level) segments.
 __device__ __forceinline__ int child_kind(int len, int depth) {   // 0 null, 1 leaf, 2 interior
     if (len == 1 || depth >= kMaxDepth) return 1;                 // src/BVH.cpp:67-76
-    if (len == 0) return 0;                                       // :77
+    if (len == 0) return 0;                                       // BVH.cpp:77
     return 2;
 }
 __global__ void k_child_count(const Seg* __restrict__ segs, int S, int depth1, const int* __restrict__ G,

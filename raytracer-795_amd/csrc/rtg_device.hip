@@ -1,6 +1,6 @@
 // rtg_device.hip — gfx950 kernels of the wavefront render loop.
 //
-// The reference's recursive per-pixel loop (src/Scene.cpp:279-350, 400-423, 496-542) is
+// The reference's recursive per-pixel loop (src/Scene.cpp:148-219, 269-292, 365-411) is
 // flattened into levels: raygen -> [trace -> shade -> shadow] per ray-tree level ->
 // bottom-up resolve -> in-order sample accumulation.  Every floating-point expression
 // follows the reference's evaluation order (compiled with -ffp-contract=off and correctly
@@ -181,7 +181,7 @@ DEV float det3(f3 c0, f3 c1, f3 c2) {
     return (h0 - h1) + h2;
 }
 
-struct Cand {           // Triangle::bvhIntersect acceptance + point (src/Shape.cpp:413-461)
+struct Cand {           // Triangle::bvhIntersect acceptance + point (src/Shape.cpp:297-345)
     bool ok;
     float beta, gamma, t;
     f3 p;
@@ -219,7 +219,7 @@ DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps) {
     c.p = o + d * c.t;
     return c;
 }
-// Sphere::bvhIntersect root selection (src/Shape.cpp:463-507)
+// Sphere::bvhIntersect root selection (src/Shape.cpp:347-391)
 DEV bool sphere_test(f3 o, f3 d, f3 c, float R, float eps, f3& ip) {
     f3 oc = o - c;
     float dd = dot(d, oc);
@@ -243,7 +243,7 @@ DEV float gett(f3 o, f3 d, f3 p) {
     t = (p.z - o.z) / d.z;
     return t;
 }
-// Transforming::TransformRay (src/Helper.cpp:164-187)
+// Transforming::TransformRay (src/Helper.cpp:110-133)
 DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d2) {
     if (T.ident && __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z) &&
         __builtin_isfinite(d.x) && __builtin_isfinite(d.y) && __builtin_isfinite(d.z) && __builtin_isfinite(time)) {
@@ -568,7 +568,7 @@ DEV f3 tex_pixel(const SceneView& sv, const TextureDev& t, int i, int j) {   // 
     const float* p = sv.texels + t.texel_offset + ((long long)j * t.w + i) * 3;
     return mk(p[0], p[1], p[2]);
 }
-DEV f3 tex_color(const SceneView& sv, const TextureDev& t, float u, float v) {   // :111-131
+DEV f3 tex_color(const SceneView& sv, const TextureDev& t, float u, float v) {   // Texture.cpp:111-131
     u = u - floorf(u);
     v = v - floorf(v);
     float i = u * (float)t.w;
@@ -581,7 +581,7 @@ DEV f3 tex_color(const SceneView& sv, const TextureDev& t, float u, float v) {  
     float w00 = (1 - a) * (1 - b), w01 = (1 - a) * b, w10 = a * (1 - b), w11 = a * b;
     return ((c00 * w00 + c01 * w01) + c10 * w10) + c11 * w11;
 }
-DEV void tex_change(const SceneView& sv, const TextureDev& t, float u, float v, float& du, float& dv) {  // :76-109
+DEV void tex_change(const SceneView& sv, const TextureDev& t, float u, float v, float& du, float& dv) {  // Texture.cpp:76-109
     u = u - floorf(u);
     v = v - floorf(v);
     int i = (int)(u * (float)t.w);
@@ -631,7 +631,7 @@ DEV f3 perlin_gradient(f3 p, float scale, int nc) {     // src/Perlin.cpp:36-50
     return mk((perlin_compute(xe, scale, nc) - o) / eps, (perlin_compute(ye, scale, nc) - o) / eps,
               (perlin_compute(ze, scale, nc) - o) / eps);
 }
-DEV f3 ortho_u(f3 v) {                                  // src/Helper.cpp:322-343
+DEV f3 ortho_u(f3 v) {                                  // src/Helper.cpp:322-342
     float a0 = fabsf(v.x), a1 = fabsf(v.y), a2 = fabsf(v.z);
     f3 nl = v;
     if (a0 <= a1 && a0 <= a2) nl.x = 1.0f;
@@ -666,7 +666,7 @@ DEV void perlin_decal(const TextureDev& t, Ret& ret) {
         ret.normal = normalized(ret.normal);
     }
 }
-// Sphere::TextureComputation, src/Shape.cpp:516-619
+// Sphere::TextureComputation, src/Shape.cpp:400-503
 DEV void sphere_texture(const SceneView& sv, const Geometry& g, Ret& ret) {
     ret.dm = RTG_DECAL_NONE;
     f3 c = ld3(g.center);
@@ -710,7 +710,7 @@ DEV void texcoord(const SceneView& sv, int idx, float& u, float& v) {
     if (idx < 0 || idx >= sv.num_texcoords) { u = 0; v = 0; return; }
     u = sv.texcoords[2 * idx]; v = sv.texcoords[2 * idx + 1];
 }
-// Triangle::TextureComputation, src/Shape.cpp:621-732
+// Triangle::TextureComputation, src/Shape.cpp:505-616
 DEV void triangle_texture(const SceneView& sv, const Geometry& g, int4 vi, f3 e1, f3 e2, float beta, float gamma,
                           Ret& ret) {
     ret.dm = RTG_DECAL_NONE;
@@ -757,7 +757,7 @@ DEV void triangle_texture(const SceneView& sv, const Geometry& g, int4 vi, f3 e1
 
 // Re-derive the full ReturnVal of a hit found by closest_hit: the winning primitive's
 // object-space intersection (identical arithmetic), texturing, then the top-level
-// world point and TransformNormal (src/Helper.cpp:93-131).
+// world point and TransformNormal (src/Helper.cpp:39-77).
 // FULL = false: the scene has no textures (the host checks), so texturing is compiled out.
 template <bool FULL = true>
 DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h) {
@@ -803,7 +803,7 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h)
 }
 
 // ------------------------------------------------------------------ lights (src/Light.cpp)
-DEV float conductor_fresnel(float n_t, float k_t, f3 ray, f3 normal) {   // Light.cpp:156-166, Scene.cpp:266-277
+DEV float conductor_fresnel(float n_t, float k_t, f3 ray, f3 normal) {   // Light.cpp:18-28, Scene.cpp:135-146
     float cos_t = -dot(ray, normal);
     float twoNtCost = (2 * n_t) * cos_t;
     float cosSquared = (float)sq_d(cos_t);
@@ -812,7 +812,7 @@ DEV float conductor_fresnel(float n_t, float k_t, f3 ray, f3 normal) {   // Ligh
     float rp = ((ntk * cosSquared - twoNtCost) + 1) / ((ntk * cosSquared + twoNtCost) + 1);
     return 0.5f * (rs + rp);
 }
-DEV float geometry_ts(f3 wi, f3 wo, f3 wh, f3 n) {      // Light.cpp:187-198
+DEV float geometry_ts(f3 wi, f3 wo, f3 wh, f3 n) {      // Light.cpp:49-60
     float left = (2.0f * dot(n, wh)) * dot(n, wo);
     left = left / dot(wo, wh);
     float right = (2.0f * dot(n, wh)) * dot(n, wi);
@@ -820,12 +820,12 @@ DEV float geometry_ts(f3 wi, f3 wo, f3 wh, f3 n) {      // Light.cpp:187-198
     float x = stdmin(left, right);
     return stdmin(1.0f, x);
 }
-DEV float distribution_ts(float cosAlpha, int p) {       // Light.cpp:150-154
+DEV float distribution_ts(float cosAlpha, int p) {       // Light.cpp:12-16
     float x = (float)((double)((float)p + 2.0f) / (double)(2.0f * PI_D));
     x = (float)((double)x * pow((double)cosAlpha, (double)p));
     return x;
 }
-DEV f3 term_brdf(f3 wi, f3 wo, f3 n, const MaterialDev& m) {   // Light.cpp:200-293
+DEV f3 term_brdf(f3 wi, f3 wo, f3 n, const MaterialDev& m) {   // Light.cpp:62-155
     f3 kd = ld3(m.diffuse), ks = ld3(m.specular);
     int p = m.phong_exp;
     switch (m.brdf) {
@@ -878,7 +878,7 @@ DEV f3 term_brdf(f3 wi, f3 wo, f3 n, const MaterialDev& m) {   // Light.cpp:200-
         return mk(0, 0, 0);
     }
 }
-DEV f3 brdf(f3 wi, f3 wo, f3 n, f3 radiance, const MaterialDev& m) {   // Light.cpp:295-300
+DEV f3 brdf(f3 wi, f3 wo, f3 n, f3 radiance, const MaterialDev& m) {   // Light.cpp:157-162
     f3 t = term_brdf(wi, wo, n, m);
     float cosAngle = fmax0(dot(wi, n));
     return cw(radiance, t) * cosAngle;
@@ -900,7 +900,7 @@ DEV f3 phong_or_brdf(f3 LC, f3 wo, f3 wi, const Ret& ret, const MaterialDev& m) 
     float alpha = fmax0(dot(ret.normal, wi));
     return diffuse_term(LC, ret, m, alpha) + specular_term(LC, wo, wi, ret, m);
 }
-DEV f3 env_radiance(const SceneView& sv, const LightDev& L, f3 dir) {   // Light.cpp:701-713
+DEV f3 env_radiance(const SceneView& sv, const LightDev& L, f3 dir) {   // Light.cpp:563-575
     float theta = f_acos(dir.y);
     float phi = f_atan2(dir.z, dir.x);
     float tu = (float)((-(double)phi + PI_D) / (2 * PI_D));
@@ -935,7 +935,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     f3 dir = mk(0, 0, 0), lp = mk(0, 0, 0);
     float mode = 0.0f, tmax = FLT_MAX;
     switch (L.type) {
-    case RTG_LIGHT_POINT: {                                     // PointLight::BasicShading :376-388
+    case RTG_LIGHT_POINT: {                                     // PointLight::BasicShading Light.cpp:238-250
         f3 pos = ld3(L.pos);
         dir = toward(pos, ret.point);
         lp = pos;
@@ -945,13 +945,13 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         c = phong_or_brdf<BRDF>(LC, wo, normalized(pos - ret.point), ret, m);
         break;
     }
-    case RTG_LIGHT_DIRECTIONAL: {                               // :447-459
+    case RTG_LIGHT_DIRECTIONAL: {                               // Light.cpp:309-321
         dir = -ld3(L.dir);
         mode = 2.0f;
         c = phong_or_brdf<BRDF>(ld3(L.inten), wo, dir, ret, m);
         break;
     }
-    case RTG_LIGHT_SPOT: if constexpr (FULL || SPOT) {          // :547-574
+    case RTG_LIGHT_SPOT: if constexpr (FULL || SPOT) {          // Light.cpp:409-436
         f3 pos = ld3(L.pos);
         dir = toward(pos, ret.point);
         lp = pos;
@@ -969,7 +969,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         }
         break;
     }
-    case RTG_LIGHT_AREA: if constexpr (FULL) {                 // :660-683
+    case RTG_LIGHT_AREA: if constexpr (FULL) {                 // Light.cpp:522-545
         float xi[4];
         rng4(seed, pixel, sample, path, RNG_AREA, (uint32_t)li, 0, xi);
         float uChi = xi[0] - 0.5f, vChi = xi[1] - 0.5f;
@@ -986,7 +986,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         c = phong_or_brdf<BRDF>(LC, wo, normalized(smp - ret.point), ret, m);
         break;
     }
-    case RTG_LIGHT_ENVIRONMENT: if constexpr (FULL) {          // :766-798
+    case RTG_LIGHT_ENVIRONMENT: if constexpr (FULL) {          // Light.cpp:628-660
         f3 n = ret.normal;
         f3 u = ortho_u(n);
         f3 w = cross(n, u);
@@ -1061,7 +1061,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     }
     // A query whose unshadowed contribution is exactly +0 in every channel (a light behind
     // the surface with no specular lobe left) need not be traced: blocked, the light adds the
-    // reference's Vector3f(0,0,0) (src/Light.cpp:188-205, 447-459), unblocked it adds c = +0;
+    // reference's Vector3f(0,0,0) (src/Light.cpp:188-204, 270-275), unblocked it adds c = +0;
     // both leave the running sum bit-identical.  -0 / NaN channels keep the query.
     if ((mode == 1.0f || mode == 2.0f) && (__float_as_uint(c.x) | __float_as_uint(c.y) | __float_as_uint(c.z)) == 0u)
         mode = 0.0f;
@@ -1098,7 +1098,7 @@ DEV void slot_pixel(const CameraDev& cam, const PassDev& ps, int slot, uint32_t&
     pixel = (uint32_t)(y * cam.nx + x);
     sample = (uint32_t)(ps.s0 + sl);
 }
-DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f3 dir) {   // Scene.cpp:544-566
+DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f3 dir) {   // Scene.cpp:413-435
     if (sv.env_light != -1) {
         const LightDev& L = sv.lights[sv.env_light];
         if (L.type != RTG_LIGHT_ENVIRONMENT) return ld3(sv.background);
@@ -1127,7 +1127,7 @@ DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int
     f3 o = pos, d;
     float time = 0.0f;
     if (cam.total > 1) {
-        // PixelLBCorner (Camera.cpp:84-92) + getSampleRay (:94-113) + AddDepthOfField (:119-139)
+        // PixelLBCorner (Camera.cpp:84-92) + getSampleRay (Camera.cpp:94-113) + AddDepthOfField (Camera.cpp:119-139)
         float u = cam.l + (float)x * cam.pw;
         float v = cam.t - (float)(y + 1) * cam.ph;
         f3 m = pos + gaze * cam.dist;
@@ -1229,7 +1229,7 @@ DEV RayRec make_ray(f3 o, f3 d, float time) {
     return r;
 }
 
-// Scene::MirrorReflectance (src/Scene.cpp:163-186): reflected ray of node `path`
+// Scene::MirrorReflectance (src/Scene.cpp:32-55): reflected ray of node `path`
 DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialDev& m, uint64_t seed,
                     uint32_t pixel, uint32_t sample, uint64_t path, f3& ro, f3& rd) {
     f3 wo = -dir;
@@ -1299,7 +1299,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
         bool basic = false;
         if (h.obj < 0) {
             if (level == 0) {
-                // SingleSample passes (row=x, col=y) (Scene.cpp:496-511); MultiSample (row=y, col=x)
+                // SingleSample passes (row=x, col=y) (Scene.cpp:365-380); MultiSample (row=y, col=x)
                 f3 bg = !FULL ? ld3(sv.background)
                       : (cam.total > 1) ? background(sv, cam, y, x, d) : background(sv, cam, x, y, d);
                 nd.cr = bg.x; nd.cg = bg.y; nd.cb = bg.z;
@@ -1309,15 +1309,15 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
             Ret ret = hit_record<FULL && TEX>(sv, o, d, time, h);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
-            if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading :361-372
+            if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading Scene.cpp:230-241
                 nd.cr = ret.tc.x; nd.cg = ret.tc.y; nd.cb = ret.tc.z;
             } else {
                 const MaterialDev m = sv.materials[ret.matIndex - 1];
                 int depth = mt.depth;
                 uint64_t p0 = 2 * path, p1 = 2 * path + 1;
-                if (m.type == RTG_MAT_NORMAL || depth <= 0) {            // RecursiveShading :286-289
+                if (m.type == RTG_MAT_NORMAL || depth <= 0) {            // RecursiveShading Scene.cpp:148-158
                     basic = true;
-                } else if (m.type == RTG_MAT_MIRROR) {                   // :290-296
+                } else if (m.type == RTG_MAT_MIRROR) {                   // Scene.cpp:159-165
                     basic = true;
                     nd.kind = NK_MIRROR;
                     f3 ro, rd;
@@ -1326,7 +1326,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                         has1 = true; c1r = make_ray(ro, rd, time);
                         c1m.slot = mt.slot; c1m.path_lo = (unsigned)p1; c1m.path_hi = (unsigned)(p1 >> 32); c1m.depth = depth - 1;
                     }
-                } else if (m.type == RTG_MAT_DIELECTRIC) {               // :297-340, DielectricRefraction :188-249
+                } else if (m.type == RTG_MAT_DIELECTRIC) {               // Scene.cpp:166-209, DielectricRefraction Scene.cpp:57-118
                     float dp = dot(d, ret.normal);
                     float nt = m.refraction_index;
                     float snell, n_t, n_i;
@@ -1359,7 +1359,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                         has1 = true; c1r = make_ray(ro, rd, time);
                         c1m.slot = mt.slot; c1m.path_lo = (unsigned)p1; c1m.path_hi = (unsigned)(p1 >> 32); c1m.depth = depth - 1;
                     }
-                } else {                                                 // conductor :341-349
+                } else {                                                 // conductor Scene.cpp:210-218
                     basic = true;
                     nd.kind = NK_CONDUCTOR;
                     nd.F = conductor_fresnel(m.refraction_index, m.absorption_index, d, ret.normal);
@@ -1371,7 +1371,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                     }
                 }
                 if (basic) {
-                    // Scene::ambient :153-161 (0 + La*ka); the lights are added in order by
+                    // Scene::ambient Scene.cpp:22-30 (0 + La*ka); the lights are added in order by
                     // k_shadow (one light) or k_light_sum (several)
                     f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
@@ -1452,7 +1452,7 @@ struct DielSplit {
     float F;
     f3 tdir, torg;
 };
-DEV DielSplit dielectric_split(const SceneView& sv, f3 d, const Ret& ret, const MaterialDev& m) {   // :188-259
+DEV DielSplit dielectric_split(const SceneView& sv, f3 d, const Ret& ret, const MaterialDev& m) {   // Scene.cpp:57-128
     DielSplit r;
     float dp = dot(d, ret.normal);
     float nt = m.refraction_index;
@@ -1696,7 +1696,7 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const
 // added to the node colour here (col + c or col + 0, as Scene::BasicShading's light loop
 // does); with several, the visibility is recorded and k_light_sum adds them in light order.
 // Each query is a full closest-hit FindIntersection, as Light::IsShadow does
-// (src/Light.cpp:188-205): the distance test below decides blocking.
+// (src/Light.cpp:188-204): the distance test below decides blocking.
 template <bool EXHAUSTIVE, bool STATS>
 __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const SceneView sv,
                                                                        const ShadowPlanes shadows, bool lean,
@@ -1817,12 +1817,12 @@ __global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const Sha
     nodes.col[i] = make_float4(col.x, col.y, col.z, nc.w);
 }
 
-DEV f3 nan_check(f3 c) { return isnan3(c) ? mk(0, 0, 0) : c; }   // Scene::NanCheck :352-359
+DEV f3 nan_check(f3 c) { return isnan3(c) ? mk(0, 0, 0) : c; }   // Scene::NanCheck Scene.cpp:221-228
 
-// Bottom-up combination of RecursiveShading (src/Scene.cpp:279-350): the colour of one node
+// Bottom-up combination of RecursiveShading (src/Scene.cpp:148-219): the colour of one node
 // from its basic shading and its children's (already resolved) colours.
 // Node i of `self` (colour record nc) against its children in `child`.  A missed refracted
-// child's point is (0,0,0) (src/Helper.cpp:75): the child's point plane is read only for hits.
+// child's point is (0,0,0) (src/Helper.cpp:21): the child's point plane is read only for hits.
 DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& self, const NodePlanes& child) {
     const int kind = __float_as_int(nc.w) & 0xFF;
     f3 basic = mk(nc.x, nc.y, nc.z);
@@ -1848,7 +1848,7 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
         res = basic + rc;
     } else {
         float F = nd.F;
-        float bd = norm(q0 - p);                                     // BeerLaw distance :241
+        float bd = norm(q0 - p);                                     // beerDistance Scene.cpp:110
         f3 beer = mk(f_exp(-m.absorption[0] * bd), f_exp(-m.absorption[1] * bd), f_exp(-m.absorption[2] * bd));
         if (kind == NK_DIEL_ENTER) {
             f3 inside = c0 * (1 - F);
@@ -1878,8 +1878,7 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodeP
     nodes.col[i] = make_float4(res.x, res.y, res.z, nc.w);
 }
 
-// Scene::MultiSample sum order: color += sample_i in sample order (src/Scene.cpp:519-540).
-// Scene::MultiSample / SingleSample (src/Scene.cpp:517-542): color += sample_s in sample order.
+// Scene::SingleSample / MultiSample (src/Scene.cpp:365-411): color += sample_s in sample order.
 // A block takes 64 pixels: their samples' colours are staged through LDS with coalesced loads
 // (the slots of a pixel are adjacent; one lane per slot), then one lane per pixel sums them in
 // order.  mode 2: the single sample itself; 1: first chunk (start from 0); 0: continue the

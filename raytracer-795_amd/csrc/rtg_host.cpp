@@ -1,8 +1,8 @@
 // rtg_host.cpp — C ABI of librtg: scene flattening for gfx950 and the wavefront driver.
 //
 // rtg_scene_create() performs what Scene::renderScene() does before its pixel loop
-// (src/Scene.cpp:427-458): transformation matrices with glm's arithmetic
-// (src/Helper.cpp:189-280), smooth vertex normals (src/Shape.cpp:378-406) and one
+// (src/Scene.cpp:296-323): transformation matrices with glm's arithmetic
+// (src/Helper.cpp:135-226), smooth vertex normals (src/Shape.cpp:262-290) and one
 // median-split BVH per object (src/BVH.cpp:53-135) — reproduced bit-for-bit, then
 // linearised into 64-byte child-box nodes and pre-gathered triangles in BVH order.
 // rtg_render() drives the per-level kernels of rtg_device.hip.
@@ -173,7 +173,7 @@ Mat4 inverse_transpose(const Mat4& M) {              // glm::inverseTranspose (g
         for (int r = 0; r < 4; r++) I.c[c][r] = I.c[c][r] / det;
     return I;
 }
-// ComputeObjectTransformations composition (src/Helper.cpp:207-230): reverse list order,
+// ComputeObjectTransformations composition (src/Helper.cpp:135-176): reverse list order,
 // a Composite replaces the accumulated model.
 Mat4 compose(const rtg_scene_desc* d, int first, int count) {
     Mat4 M = identity();
@@ -237,7 +237,7 @@ struct BuildCtx {
     std::vector<float> scratch;
 };
 
-void range_box(BuildCtx& B, int start, int end, float mn[3], float mx[3]) {   // ComputeBoundingBox :268-283
+void range_box(BuildCtx& B, int start, int end, float mn[3], float mx[3]) {   // ComputeBoundingBox BVH.cpp:268-283
     float a0 = FLT_MAX, a1 = FLT_MAX, a2 = FLT_MAX, b0 = -FLT_MAX, b1 = -FLT_MAX, b2 = -FLT_MAX;
     const int* p = B.prims->data();
     for (int i = start; i < end; i++) {
@@ -248,7 +248,7 @@ void range_box(BuildCtx& B, int start, int end, float mn[3], float mx[3]) {   //
     mn[0] = a0; mn[1] = a1; mn[2] = a2; mx[0] = b0; mx[1] = b1; mx[2] = b2;
 }
 
-// BVH::ConstructionHelper (src/BVH.cpp:64-110).  FindMedian's sort (:117-135) is replaced by
+// BVH::ConstructionHelper (src/BVH.cpp:64-110).  FindMedian's sort (BVH.cpp:117-135) is replaced by
 // nth_element selection, which yields the same order statistics.
 int construct(BuildCtx& B, int start, int end, int splitType, int depth) {
     if (start == end - 1 || depth >= 30) {
@@ -605,7 +605,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         s->invT.push_back(inverse_transpose(m));
     }
 
-    // smooth vertex normals (src/Scene.cpp:433-449)
+    // smooth vertex normals (src/Scene.cpp:302-318)
     std::vector<V3> vn(nv, v3(0, 0, 0));
     for (int i = 0; i < d->num_objects; i++) {
         const rtg_object_desc& o = d->objects[i];
@@ -638,13 +638,13 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         int np = (int)(pv.size() / 3);
         std::vector<V3> centers(np), bmin(np), bmax(np);
         for (int k = 0; k < np; k++) {
-            if (o.type == RTG_OBJ_SPHERE) {                            // Shape.cpp:171-183
+            if (o.type == RTG_OBJ_SPHERE) {                            // Shape.cpp:55-67
                 V3 c = verts[o.center - 1];
                 float R = o.radius;
                 centers[k] = c;
                 bmin[k] = v3(c.x - R, c.y - R, c.z - R);
                 bmax[k] = v3(c.x + R, c.y + R, c.z + R);
-            } else {                                                  // Shape.cpp:278-306
+            } else {                                                  // Shape.cpp:162-190
                 V3 a = verts[pv[3 * k] - 1], b = verts[pv[3 * k + 1] - 1], c = verts[pv[3 * k + 2] - 1];
                 centers[k] = v3(((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f);
                 bmin[k] = v3(minOf3(a.x, b.x, c.x), minOf3(a.y, b.y, c.y), minOf3(a.z, b.z, c.z));
@@ -737,7 +737,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 float fi;
                 memcpy(&fi, &f, 4);
                 tg.p2 = make_float4(amc.z, fi, 0.0f, 0.0f);
-                int smooth = (o.type == RTG_OBJ_TRIANGLE) ? 1 : o.smooth;   // Shape.cpp:378-392 quirk
+                int smooth = (o.type == RTG_OBJ_TRIANGLE) ? 1 : o.smooth;   // Shape.cpp:262-276 quirk
                 pi = make_int4(i1, i2, i3, smooth);
                 double e = (double)(ieps > 0 ? ieps : 0.0f);
                 double ext = e * ((double)vnorm(b - a) + (double)vnorm(c - a));
@@ -871,7 +871,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         memcpy(L.pos, l.position, 12); memcpy(L.inten, l.intensity, 12);
         L.size = l.size; L.tex = l.texture;
         V3 dir = v3(l.direction[0], l.direction[1], l.direction[2]);
-        if (l.type == RTG_LIGHT_DIRECTIONAL || l.type == RTG_LIGHT_SPOT) {   // Light.cpp:394-398, 465-474
+        if (l.type == RTG_LIGHT_DIRECTIONAL || l.type == RTG_LIGHT_SPOT) {   // Light.cpp:256-260, 327-336
             V3 n = normalized(dir);
             L.dir[0] = n.x; L.dir[1] = n.y; L.dir[2] = n.z;
         }
@@ -881,7 +881,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             L.cos_fall = (float)cos((double)L.fall);
             L.cos_cov = (float)cos((double)L.coverage);
         }
-        if (l.type == RTG_LIGHT_AREA) {                                      // Light.cpp:580-593
+        if (l.type == RTG_LIGHT_AREA) {                                      // Light.cpp:442-455
             V3 n = normalized(dir);
             float a0 = fabsf(n.x), a1 = fabsf(n.y), a2 = fabsf(n.z);
             V3 nl = n;
@@ -1130,7 +1130,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     Counters* sctr = o.collect_stats ? d_stats : nullptr;
 
     // the frame's passes: pixel ranges (outer) x sample chunks (inner); all chunks of one pixel
-    // range go to the same lane, in order (MultiSample's in-order sum, src/Scene.cpp:519-540)
+    // range go to the same lane, in order (the in-order sum of MultiSample, src/Scene.cpp:386-409)
     std::vector<PassDev> plist;
     for (int p0 = 0; p0 < npix; p0 += np_pass)
         for (int s0 = 0; s0 < total; s0 += ns_chunk) {

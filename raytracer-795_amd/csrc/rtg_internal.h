@@ -18,7 +18,7 @@ constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:5
 constexpr int kTraceBlock = 64;     // threads per traversal block (LDS stack: 128 B per lane)
 constexpr int kShadeBlock = 512;    // k_shade (simple variants): one queue atomic per block
 
-// One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:86-127):
+// One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:32-73):
 // objects first, then instances.  Read with scalar loads (wave-uniform loop).
 struct TopObject {
     float inv[16];          // glm::inverse(model), column-major
@@ -80,7 +80,7 @@ struct Node4 {
 };
 
 // Triangle in BVH order: the Cramer-rule operands of Triangle::bvhIntersect
-// (src/Shape.cpp:415-432): a, a-b, a-c.  w lanes: x = original face index.
+// (src/Shape.cpp:299-316): a, a-b, a-c.  w lanes: x = original face index.
 struct TriGeom {
     float4 p0;  // a.xyz, (a-b).x
     float4 p1;  // (a-b).yz, (a-c).xy
@@ -220,7 +220,7 @@ enum NodeKind : int {
 };
 
 struct NodeRec {        // 48 B, one per traced ray
-    float px, py, pz;   // world hit point ((0,0,0) on a miss, src/Helper.cpp:75)
+    float px, py, pz;   // world hit point ((0,0,0) on a miss, src/Helper.cpp:21)
     float cr, cg, cb;   // basic shading, then the resolved color
     int kind;
     float F;            // dielectric Fresnel / conductor Fresnel

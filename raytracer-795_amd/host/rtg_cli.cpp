@@ -6,7 +6,7 @@
 //
 // --devices G renders every camera on G GPUs (device N and the next G-1): one host thread per
 // GPU, row-block pixel shards, RCCL gather of the rows onto device N -- the reference's
-// renderScene fork over 8 std::threads (src/Scene.cpp:340-356) moved to GPUs.
+// renderScene fork over 8 std::threads (src/Scene.cpp:294-363, threads at 340-356) moved to GPUs.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>

@@ -1,6 +1,6 @@
 // scene_io.cpp — native host side of the drop-in: the reference's Parser (src/Parser.h),
-// Image::saveImage (src/Image.cpp:186-263, src/Helper.cpp:415-466) and renderScene's camera
-// loop (src/Scene.cpp:425-494), in C++ above the C ABI of include/rtg.h.
+// Image::saveImage (src/Image.cpp:26-107, src/Helper.cpp:361-412) and renderScene's camera
+// loop (src/Scene.cpp:294-363), in C++ above the C ABI of include/rtg.h.
 //
 // The parse follows src/Parser.h function by function (file:line cited per block) with the
 // same numeric conversions (sscanf "%f" / tinyxml2 Query*Text for attributes and vectors,
@@ -94,7 +94,7 @@ bool attr_int(const rtgh::XmlElement* e, const char* name, int& out) {   // Quer
     return v && sscanf(v->c_str(), "%d", &out) == 1;
 }
 
-// Parser::ParseObjectTransformations (src/Parser.h:769-797)
+// Parser::ParseObjectTransformations (src/Parser.h:769-796)
 void parse_object_transformations(const char* str, std::vector<rtg_xform_ref>& out) {
     size_t cur = 0, n = strlen(str);
     while (cur < n) {
@@ -124,7 +124,7 @@ std::vector<int> parse_textures_list(const char* str) {
 }
 
 // whitespace-separated numbers, what the reference's atof cursor loops read
-// (ParseVertices :684-725, ParseTextureCoordinates :727-767, mesh faces :1117-1141)
+// (ParseVertices Parser.h:684-727, ParseTextureCoordinates Parser.h:729-767, mesh faces Parser.h:1117-1141)
 std::vector<double> numbers(const char* s) {
     std::vector<double> v;
     if (!s) return v;
@@ -150,7 +150,7 @@ bool read_file(const std::string& path, std::string& out) {
     return true;
 }
 
-// ------------------------------------------------------------------ PLY (what happly gives Parser.h :1020-1106)
+// ------------------------------------------------------------------ PLY (what happly gives Parser.h Parser.h:1020-1106)
 // Vertex x,y,z (+u,v) as doubles and face index lists (flat: fcount[k] indices each), for
 // ascii, binary_little_endian and binary_big_endian files.  Property types are resolved once
 // per header so the 1 M-triangle meshes load at memory speed.
@@ -472,7 +472,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
     query_float(child_text(root.get(), "ShadowRayEpsilon"), sc.shadow_eps);
     query_float(child_text(root.get(), "IntersectionTestEpsilon"), sc.int_eps);
 
-    // ParseCameras (:52-164)
+    // ParseCameras (Parser.h:52-164)
     if (const rtgh::XmlElement* ce0 = root->child("Cameras")) {
         for (const rtgh::XmlElement* ce : ce0->all("Camera")) {
             CamData c;
@@ -486,7 +486,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
             query_int(child_text(ce, "NumSamples"), d.num_samples);
             scan3(child_text(ce, "Position"), d.position);
             if (ce->child("Gaze")) scan3(child_text(ce, "Gaze"), d.gaze);
-            if (ce->child("GazePoint")) {                                  // :116-123
+            if (ce->child("GazePoint")) {                                  // Parser.h:116-123
                 float gp[3];
                 scan3(child_text(ce, "GazePoint"), gp);
                 for (int k = 0; k < 3; k++) d.gaze[k] = gp[k] - d.position[k];
@@ -500,7 +500,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
                 c.image_name = a == std::string::npos ? "" : s.substr(a, b - a + 1);
             }
             if (const char* np = child_text(ce, "NearPlane")) sscanf(np, "%f %f %f %f", &d.left, &d.right, &d.bottom, &d.top);
-            if (ce->child("FovY")) {                                       // :144-158
+            if (ce->child("FovY")) {                                       // Parser.h:144-158
                 float fov = 0.0f;
                 query_float(child_text(ce, "FovY"), fov);
                 const float fovr = (float)((double)(fov * 0.5f) * (3.14159265358979323846 / (double)180.0f));
@@ -546,7 +546,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         }
     }
 
-    // ParseBRDF (:166-302): (type, id, exponent)
+    // ParseBRDF (Parser.h:166-302): (type, id, exponent)
     struct Brdf { int type, id, exp; };
     std::vector<Brdf> brdfs;
     if (const rtgh::XmlElement* be = root->child("BRDFs")) {
@@ -566,7 +566,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         }
     }
 
-    // ParseMaterials (:304-472)
+    // ParseMaterials (Parser.h:304-474)
     if (const rtgh::XmlElement* me0 = root->child("Materials")) {
         for (const rtgh::XmlElement* me : me0->all("Material")) {
             rtg_material_desc m{};
@@ -601,7 +601,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         }
     }
 
-    // ParseTextures (:476-605): fields carry over between TextureMaps
+    // ParseTextures (Parser.h:476-605): fields carry over between TextureMaps
     std::map<std::string, std::pair<std::vector<float>, std::pair<int, int>>> cache;
     auto image = [&](const std::string& path, TexData& t) -> int {
         auto it = cache.find(path);
@@ -663,7 +663,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         }
     }
 
-    // ParseTransformations (:607-682)
+    // ParseTransformations (Parser.h:607-682)
     if (const rtgh::XmlElement* tr = root->child("Transformations")) {
         for (const rtgh::XmlElement* t : tr->all("Translation")) { float v[3]; scan3(text_of(t), v); sc.translations.insert(sc.translations.end(), v, v + 3); }
         for (const rtgh::XmlElement* t : tr->all("Scaling")) { float v[3]; scan3(text_of(t), v); sc.scalings.insert(sc.scalings.end(), v, v + 3); }
@@ -688,7 +688,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         }
     }
 
-    // ParseVertices / ParseTextureCoordinates (:684-767): atof -> double -> float
+    // ParseVertices / ParseTextureCoordinates (Parser.h:684-767): atof -> double -> float
     {
         std::vector<double> v = numbers(child_text(root.get(), "VertexData"));
         for (size_t k = 0; k + 2 < v.size(); k += 3)
@@ -697,7 +697,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         for (size_t k = 0; k + 1 < t.size(); k += 2) sc.texcoords.insert(sc.texcoords.end(), {(float)t[k], (float)t[k + 1]});
     }
 
-    // ParseObjects (:798-1195); hw7: <LightSphere> after the spheres, <LightMesh> after the meshes
+    // ParseObjects (Parser.h:798-1195); hw7: <LightSphere> after the spheres, <LightMesh> after the meshes
     const rtgh::XmlElement* oe = root->child("Objects");
     if (!oe) return fail(RTG_ERR_INVALID, "no <Objects>");
     auto common = [&](const rtgh::XmlElement* el, ObjData& o) {
@@ -749,7 +749,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         const std::string* ply = nullptr;
         for (const auto& a : fe->attrs)
             if (strncmp(a.first.c_str(), "plyFile", 7) == 0) { ply = &a.second; break; }
-        if (ply) {                                                          // :1020-1106
+        if (ply) {                                                          // Parser.h:1020-1106
             Ply P;
             int rc = read_ply(base + *ply, P);
             if (rc) return rc;
@@ -770,7 +770,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
             }
             for (double x : P.xyz) sc.vertices.push_back((float)x);
             o.d.texture_offset = texture_offset - vertex_count;
-        } else {                                                            // :1109-1148
+        } else {                                                            // Parser.h:1109-1149
             int vo = 0, to = 0;
             attr_int(fe, "vertexOffset", vo);
             attr_int(fe, "textureOffset", to);
@@ -781,7 +781,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         }
         sc.objects.push_back(std::move(o));
     }
-    for (const rtgh::XmlElement* el : oe->all("MeshInstance")) {           // :1151-1195
+    for (const rtgh::XmlElement* el : oe->all("MeshInstance")) {           // Parser.h:1151-1195
         InstData it;
         attr_int(el, "id", it.d.id);
         int base_id = 0;
@@ -804,7 +804,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
         sc.instances.push_back(it);
     }
 
-    // ParseLights (:1197-1315): Point, Directional, Spot, Area, SphericalDirectional
+    // ParseLights (Parser.h:1197-1315): Point, Directional, Spot, Area, SphericalDirectional
     if (const rtgh::XmlElement* le = root->child("Lights")) {
         scan3(child_text(le, "AmbientLight"), sc.ambient);
         for (const rtgh::XmlElement* l : le->all("PointLight")) {
@@ -857,7 +857,7 @@ int parse(const std::string& xml_path, rtgh_scene& sc) {
             sc.lights.push_back(d);
         }
     }
-    // Scene ctor: the last replace_background texture (src/Scene.cpp:625-631)
+    // Scene ctor: the last replace_background texture (src/Scene.cpp:494-500)
     for (size_t i = 0; i < sc.textures.size(); i++)
         if (sc.textures[i].d.decal == RTG_DECAL_REPLACE_BACKGROUND) sc.background_texture = (int)i;
     return RTG_OK;
@@ -912,7 +912,7 @@ void flatten(rtgh_scene& sc) {
     d.lights = P(sc.lights); d.num_lights = (int)sc.lights.size();
 }
 
-// Image::IsPNG (src/Image.cpp:196-220): ".png" anywhere in the name
+// Image::IsPNG (src/Image.cpp:36-60): ".png" anywhere in the name
 bool is_png(const char* name) {
     int c = 0;
     for (const char* p = name; *p; p++) {
@@ -1087,7 +1087,7 @@ int32_t rtgh_save_image(const char* name, const float* rgb, int32_t nx, int32_t 
     });
 }
 
-// Scene::renderScene (src/Scene.cpp:425-494): precompute once, render and save every camera.
+// Scene::renderScene (src/Scene.cpp:294-363): precompute once, render and save every camera.
 int32_t rtgh_render_scene(const char* xml_path, int32_t device, uint64_t seed, const char* out_dir) {
     return rtgh_render_scene_multi(xml_path, device, 0, seed, out_dir);
 }

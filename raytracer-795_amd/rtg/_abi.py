@@ -15,7 +15,7 @@ RTG_DEVICE_HOST_ONLY = -1
 STATUS = {0: "RTG_OK", -1: "RTG_ERR_INVALID", -2: "RTG_ERR_NO_DEVICE", -3: "RTG_ERR_OOM",
           -4: "RTG_ERR_HIP", -5: "RTG_ERR_UNSUPPORTED"}
 
-# enums (src/defs.h:8-11, src/Material.h:8-9, src/Light.h:12)
+# enums (src/defs.h:8-11, src/Material.h:7-8, src/Light.h:12)
 OBJ_SPHERE, OBJ_TRIANGLE, OBJ_MESH = 0, 1, 2
 XF_TRANSLATION, XF_SCALING, XF_ROTATION, XF_COMPOSITE = 1, 2, 3, 4
 MAT_NORMAL, MAT_MIRROR, MAT_CONDUCTOR, MAT_DIELECTRIC = 0, 1, 2, 3

@@ -1,11 +1,11 @@
 """Host mirror of `Scene::renderScene()` / `Image` over the librtg C ABI.
 
-    sc = rtg.parse_xml("scene.xml")        # new Scene(xml)         (src/Scene.cpp:586)
-    rtg.render_scene(sc)                   # pScene->renderScene()  (src/Scene.cpp:425)
+    sc = rtg.parse_xml("scene.xml")        # new Scene(xml)         (src/Scene.cpp:455)
+    rtg.render_scene(sc)                   # pScene->renderScene()  (src/Scene.cpp:294)
 
 `Renderer` keeps the flattened scene resident on one GPU (rtg_scene_create) and renders
 cameras into host or device framebuffers; `save_image` writes what Image::saveImage does
-(src/Image.cpp:186-267): a P3 text PPM clamped to 255 when the name contains ".png",
+(src/Image.cpp:26-107): a P3 text PPM clamped to 255 when the name contains ".png",
 otherwise an OpenEXR file (half RGB).
 """
 from __future__ import annotations
@@ -156,7 +156,7 @@ def _bvh(fn, handle, obj):
 
 # ---------------------------------------------------------------------------- Image
 def _is_png(name: str) -> bool:
-    """Image::IsPNG (src/Image.cpp:196-220): the substring ".png" anywhere in the name."""
+    """Image::IsPNG (src/Image.cpp:36-60): the substring ".png" anywhere in the name."""
     c = 0
     for ch in name:
         if ch == ".":
@@ -191,7 +191,7 @@ def ppm_p3_bytes(rgb: np.ndarray) -> bytes:
 
 def exr_half_bytes(rgb: np.ndarray) -> bytes:
     """Minimal scanline OpenEXR, ZIP compression off, HALF B/G/R channels (what
-    ExrLibrary::SaveExr requests, src/Helper.cpp:415-466)."""
+    ExrLibrary::SaveExr requests, src/Helper.cpp:361-412)."""
     h, w, _ = rgb.shape
     half = np.asarray(rgb, np.float32).astype(np.float16)
 
@@ -225,7 +225,7 @@ def exr_half_bytes(rgb: np.ndarray) -> bytes:
 
 
 def save_image(name: str, rgb: np.ndarray) -> str:
-    """Image::saveImage (src/Image.cpp:186-194)."""
+    """Image::saveImage (src/Image.cpp:26-34)."""
     data = ppm_p3_bytes(rgb) if _is_png(name) else exr_half_bytes(rgb)
     with open(name, "wb") as fh:
         fh.write(data)
@@ -282,7 +282,7 @@ class Comm:
 
 
 def render_scene(scene: Scene, out_dir: str | None = None, device: int = 0, seed: int = DEFAULT_SEED) -> list:
-    """Scene::renderScene (src/Scene.cpp:425-494): every camera rendered and saved.  A camera
+    """Scene::renderScene (src/Scene.cpp:294-363): every camera rendered and saved.  A camera
     with a hw5 <Tonemap> also gets its tone-mapped image (tonemapped_name; a .png ImageName is
     written tone-mapped instead of clamped)."""
     written = []

@@ -1,7 +1,7 @@
 """Host-side scene model: the state the reference's Parser leaves in `Scene`.
 
 Mirrors src/Parser.h (ParseSceneAttributes/Cameras/BRDF/Materials/Textures/
-Transformations/Vertices/TextureCoordinates/Objects/Lights) and src/Scene.cpp:586-634,
+Transformations/Vertices/TextureCoordinates/Objects/Lights) and src/Scene.cpp:455-504,
 including its quirks (texture-map state carried from one TextureMap to the next,
 `ParseObjectTransformations` only recognising a composite as the first token,
 quad faces of PLY meshes split into (0,1,2),(2,3,0)).  `Scene.to_desc()` flattens the
@@ -84,7 +84,7 @@ class Camera:                       # src/Camera.h, src/Parser.h:52-164
 
 
 @dataclass
-class Material:                     # src/Material.h, src/Parser.h:304-472
+class Material:                     # src/Material.h, src/Parser.h:304-474
     id: int = 1
     type: int = A.MAT_NORMAL
     brdf: int = A.BRDF_NONE
@@ -350,7 +350,7 @@ def _query_float(text: str | None, default: float) -> float:
 
 
 def parse_object_transformations(s: str) -> list:
-    """Parser::ParseObjectTransformations (src/Parser.h:763-791), quirks included."""
+    """Parser::ParseObjectTransformations (src/Parser.h:769-796), quirks included."""
     out = []
     kinds = {"t": A.XF_TRANSLATION, "s": A.XF_SCALING, "r": A.XF_ROTATION, "c": A.XF_COMPOSITE}
     cur, n = 0, len(s)
@@ -513,7 +513,7 @@ def _dir_of(xml_path: str) -> str:
 
 
 def parse_xml(xml_path: str) -> Scene:
-    """Parse a CENG795 scene file like `new Scene(xml)` (src/Scene.cpp:586-634)."""
+    """Parse a CENG795 scene file like `new Scene(xml)` (src/Scene.cpp:455-504)."""
     root = ET.parse(xml_path).getroot()
     sc = Scene()
     base = _dir_of(xml_path)
@@ -522,7 +522,7 @@ def parse_xml(xml_path: str) -> Scene:
     sc.background = tuple(_f3(_text(root, "BackgroundColor")))
     sc.shadow_eps = _query_float(_text(root, "ShadowRayEpsilon"), float(f32(0.002)))
     sc.int_eps = _query_float(_text(root, "IntersectionTestEpsilon"), float(f32(0.001)))
-    # ParseCameras (:52-164)
+    # ParseCameras (Parser.h:52-164)
     for ce in root.find("Cameras").findall("Camera"):
         cam = Camera()
         cam.id = int(ce.get("id", "0"))
@@ -574,7 +574,7 @@ def parse_xml(xml_path: str) -> Scene:
                 cam.pt_flags |= {"importancesampling": A.PT_IMPORTANCE, "nexteventestimation": A.PT_NEE,
                                  "russianroulette": A.PT_RUSSIAN_ROULETTE}.get(tok.strip().lower(), 0)
         sc.cameras.append(cam)
-    # ParseBRDF (:166-302)
+    # ParseBRDF (Parser.h:166-302)
     brdfs = []   # (type, id, exponent)
     be = root.find("BRDFs")
     if be is not None:
@@ -593,7 +593,7 @@ def parse_xml(xml_path: str) -> Scene:
                 else:
                     ty = A.BRDF_TSF if _attr_prefix(b, "kdfresnel", "true") else A.BRDF_TS
                 brdfs.append((ty, bid, ex))
-    # ParseMaterials (:304-472)
+    # ParseMaterials (Parser.h:304-474)
     for me in root.find("Materials").findall("Material"):
         m = Material()
         m.id = int(me.get("id", "0"))
@@ -632,7 +632,7 @@ def parse_xml(xml_path: str) -> Scene:
         m.absorption_index = _query_float(_text(me, "AbsorptionIndex"), 0.0)
         m.absorption_coeff = tuple(_f3(_text(me, "AbsorptionCoefficient")))
         sc.materials.append(m)
-    # ParseTextures (:476-605): state carries over between TextureMaps
+    # ParseTextures (Parser.h:476-605): state carries over between TextureMaps
     te = root.find("Textures")
     if te is not None:
         ie = te.find("Images")
@@ -685,7 +685,7 @@ def parse_xml(xml_path: str) -> Scene:
             else:
                 tx.kind = A.TEX_PERLIN
             sc.textures.append(tx)
-    # ParseTransformations (:607-682)
+    # ParseTransformations (Parser.h:607-682)
     tr = root.find("Transformations")
     if tr is not None:
         for t in tr.findall("Translation"):
@@ -702,7 +702,7 @@ def parse_xml(xml_path: str) -> Scene:
                 row, col = divmod(k, 4)
                 col_major[col * 4 + row] = val
             sc.composites.append(tuple(col_major))
-    # ParseVertices / ParseTextureCoordinates (:684-767): atof -> double -> float
+    # ParseVertices / ParseTextureCoordinates (Parser.h:684-767): atof -> double -> float
     vd = root.find("VertexData")
     verts = []
     if vd is not None and vd.text:
@@ -721,7 +721,7 @@ def parse_xml(xml_path: str) -> Scene:
     def ntcs():
         return len(tcs) + sum(a.shape[0] for a in extra_t)
 
-    # ParseObjects (:798-1195)
+    # ParseObjects (Parser.h:798-1195)
     oe = root.find("Objects")
 
     def common(el, o):
@@ -820,7 +820,7 @@ def parse_xml(xml_path: str) -> Scene:
     sc.vertices = np.concatenate(parts_v).astype(f32) if parts_v else np.zeros((0, 3), f32)
     parts_t = [np.asarray(tcs, f32).reshape(-1, 2)] + extra_t
     sc.texcoords = np.concatenate(parts_t).astype(f32)
-    # ParseLights (:1197-1315): Point, Directional, Spot, Area, SphericalDirectional
+    # ParseLights (Parser.h:1197-1315): Point, Directional, Spot, Area, SphericalDirectional
     le = root.find("Lights")
     amb = _text(le, "AmbientLight")
     sc.ambient = tuple(_f3(amb)) if amb is not None else (0.0, 0.0, 0.0)
@@ -851,7 +851,7 @@ def parse_xml(xml_path: str) -> Scene:
                       bump_factor=1.0, texels=load_image(sc.images[iid - 1]), image_id=iid)
         sc.textures.append(tex)
         sc.lights.append(Light(type=A.LIGHT_ENVIRONMENT, texture=len(sc.textures) - 1, image_id=iid))
-    # Scene ctor: last replace_background texture (src/Scene.cpp:625-631)
+    # Scene ctor: last replace_background texture (src/Scene.cpp:494-500)
     sc.background_texture = -1
     for i, tx in enumerate(sc.textures):
         if tx.decal == A.DECAL_REPLACE_BACKGROUND:

@@ -128,9 +128,9 @@ def simple(nx=800, ny=800) -> Scene:
 
 
 def bgtex(nx=48, ny=32, spp=1, interp=A.INTERP_NN) -> Scene:
-    """`simple` in front of a replace_background image texture (src/Scene.cpp:544-566): at 1 spp
+    """`simple` in front of a replace_background image texture (src/Scene.cpp:413-435): at 1 spp
     SingleSample passes (row = x, col = y), so the background is looked up transposed; at > 1
-    spp it is not (src/Scene.cpp:496-542)."""
+    spp it is not (src/Scene.cpp:365-411)."""
     sc = simple(nx, ny)
     sc.cameras[0].num_samples = spp
     sc.cameras[0].image_name = "bgtex.png"
@@ -192,7 +192,7 @@ def dragon1m(nx=1920, ny=1080, spp=64, nu=1000, nv=500) -> Scene:
     b = _add_vertices(sc, v)
     sc.objects.append(Object(type=A.OBJ_MESH, id=1, material=1, faces=(f + b).astype(np.int32),
                              ply_file="dragon1m.ply",
-                             texture_offset=len(sc.texcoords) + 1 - b))   # what Parser.h:1087-1147 derives
+                             texture_offset=len(sc.texcoords) + 1 - b))   # what Parser.h:1051, 1099-1102 derives
     sc.lights.append(Light(type=A.LIGHT_POINT, position=(3, 5, 4), intensity=(22000, 22000, 22000)))
     return sc
 

@@ -1,7 +1,7 @@
 """Multi-GPU pixel sharding.
 
 Rank r of G renders the rows y with (y // B) % G == r, B = ROW_BLOCK = 4 (the reference
-interleaves pixel columns over its 8 threads, src/Scene.cpp:400-423; the library tiles a
+interleaves pixel columns over its 8 threads, src/Scene.cpp:269-292; the library tiles a
 shard's pixels 16x4 for B = 4, so each tile stays image-contiguous and its rays as coherent
 as on one GPU, while 270 blocks over the ranks keep their loads balanced) into a
 zero-initialised full-frame accumulator, or compactly (gather_frame).  Summing the G frames is exact because

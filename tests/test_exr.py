@@ -113,7 +113,7 @@ def test_corrupt_and_unsupported_fail_loudly(tmp_path):
 
 
 def test_native_writer_reads_back(tmp_path):
-    """rtgh_save_image's OpenEXR HALF output (Image::saveImage, src/Helper.cpp:361-412)
+    """rtgh_save_image's OpenEXR HALF output (Image::saveImage -> ExrLibrary::SaveExr, src/Image.cpp:26-34, src/Helper.cpp:361-412)
     decodes to the half-rounded framebuffer."""
     rng = np.random.default_rng(11)
     img = (rng.uniform(0, 300, (17, 23, 3))).astype(np.float32)

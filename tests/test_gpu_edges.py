@@ -1,6 +1,6 @@
 """Edge cases of the render path on the GPU, each against the oracle bit for bit: empty and
 light-less scenes, degenerate image sizes, MaxRecursionDepth 0, many lights (the in-order
-light sum of Scene::RecursiveShading, src/Scene.cpp:279-350), every primary ray missing, and
+light sum of Scene::RecursiveShading, src/Scene.cpp:148-219), every primary ray missing, and
 empty / NaN ray batches for rtg_trace_closest (src/Helper.cpp:28-30 returns {} on NaN)."""
 import numpy as np
 import pytest

@@ -37,7 +37,7 @@ def test_cli_matches_python_host(gpu, tmp_path, name, make):
 
 
 def test_cli_exr_output(gpu, tmp_path):
-    """Non-.png names go through the OpenEXR HALF writer (src/Helper.cpp:415-466)."""
+    """Non-.png names go through the OpenEXR HALF writer (src/Helper.cpp:361-412)."""
     sc = scenegen.cornell_pt(24, 18, spp=2)
     sc.cameras[0].image_name = "pt.exr"
     xml = write_xml(sc, str(tmp_path / "pt.xml"))

@@ -1,6 +1,6 @@
 """Multi-GPU fan-out behind the C ABI (SURVEY.md §8(b) Threading row, §8(e)).
 
-The reference forks 8 std::threads inside renderScene (src/Scene.cpp:340-356); librtg forks one
+The reference forks 8 std::threads inside renderScene (src/Scene.cpp:294-363); librtg forks one
 host thread per GPU inside rtg_render (rtg_render_opts.num_devices) and gathers the row-block
 shards over RCCL, or, one process per GPU, through rtg_comm_* + rtg_render_ranked.  On a 1-GPU
 box the RCCL path runs with one rank (ncclCommInitAll / ncclCommInitRank over one device, the

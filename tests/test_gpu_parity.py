@@ -143,7 +143,7 @@ def test_render_is_deterministic(gpu):
 
 def test_sample_chunks_accumulate_in_order(gpu):
     """spp above the ray batch: sample chunks of one pixel range run as successive passes on
-    one stream, so MultiSample's in-order sum (src/Scene.cpp:519-540) is kept bit for bit."""
+    one stream, so the in-order sum of MultiSample (src/Scene.cpp:386-409) is kept bit for bit."""
     sc = scenegen.cornell(24, 18, spp=8)
     with rtg.Renderer(sc, device=gpu) as r:
         a = r.render(0)

@@ -1,7 +1,7 @@
 """Product host-side flattening (librtg, RTG_DEVICE_HOST_ONLY) against the oracle,
 bit for bit: per-object BVH permutation / topology / boxes (src/BVH.cpp:64-135),
-inverse and inverse-transpose matrices (src/Helper.cpp:189-280) and smooth vertex normals
-(src/Scene.cpp:433-449).  The product builds its BVH with nth_element selection and the
+inverse and inverse-transpose matrices (src/Helper.cpp:135-226) and smooth vertex normals
+(src/Scene.cpp:302-318).  The product builds its BVH with nth_element selection and the
 oracle with a full sort per node (as the reference does); both must agree exactly."""
 import ctypes as C
 

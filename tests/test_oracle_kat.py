@@ -73,7 +73,7 @@ def test_triangle_barycentric_epsilon_band():
 
 
 def test_object_rejected_when_nearest_candidate_is_behind_origin():
-    """src/BVH.cpp:159-173 + src/Helper.cpp:93-104: a mesh whose nearest candidate has
+    """src/BVH.cpp:159-173 + src/Helper.cpp:39-49: a mesh whose nearest candidate has
     t in [-eps, 0] contributes nothing, even if it has a valid hit further along."""
     verts = [(-1, -1, 0.0005), (1, -1, 0.0005), (0, 1, 0.0005),       # just behind the origin
              (-1, -1, -2), (1, -1, -2), (0, 1, -2)]                     # in front
@@ -97,7 +97,7 @@ QUIRK_DIRS = [(0.0, 0.0, -1.0), (-0.0, -0.0, -1.0), (1e-30, 1e-30, -1.0), (1e-7,
 
 
 def test_axis_parallel_and_tiny_direction_quirks():
-    """BVH::RayBBoxIntersection (src/BVH.cpp:224-233): a zero direction component takes the
+    """BVH::RayBBoxIntersection (src/BVH.cpp:212-233): a zero direction component takes the
     `else` branch, (max-o)/0 = +inf becomes the slab entry and the box is missed (glm's
     mat4*vec4 turns -0 into +0, so both signs miss).  Ray::gett (src/Ray.cpp:21-36) then
     rejects a tiny x component: p.x rounds back to o.x, t = 0, and `distance > 0` fails."""
@@ -165,9 +165,9 @@ def test_oracle_render_is_deterministic_and_finite():
 
 
 def test_background_texture_transposed_at_1spp():
-    """Scene::SingleSample passes (row = x, col = y) to GetBackgroundColor (src/Scene.cpp:496-511,
+    """Scene::SingleSample passes (row = x, col = y) to GetBackgroundColor (src/Scene.cpp:365-380,
     544-566), so at 1 spp a replace_background texture is looked up at (u, v) = (y/nx, x/ny);
-    MultiSample (> 1 spp) uses (x/nx, y/ny); coordinates wrap (src/Texture.cpp:111-119)."""
+    MultiSample (> 1 spp) uses (x/nx, y/ny); coordinates wrap (GetColorAtCoordinates, src/Texture.cpp:111-119)."""
     nx, ny = 48, 32
     for spp in (1, 4):
         sc = scenegen.bgtex(nx, ny, spp=spp)

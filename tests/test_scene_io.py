@@ -63,7 +63,7 @@ def test_textured_round_trip(tmp_path):
 
 
 def test_object_transformation_parsing_quirks():
-    # src/Parser.h:763-791: tokens are found only at s/t/r (a composite only as first token)
+    # src/Parser.h:769-796: tokens are found only at s/t/r (a composite only as first token)
     T, S, R, Cc = A.XF_TRANSLATION, A.XF_SCALING, A.XF_ROTATION, A.XF_COMPOSITE
     assert parse_object_transformations("t1 s2 r3") == [(T, 1), (S, 2), (R, 3)]
     assert parse_object_transformations("c1 t2") == [(Cc, 1), (T, 2)]
