@@ -4,7 +4,8 @@
 // The reference decodes with its vendored tinyexr (LoadEXR, src/Helper.cpp:346-359) and keeps
 // RGBA floats; the texture code reads R, G, B.  This is a restatement of the published
 // OpenEXR 2 file layout (magic/version, attribute header, offset table, chunks) and of its
-// codecs, written from the format description:
+// codecs, written from the format description (the PIZ wavelet's inverse is derived from the
+// forward lifting equations, see wavelet_inverse_2d):
 //   RLE   signed run counts, then the byte predictor and the two-half interleave
 //   ZIPS/ZIP  zlib (1 / 16 lines per chunk), same predictor and interleave
 //   PIZ   per-block value bitmap + forward LUT, canonical Huffman with run-length pseudo
@@ -261,65 +262,73 @@ bool huf_decode(const unsigned char* in, size_t n_in, uint16_t* out, size_t n_ou
     return true;
 }
 
-inline void wdec14(uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
-    const int hi = (int16_t)h;
-    const int ai = (int16_t)l + (hi & 1) + (hi >> 1);
-    a = (uint16_t)(int16_t)ai;
-    b = (uint16_t)(int16_t)(ai - hi);
-}
+// PIZ's wavelet (OpenEXR 2 format description, "PIZ compression"): a multi-level 2-D Haar-like
+// transform with integer lifting.  One forward step maps a pair (a, b) to
+//   narrow form (every value < 2^14):   lo = (a + b) >> 1,      hi = a - b        (signed 16-bit)
+//   wide form (modular, values >= 2^14): hi = (a + 2^15 - b) mod 2^16,
+//                                        lo = (a + 2^15 + b) / 2 mod 2^16 (2^15 added when a + 2^15 < b)
+// The inverse steps below follow from those definitions: in the narrow form a + b and a - b
+// have the same parity, so a = lo + (hi + (hi & 1)) / 2 exactly and b = a - hi; in the wide form
+// b = lo - hi / 2 and a = hi + b - 2^15, both mod 2^16.
+struct InverseLift {
+    bool wide;
+    void operator()(uint16_t lo, uint16_t hi, uint16_t& a, uint16_t& b) const {
+        if (!wide) {
+            const int h = (int16_t)hi;
+            const int av = (int16_t)lo + ((h + (h & 1)) >> 1);
+            a = (uint16_t)(int16_t)av;
+            b = (uint16_t)(int16_t)(av - h);
+        } else {
+            const unsigned bv = ((unsigned)lo - ((unsigned)hi >> 1)) & 0xFFFFu;
+            a = (uint16_t)(((unsigned)hi + bv + 0x8000u) & 0xFFFFu);   // - 2^15 == + 2^15 mod 2^16
+            b = (uint16_t)bv;
+        }
+    }
+};
 
-inline void wdec16(uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) {
-    const int m = l, d = h;
-    const int bb = (m - (d >> 1)) & 0xffff;
-    const int aa = (d + bb - 0x8000) & 0xffff;
-    b = (uint16_t)bb;
-    a = (uint16_t)aa;
-}
-
-// inverse of the 2-D wavelet over an nx x ny array with element stride ox and line stride oy
-void wav2_decode(uint16_t* in, int nx, int ox, int ny, int oy, uint16_t mx) {
-    const bool w14 = mx < (1 << 14);
-    const int n = nx > ny ? ny : nx;
-    int p = 1, p2;
-    while (p <= n) p <<= 1;
-    p >>= 1;
-    p2 = p;
-    p >>= 1;
-    auto dec = [w14](uint16_t l, uint16_t h, uint16_t& a, uint16_t& b) { if (w14) wdec14(l, h, a, b); else wdec16(l, h, a, b); };
-    while (p >= 1) {
-        uint16_t* py = in;
-        uint16_t* ey = in + (ptrdiff_t)oy * (ny - p2);
-        const int oy1 = oy * p, oy2 = oy * p2, ox1 = ox * p, ox2 = ox * p2;
-        uint16_t i00, i01, i10, i11;
-        for (; py <= ey; py += oy2) {
-            uint16_t* px = py;
-            uint16_t* ex = py + (ptrdiff_t)ox * (nx - p2);
-            for (; px <= ex; px += ox2) {
-                uint16_t* p01 = px + ox1;
-                uint16_t* p10 = px + oy1;
-                uint16_t* p11 = p10 + ox1;
-                dec(*px, *p10, i00, i10);
-                dec(*p01, *p11, i01, i11);
-                dec(i00, i01, *px, *p01);
-                dec(i10, i11, *p10, *p11);
+// Inverse transform of one nx x ny plane of 16-bit words at `base`, sample (i, j) at
+// base[i * sx + j * sy].  The encoder halves the lattice level by level: at the level with pair
+// distance p (lattice step q = 2p) every q-aligned 2x2 cell {(i, j), (i+p, j), (i, j+p), (i+p, j+p)}
+// was transformed along x, then along y; a last odd column (nx & p) or row (ny & p) of cells was
+// transformed along one axis only.  Decoding runs the levels coarse to fine: p from half the
+// largest power of two <= min(nx, ny) down to 1, each cell along y first, then along x.
+void wavelet_inverse_2d(uint16_t* base, int nx, int ny, int sx, int sy, uint16_t maxval) {
+    const InverseLift lift{maxval >= (1 << 14)};
+    auto at = [&](int i, int j) -> uint16_t& { return base[(ptrdiff_t)i * sx + (ptrdiff_t)j * sy]; };
+    const int n = std::min(nx, ny);
+    int top = 1;
+    while (top * 2 <= n) top *= 2;               // largest power of two <= n
+    for (int p = top / 2; p >= 1; p /= 2) {
+        const int q = 2 * p;
+        const int ci = (nx - q) / q + 1, cj = (ny - q) / q + 1;   // full cells per row / column
+        for (int cy = 0; cy < cj; cy++) {
+            const int j = cy * q;
+            for (int cx = 0; cx < ci; cx++) {
+                const int i = cx * q;
+                uint16_t t00, t01, t10, t11;
+                lift(at(i, j), at(i, j + p), t00, t10);          // along y, left column
+                lift(at(i + p, j), at(i + p, j + p), t01, t11);  // along y, right column
+                lift(t00, t01, at(i, j), at(i + p, j));          // along x, top row
+                lift(t10, t11, at(i, j + p), at(i + p, j + p));  // along x, bottom row
             }
-            if (nx & p) {
-                uint16_t* p10 = px + oy1;
-                dec(*px, *p10, i00, *p10);
-                *px = i00;
+            if (nx & p) {                                        // odd column of cells: y only
+                const int i = ci * q;
+                uint16_t a, b;
+                lift(at(i, j), at(i, j + p), a, b);
+                at(i, j) = a;
+                at(i, j + p) = b;
             }
         }
-        if (ny & p) {
-            uint16_t* px = py;
-            uint16_t* ex = py + (ptrdiff_t)ox * (nx - p2);
-            for (; px <= ex; px += ox2) {
-                uint16_t* p01 = px + ox1;
-                dec(*px, *p01, i00, *p01);
-                *px = i00;
+        if (ny & p) {                                            // odd row of cells: x only
+            const int j = cj * q;
+            for (int cx = 0; cx < ci; cx++) {
+                const int i = cx * q;
+                uint16_t a, b;
+                lift(at(i, j), at(i + p, j), a, b);
+                at(i, j) = a;
+                at(i + p, j) = b;
             }
         }
-        p2 = p;
-        p >>= 1;
     }
 }
 
@@ -354,7 +363,7 @@ bool piz_decode(const unsigned char* in, size_t n, unsigned char* out, int nx, i
     size_t start = 0;
     for (const Chan& c : chans) {
         const int size = type_bytes(c.type) / 2;
-        for (int j = 0; j < size; j++) wav2_decode(tmp.data() + start + j, nx, size, ny, nx * size, maxv);
+        for (int j = 0; j < size; j++) wavelet_inverse_2d(tmp.data() + start + j, nx, ny, size, nx * size, maxv);
         start += (size_t)nx * ny * size;
     }
     for (size_t i = 0; i < total; i++) tmp[i] = lut[tmp[i]];

@@ -162,3 +162,15 @@ def test_corrupted_files_never_crash(tmp_path, comp):
             assert img.ndim == 3 and img.shape[2] == 3
         except RtgError:
             pass
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (1, 29), (31, 1), (2, 3), (33, 17), (64, 63), (5, 100)])
+@pytest.mark.parametrize("ptype", [X.HALF, X.FLOAT], ids=["half", "float"])
+def test_piz_wavelet_odd_shapes(tmp_path, w, h, ptype):
+    """The inverse PIZ wavelet on lattices whose sides are not powers of two (odd cell columns /
+    rows at every level, degenerate one-pixel sides), both lifting forms (FLOAT words exceed 2^14
+    distinct values), against the test-side encoder."""
+    ch = _image(w, h, seed=w * 131 + h, scale=3.0)
+    p = str(tmp_path / f"piz_{w}x{h}.exr")
+    X.write_exr(p, ch, X.PIZ, ptype)
+    _check(p, ch, ptype)
