@@ -246,6 +246,11 @@ typedef struct rtg_render_opts {
                                 the N-shard path on fewer GPUs; results are identical). */
 } rtg_render_opts;
 
+/* Automatic pass size (rays per pass) of a render: at most 24M rays, lowered so that the level
+   buffers of `lanes` passes in flight fit half of `device_bytes` (0 = no memory limit), at 2 x
+   (228 + 68 x max(num_lights - 1, 0)) bytes per ray [+ 96 for the path tracer]; at least 64K. */
+int64_t rtg_pass_rays(int32_t num_lights, int32_t path_tracer, int32_t lanes, uint64_t device_bytes);
+
 /* Number of image rows y < ny with (y / row_block) % row_stride == row_offset. */
 int32_t rtg_shard_rows(int32_t ny, int32_t row_offset, int32_t row_stride, int32_t row_block);
 

@@ -1072,11 +1072,21 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     if (npix_ll > (1LL << 30)) return fail(RTG_ERR_UNSUPPORTED, "image too large");
     int npix = (int)npix_ll;
     int total = cam->num_samples;
-    // auto batch: a whole multiple of the lanes in flight, as few passes as the 24M-ray cap
-    // allows, at least 2M rays each -- every lane gets the same number of equal passes, so the
-    // lanes' level tails end together and overlap each other's work (1080p64 dragon, passes x
-    // lanes: 1 GPU 16x3 -> 8x8 58.2 -> 58.1 ms; a 1/4 row shard 4x3 -> 8x8 16.0 -> 15.2 ms; a 1/8
-    // shard 3x3 -> 8x8 9.15 -> 8.1 ms)
+    if (cam->integrator != RTG_INTEGRATOR_REFERENCE && cam->integrator != RTG_INTEGRATOR_PATH)
+        return fail(RTG_ERR_INVALID, "unknown integrator");
+    const bool pt = cam->integrator == RTG_INTEGRATOR_PATH;
+    SceneView sv = s->sv;                    // per-render view: the path tracer's light loop
+    if (pt) {
+        sv.pt_flags = cam->pt_flags;
+        if (cam->pt_flags & RTG_PT_NEE) sv.num_lights += s->num_emit;
+    }
+    const int nL = sv.num_lights;
+    // auto batch: a whole multiple of the lanes in flight, as few passes as the ray cap allows,
+    // at least 2M rays each -- every lane gets the same number of equal passes, so the lanes'
+    // level tails end together and overlap each other's work (1080p64 dragon, passes x lanes:
+    // 1 GPU 16x3 -> 8x8 58.2 -> 58.1 ms; a 1/4 row shard 4x3 -> 8x8 16.0 -> 15.2 ms; a 1/8 shard
+    // 3x3 -> 8x8 9.15 -> 8.1 ms).  The cap is 24M rays, lowered so that every lane's level buffers
+    // fit half the device memory (rtg_pass_rays: many lights cost 68 B per ray and light).
     const int lanes_req = o.streams > 0 ? std::min(o.streams, 8) : s->num_lanes;
     const long long frame_rays = (long long)npix * total;
     int ns_chunk, np_pass;
@@ -1086,7 +1096,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         ns_chunk = (int)std::max<long long>(1, std::min<long long>(total, max_batch));
         np_pass = (int)std::max<long long>(1, std::min<long long>(npix, max_batch / ns_chunk));
     } else {
-        const long long kMin = 2LL << 20, kMax = 24LL << 20;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) total_b = 0;
+        const long long kMax = rtg_pass_rays(nL, pt ? 1 : 0, lanes_req, (uint64_t)total_b);
+        const long long kMin = std::min<long long>(2LL << 20, kMax);
         const long long lanes_eff = std::max(1LL, std::min<long long>(lanes_req, (frame_rays + kMin - 1) / kMin));
         const long long passes = lanes_eff * ((frame_rays + lanes_eff * kMax - 1) / (lanes_eff * kMax));
         if (total > kMax) {                 // absurd spp: sample chunks of one pixel
@@ -1098,15 +1111,6 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         }
     }
     int exhaustive = o.traversal == 1;
-    if (cam->integrator != RTG_INTEGRATOR_REFERENCE && cam->integrator != RTG_INTEGRATOR_PATH)
-        return fail(RTG_ERR_INVALID, "unknown integrator");
-    const bool pt = cam->integrator == RTG_INTEGRATOR_PATH;
-    SceneView sv = s->sv;                    // per-render view: the path tracer's light loop
-    if (pt) {
-        sv.pt_flags = cam->pt_flags;
-        if (cam->pt_flags & RTG_PT_NEE) sv.num_lights += s->num_emit;
-    }
-    const int nL = sv.num_lights;
 
     int rc;
     if ((rc = s->d_acc.grow(sizeof(float) * 3 * std::max<size_t>(npix, 1)))) return rc;
@@ -1401,6 +1405,17 @@ int32_t rtg_render_device(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
         if (opts && (opts->num_devices > 1 || opts->devices)) return render_multi(s, cam, opts, rgb_out_device, (hipStream_t)stream);
         return render_impl(s, cam, opts, rgb_out_device, (hipStream_t)stream);
     });
+}
+
+int64_t rtg_pass_rays(int32_t num_lights, int32_t path_tracer, int32_t lanes, uint64_t device_bytes) {
+    // device bytes per ray of a pass, per level in flight: hit 16 + node records 48 + shadow
+    // records 64 and list entry 4 per light + room for two child rays (32 + 16 each) [+ path
+    // records 16 for the ray and 32 for its children]; x2 for the level that spawned it
+    const double per_ray = 2.0 * (16.0 + 48.0 + 68.0 * std::max(num_lights, 1) + 96.0 + (path_tracer ? 48.0 : 0.0));
+    const long long kCap = 24LL << 20, kFloor = 1LL << 16;
+    if (device_bytes == 0) return kCap;
+    const double budget = 0.5 * (double)device_bytes / (double)std::max(lanes, 1);
+    return std::max(kFloor, std::min(kCap, (long long)(budget / per_ray)));
 }
 
 int32_t rtg_shard_rows(int32_t ny, int32_t row_offset, int32_t row_stride, int32_t row_block) {

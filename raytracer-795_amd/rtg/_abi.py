@@ -167,6 +167,7 @@ EXPORTS = {
                                       C.c_void_p]),
     "rtg_last_render_stats": (C.c_int32, [C.c_void_p, C.POINTER(RenderStats)]),
     "rtg_shard_rows": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "rtg_pass_rays": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_uint64]),
     "rtg_tonemap": (C.c_int32, [C.c_int32, PF, C.c_int32, C.c_int32, C.POINTER(TonemapDesc), PF]),
     "rtg_tonemap_device": (C.c_int32, [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(TonemapDesc), C.c_void_p,
                                        C.c_void_p]),

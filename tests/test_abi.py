@@ -20,7 +20,7 @@ HEADER = os.path.join(ROOT, "include", "rtg.h")
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(rtg_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char\*)\s+(rtg_\w+)\s*\(", src, re.M)))
 
 
 def test_header_matches_ctypes_exports():
@@ -101,3 +101,20 @@ def test_device_count_without_gpu_is_safe(lib):
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(rtg.RtgError):
         A.load_library(str(tmp_path / "nope.so"))
+
+
+def test_pass_size_shrinks_with_the_lights(lib):
+    """rtg_pass_rays: the per-pass ray count is capped at 24M and shrinks so that the level
+    buffers of the passes in flight (68 B per ray and light) fit half the device memory."""
+    gb = 288 << 30                                       # one MI355X
+    one = lib.rtg_pass_rays(1, 0, 8, gb)
+    assert one == 24 << 20
+    sizes = [lib.rtg_pass_rays(n, 0, 8, gb) for n in (1, 8, 24, 64)]
+    assert sizes == sorted(sizes, reverse=True) and sizes[-1] < sizes[0]
+    for n, k in zip((1, 8, 24, 64), sizes):
+        per_ray = 2 * (16 + 48 + 68 * n + 96)
+        assert k * per_ray * 8 <= gb // 2 or k == 1 << 16
+    assert lib.rtg_pass_rays(64, 1, 8, gb) < lib.rtg_pass_rays(64, 0, 8, gb)   # path records
+    assert lib.rtg_pass_rays(64, 0, 1, gb) > lib.rtg_pass_rays(64, 0, 8, gb)   # fewer lanes
+    assert lib.rtg_pass_rays(64, 0, 8, 0) == 24 << 20                          # no limit known
+    assert lib.rtg_pass_rays(64, 0, 8, 1 << 20) == 1 << 16                     # floor
