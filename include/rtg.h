@@ -317,6 +317,10 @@ typedef enum rtg_bvh_builder {
 } rtg_bvh_builder;
 typedef struct rtg_build_opts {
     int32_t bvh_builder;     /* rtg_bvh_builder */
+    int32_t tlas;            /* top-level BVH over objects and instances, replacing the reference's
+                                linear object loop (src/Helper.cpp:32-73) with the same result (ties
+                                to the first entry): 0 = auto (>= 16 entries), 1 = off, 2 = on
+                                (>= 2 entries); env RTG_TLAS=0/1 overrides */
 } rtg_build_opts;
 /* rtg_scene_create with build options (NULL = defaults). */
 int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rtg_build_opts* opts,
@@ -325,6 +329,7 @@ typedef struct rtg_build_stats {
     double bvh_build_ms;     /* wall time of all per-object BVH constructions */
     int32_t bvh_gpu_objects; /* objects whose BVH was built on the GPU */
     int32_t num_objects;
+    int32_t tlas_nodes;      /* nodes of the top-level BVH (0: linear object loop) */
 } rtg_build_stats;
 int32_t rtg_scene_build_stats(const rtg_scene* scene, rtg_build_stats* out);
 int32_t rtg_scene_destroy(rtg_scene* scene);

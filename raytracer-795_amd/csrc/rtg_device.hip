@@ -271,14 +271,19 @@ struct Stats { unsigned nodes, tris, steps; };
 // the leaf.  This ordered traversal computes the same total order and prunes subtrees
 // whose distance lower bound exceeds the current best (EXHAUSTIVE disables pruning).
 // `tmax`: hits with gett() >= tmax are irrelevant to the caller (shadow queries).
-template <bool EXHAUSTIVE, bool STATS>
-DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st) {
+// TLAS: the entries are enumerated by the top-level BVH (near first, world boxes that cannot hold
+// an accepted hit at t <= nearest skipped) instead of the reference's linear loop; an entry
+// replaces the winner iff t < nearest, or t == nearest and it comes earlier in the loop order
+// (objects before instances, lower index first), which is the loop's first-wins rule.
+template <bool EXHAUSTIVE, bool STATS, bool TLAS = false>
+DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
+                       short* tstack = nullptr) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
     float nearest = tmax;
     const float eps = sv.int_eps;
-    for (int i = 0; i < sv.num_tops; i++) {
+    auto visit = [&](const int i) {
         const TopObject& T = sv.tops[i];
         const Geometry& g = sv.geoms[T.geom];
         f3 o2, d2;
@@ -307,7 +312,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
             const bool root_ok = g.node_base < 0 ? g.root_leaf_count > 0
                                : box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
                                          g.root_max[1], g.root_max[2]);
-            if (!root_ok) continue;
+            if (!root_ok) return;
             // distance bound from the best hit so far (see DESIGN.md "pruning")
             float boundD = FLT_MAX;
             const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
@@ -552,10 +557,72 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         }
         if (found) {
             float t = gett(o2, d2, bp);
-            if (t < nearest && t > 0) {
+            if (t > 0 && (t < nearest || (t == nearest && i < out.obj))) {   // src/Helper.cpp:43, 64
                 nearest = t;
                 out.obj = i; out.prim = bprim; out.t = t;
             }
+        }
+    };
+    const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
+    const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
+    if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {
+        for (int i = 0; i < sv.num_tops; i++) visit(i);
+        return out;
+    }
+    // top-level walk: a child box is skipped when the ray line misses it, when it lies wholly
+    // behind the origin (accepted hits have t > 0) or wholly beyond the winner so far (its hits
+    // would have t > nearest).  The boxes carry the host's rounding margins; the reciprocal slab
+    // adds 2^-18 of the magnitudes, and NaN comparisons keep a box.
+    const f3 winv = mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    auto tchild = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& key) -> bool {
+        const float ax = (mnx - o.x) * winv.x, bx = (mxx - o.x) * winv.x;
+        const float ay = (mny - o.y) * winv.y, by = (mxy - o.y) * winv.y;
+        const float az = (mnz - o.z) * winv.z, bz = (mxz - o.z) * winv.z;
+        const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+        const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        const float e = (fabsf(sl) + fabsf(le)) * 3.814697265625e-6f + 1e-30f;   // 2^-18
+        key = le - e;
+        if (sl + e < key) return false;
+        if (sl + e < 0.0f) return false;
+        return !(key > nearest * (1.0f + 1e-5f) + 1e-30f);
+    };
+    auto tleaf = [&](int ref, int cnt) {
+        for (int k = ref; k < ref + cnt; k++) visit(sv.tlas_idx[k]);
+    };
+    int tsp = 0;
+    int cur = sv.tlas_root;
+    while (true) {
+        const Node nd = sv.tlas[cur];
+        const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
+        float lk = 0.0f, rk = 0.0f;
+        bool lok = lcnt >= 0 && tchild(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lk);
+        bool rok = rcnt >= 0 && tchild(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rk);
+        const bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
+        auto still = [&](float k) { return !(k > nearest * (1.0f + 1e-5f) + 1e-30f); };
+        if (lleaf && rleaf && rk < lk) {
+            tleaf(rref, rcnt);
+            if (still(lk)) tleaf(lref, lcnt);
+            lok = rok = false;
+        } else {
+            if (lleaf) { tleaf(lref, lcnt); lok = false; }
+            if (rleaf) { if (still(rk)) tleaf(rref, rcnt); rok = false; }
+        }
+        lok = lok && still(lk);
+        rok = rok && still(rk);
+        if (lok && rok) {
+            int nearc = lref, farc = rref;
+            if (rk < lk) { nearc = rref; farc = lref; }
+            tstack[tsp * sstride] = (short)farc;
+            tsp++;
+            cur = nearc;
+        } else if (lok) {
+            cur = lref;
+        } else if (rok) {
+            cur = rref;
+        } else {
+            if (tsp == 0) break;
+            tsp--;
+            cur = tstack[tsp * sstride];
         }
     }
     return out;
@@ -1181,12 +1248,13 @@ DEV HitRec load_hit_compact(const HitRec* hits, int i) {
 }
 
 // GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no RayRec buffer).
-template <bool EXHAUSTIVE, bool STATS, bool GEN = false>
+template <bool EXHAUSTIVE, bool STATS, bool GEN = false, bool TLAS = false>
 __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayRec* __restrict__ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
                                                        const CameraDev cam, const PassDev ps, uint64_t seed,
                                                        bool compact) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
+    __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     Stats st = {0, 0, 0};
     if (i < n) {
@@ -1200,7 +1268,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
             o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
             time = r.o_t.w; tmax = r.d.w;
         }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st);
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st,
+                                                        s_tstack + (TLAS ? threadIdx.x : 0));
         if (compact) store_hit_compact(hits, i, h);
         else hits[i] = h;
     }
@@ -1697,13 +1766,14 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const
 // does); with several, the visibility is recorded and k_light_sum adds them in light order.
 // Each query is a full closest-hit FindIntersection, as Light::IsShadow does
 // (src/Light.cpp:188-204): the distance test below decides blocking.
-template <bool EXHAUSTIVE, bool STATS>
+template <bool EXHAUSTIVE, bool STATS, bool TLAS = false>
 __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const SceneView sv,
                                                                        const ShadowPlanes shadows, bool lean,
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount, const NodePlanes nodes,
                                                                        unsigned* nan_queries, Counters* ctr) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
+    __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
     Stats st = {0, 0, 0};
@@ -1731,8 +1801,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             tmax = sd.w;
         }
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
-        HitRec h = closest_hit<EXHAUSTIVE, STATS>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x,
-                                                  kTraceBlock, st);
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x,
+                                                        kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0));
         // the query's contribution / mode are re-read rather than kept live across the traversal
         // (register pressure: 128 VGPRs for 4 waves per SIMD)
         const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
@@ -1993,15 +2063,22 @@ void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, 
     dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
     const CameraDev cam = gen_cam ? *gen_cam : CameraDev{};
     const PassDev ps = gen_ps ? *gen_ps : PassDev{};
+    const bool tl = sv.tlas_root >= 0;
+#define RTG_TRACE(EX, STA, GEN)                                                                                   \
+    do {                                                                                                          \
+        if (tl) hipLaunchKernelGGL((k_trace<EX, STA, GEN, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact); \
+        else hipLaunchKernelGGL((k_trace<EX, STA, GEN, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact); \
+    } while (0)
     if (gen_cam) {   // primary rays generated in the kernel (rays unused)
-        if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
-        else if (ctr) hipLaunchKernelGGL((k_trace<false, true, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
-        else hipLaunchKernelGGL((k_trace<false, false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+        if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, true, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+        else if (ctr) RTG_TRACE(false, true, true);
+        else RTG_TRACE(false, false, true);
         return;
     }
-    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
-    else if (ctr) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
-    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, false, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+    else if (ctr) RTG_TRACE(false, true, false);
+    else RTG_TRACE(false, false, false);
+#undef RTG_TRACE
 }
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
@@ -2032,8 +2109,11 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     const NodePlanes np = node_planes(nodes, n);
     const ShadowPlanes sp = shadow_planes(shadows, cap);
     const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
+    const bool tl = sv.tlas_root >= 0;
     if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
+    else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
     else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
+    else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
     else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
     if (sv.num_lights > 1 && whitted)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, sp, np, n);

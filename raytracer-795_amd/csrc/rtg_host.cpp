@@ -343,6 +343,133 @@ int build_node4(const std::vector<HNode>& hn, int n, int prim_base, std::vector<
     return me;
 }
 
+// ------------------------------------------------------------------ top-level BVH (TLAS)
+// World box of one top-level entry: its geometry's root range box expanded by the eps overhang
+// of its candidates (prune_pad: an accepted triangle point may lie outside its triangle), mapped
+// through the model matrix (8 corners in double), swept by the motion-blur translation (the ray
+// origin moves by -blur * time, time in [0, 1): src/Helper.cpp:110-133), then widened by a
+// rounding margin far above the float error of the ray transform.  Non-finite -> false.
+struct TBox { double lo[3], hi[3]; };
+
+bool entry_world_box(const Mat4& M, const float mn[3], const float mx[3], float pad, const float blur[3], TBox& out) {
+    for (int z = 0; z < 3; z++) { out.lo[z] = 1e300; out.hi[z] = -1e300; }
+    double scale = 0.0;
+    for (int c = 0; c < 8; c++) {
+        const double p[3] = {(c & 1) ? (double)mx[0] + pad : (double)mn[0] - pad, (c & 2) ? (double)mx[1] + pad : (double)mn[1] - pad,
+                             (c & 4) ? (double)mx[2] + pad : (double)mn[2] - pad};
+        for (int r = 0; r < 3; r++) {
+            const double w = (double)M.c[0][r] * p[0] + (double)M.c[1][r] * p[1] + (double)M.c[2][r] * p[2] + (double)M.c[3][r];
+            if (!std::isfinite(w)) return false;
+            out.lo[r] = std::min(out.lo[r], w);
+            out.hi[r] = std::max(out.hi[r], w);
+            scale = std::max(scale, std::fabs(w));
+        }
+    }
+    for (int z = 0; z < 3; z++) {
+        if (!std::isfinite((double)blur[z])) return false;
+        out.lo[z] += std::min(0.0, (double)blur[z]);
+        out.hi[z] += std::max(0.0, (double)blur[z]);
+        scale = std::max(scale, std::fabs((double)blur[z]));
+    }
+    double ext = 0.0;
+    for (int z = 0; z < 3; z++) ext = std::max(ext, out.hi[z] - out.lo[z]);
+    const double margin = 1e-4 * (scale + ext) + 1e-6;
+    for (int z = 0; z < 3; z++) { out.lo[z] -= margin; out.hi[z] += margin; }
+    return true;
+}
+
+struct TlasRef {
+    int ref, count;          // count 0: interior node `ref`; > 0: leaf, entries tlas_idx[ref .. ref+count)
+    double lo[3], hi[3];
+};
+
+double half_area(const double lo[3], const double hi[3]) {
+    const double dx = std::max(0.0, hi[0] - lo[0]), dy = std::max(0.0, hi[1] - lo[1]), dz = std::max(0.0, hi[2] - lo[2]);
+    return dx * dy + dy * dz + dz * dx;
+}
+
+// Top-down SAH over the entries' box centres (sorted along the widest centre axis), BVH2 nodes
+// with both child boxes (the `Node` layout of the object trees); a leaf holds one entry, or every
+// remaining entry at depth kTlasMaxDepth so the GPU's TLAS stack (kTlasStack entries) never
+// overflows.  Child boxes are rounded outward to float.
+TlasRef tlas_rec(const std::vector<TBox>& box, std::vector<int>& idx, int s, int e, int depth, std::vector<Node>& nodes,
+                 std::vector<int>& leaves) {
+    TlasRef R;
+    for (int z = 0; z < 3; z++) { R.lo[z] = 1e300; R.hi[z] = -1e300; }
+    double clo[3] = {1e300, 1e300, 1e300}, chi[3] = {-1e300, -1e300, -1e300};
+    for (int k = s; k < e; k++)
+        for (int z = 0; z < 3; z++) {
+            const TBox& b = box[idx[k]];
+            R.lo[z] = std::min(R.lo[z], b.lo[z]);
+            R.hi[z] = std::max(R.hi[z], b.hi[z]);
+            const double c = 0.5 * (b.lo[z] + b.hi[z]);
+            clo[z] = std::min(clo[z], c);
+            chi[z] = std::max(chi[z], c);
+        }
+    if (e - s == 1 || depth >= kTlasMaxDepth) {
+        R.ref = (int)leaves.size();
+        R.count = e - s;
+        for (int k = s; k < e; k++) leaves.push_back(idx[k]);
+        return R;
+    }
+    int axis = 0;
+    for (int z = 1; z < 3; z++)
+        if (chi[z] - clo[z] > chi[axis] - clo[axis]) axis = z;
+    std::stable_sort(idx.begin() + s, idx.begin() + e, [&](int a, int b) {
+        return box[a].lo[axis] + box[a].hi[axis] < box[b].lo[axis] + box[b].hi[axis];
+    });
+    int split = (s + e) / 2;
+    if (chi[axis] > clo[axis]) {       // SAH sweep (equal centres everywhere: split by count)
+        const int n = e - s;
+        std::vector<double> right(n + 1, 0.0);
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (int k = n - 1; k >= 1; k--) {
+            const TBox& b = box[idx[s + k]];
+            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], b.lo[z]); hi[z] = std::max(hi[z], b.hi[z]); }
+            right[k] = half_area(lo, hi) * (n - k);
+        }
+        for (int z = 0; z < 3; z++) { lo[z] = 1e300; hi[z] = -1e300; }
+        double best = 1e308;
+        for (int k = 1; k < n; k++) {
+            const TBox& b = box[idx[s + k - 1]];
+            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], b.lo[z]); hi[z] = std::max(hi[z], b.hi[z]); }
+            const double cost = half_area(lo, hi) * k + right[k];
+            if (cost < best) { best = cost; split = s + k; }
+        }
+    }
+    const TlasRef L = tlas_rec(box, idx, s, split, depth + 1, nodes, leaves);
+    const TlasRef Rr = tlas_rec(box, idx, split, e, depth + 1, nodes, leaves);
+    const int me = (int)nodes.size();
+    nodes.emplace_back();
+    float b[2][6];
+    const TlasRef* ch[2] = {&L, &Rr};
+    for (int q = 0; q < 2; q++)
+        for (int z = 0; z < 3; z++) {
+            b[q][z] = std::nextafter((float)ch[q]->lo[z], -INFINITY);
+            b[q][3 + z] = std::nextafter((float)ch[q]->hi[z], INFINITY);
+        }
+    Node& nd = nodes[me];
+    nd.a = make_float4(b[0][0], b[0][1], b[0][2], b[0][3]);
+    nd.b = make_float4(b[0][4], b[0][5], b[1][0], b[1][1]);
+    nd.c = make_float4(b[1][2], b[1][3], b[1][4], b[1][5]);
+    nd.d = make_int4(L.ref, Rr.ref, L.count, Rr.count);
+    R.ref = me;
+    R.count = 0;
+    return R;
+}
+
+// Returns the TLAS root node, or -1 (a single entry: no TLAS).
+int build_tlas(const std::vector<TBox>& box, std::vector<Node>& nodes, std::vector<int>& leaves) {
+    const int n = (int)box.size();
+    if (n < 2) return -1;
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; i++) idx[i] = i;
+    nodes.clear();
+    leaves.clear();
+    const TlasRef root = tlas_rec(box, idx, 0, n, 0, nodes, leaves);
+    return root.count == 0 ? root.ref : -1;
+}
+
 // ------------------------------------------------------------------ device buffer helper
 struct DBuf {
     void* p = nullptr;
@@ -428,7 +555,10 @@ struct rtg_scene {
     std::vector<int> orig_prim;              // absolute BVH position -> original prim index
     SceneView sv{};
     DBuf d_tops, d_geoms, d_nodes, d_nodes4, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
-        d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf;
+        d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf, d_tlas, d_tlasidx;
+    int tlas_mode = 0;                       // rtg_build_opts.tlas
+    int tlas_root = -1;                      // top-level BVH root node (-1: linear object loop)
+    int tlas_count = 0;                      // its nodes
     int num_emit = 0;                        // hw7 object lights
     // render workspace
     std::vector<Lane> lanes;
@@ -530,7 +660,7 @@ static int validate(const rtg_scene_desc* d) {
 static std::vector<DBuf*> scene_buffers(rtg_scene* s) {
     return {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices,
             &s->d_vnormals, &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights,
-            &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf};
+            &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_tlas, &s->d_tlasidx};
 }
 
 // Point the kernels' SceneView at this scene's device buffers.
@@ -552,6 +682,8 @@ static void bind_view(rtg_scene* s) {
     sv.top_emit = s->d_topemit.as<int>();
     sv.emit_tris = s->d_etris.as<float>();
     sv.emit_cdf = s->d_ecdf.as<float>();
+    sv.tlas = s->d_tlas.as<Node>();
+    sv.tlas_idx = s->d_tlasidx.as<int>();
 }
 
 static void scene_free(rtg_scene* s) {
@@ -591,11 +723,13 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
 
     // matrices (objects, then instances)
     std::vector<Mat4> model(d->num_objects);
+    std::vector<Mat4> top_model;             // per top-level entry (objects, then instances)
     s->inv.clear(); s->invT.clear();
     for (int i = 0; i < d->num_objects; i++) {
         model[i] = compose(d, d->objects[i].xform_first, d->objects[i].xform_count);
         s->inv.push_back(inverse(model[i]));
         s->invT.push_back(inverse_transpose(model[i]));
+        top_model.push_back(model[i]);
     }
     for (int i = 0; i < d->num_instances; i++) {
         const rtg_instance_desc& in = d->instances[i];
@@ -603,6 +737,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         if (!in.reset_transform) m = mul(m, model[in.base_object]);
         s->inv.push_back(inverse(m));
         s->invT.push_back(inverse_transpose(m));
+        top_model.push_back(m);
     }
 
     // smooth vertex normals (src/Scene.cpp:302-318)
@@ -841,6 +976,30 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         T.ident = ident ? 1 : 0;
     }
 
+    // top-level BVH over the entries (objects, then instances): replaces the reference's linear
+    // object loop (src/Helper.cpp:32-73) for scenes with many objects
+    std::vector<Node> tlas_nodes;
+    std::vector<int> tlas_idx;
+    s->tlas_root = -1;
+    const int ntops = d->num_objects + d->num_instances;
+    const bool want_tlas = s->tlas_mode == 2 ? ntops >= 2 : (s->tlas_mode == 0 && ntops >= kTlasMinEntries);
+    if (want_tlas) {
+        std::vector<TBox> boxes(ntops);
+        bool ok = true;
+        for (int i = 0; i < ntops && ok; i++) {
+            const int gi = tops[i].geom;
+            const ObjBVH& ob = s->bvh[gi];
+            if (ob.root < 0) {            // no primitives: never hit; an empty box far away
+                for (int z = 0; z < 3; z++) { boxes[i].lo[z] = 1e300; boxes[i].hi[z] = -1e300; }
+                continue;
+            }
+            const HNode& r = ob.nodes[ob.root];
+            ok = entry_world_box(top_model[i], r.mn, r.mx, geoms[gi].prune_pad, tops[i].blur, boxes[i]);
+        }
+        if (ok) s->tlas_root = build_tlas(boxes, tlas_nodes, tlas_idx);
+        s->tlas_count = s->tlas_root >= 0 ? (int)tlas_nodes.size() : 0;
+    }
+
     // materials, textures, lights
     std::vector<MaterialDev> mats(d->num_materials);
     for (int i = 0; i < d->num_materials; i++) {
@@ -946,7 +1105,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         (rc = upload(s->d_vnormals, s->vnormals)) || (rc = upload(s->d_texcoords, tcflat)) ||
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
         (rc = upload(s->d_lights, lights)) || (rc = upload(s->d_origprim, s->orig_prim)) ||
-        (rc = upload(s->d_topemit, top_emit)) || (rc = upload(s->d_etris, etris)) || (rc = upload(s->d_ecdf, ecdf)))
+        (rc = upload(s->d_topemit, top_emit)) || (rc = upload(s->d_etris, etris)) || (rc = upload(s->d_ecdf, ecdf)) ||
+        (rc = upload(s->d_tlas, tlas_nodes)) || (rc = upload(s->d_tlasidx, tlas_idx)))
         return rc;
 
     SceneView& sv = s->sv;
@@ -957,6 +1117,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.num_textures = d->num_textures;
     sv.num_lights = d->num_lights;
     sv.num_emit = s->num_emit;
+    sv.tlas_root = s->tlas_root;
     sv.pt_flags = 0;
     sv.max_depth = d->max_recursion_depth;
     sv.shadow_eps = d->shadow_ray_eps;
@@ -995,6 +1156,7 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         if (!out) return fail(RTG_ERR_INVALID, "null out pointer");
         if (opts && (opts->bvh_builder < RTG_BVH_AUTO || opts->bvh_builder > RTG_BVH_GPU))
             return fail(RTG_ERR_INVALID, "bvh_builder");
+        if (opts && (opts->tlas < 0 || opts->tlas > 2)) return fail(RTG_ERR_INVALID, "tlas");
         *out = nullptr;
         int rc = validate(desc);
         if (rc) return rc;
@@ -1011,6 +1173,8 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         s->device = device;
         if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
         s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
+        s->tlas_mode = opts ? opts->tlas : 0;
+        if (const char* e = getenv("RTG_TLAS")) s->tlas_mode = atoi(e) == 0 ? 1 : 2;
         rc = build_scene(s, desc);
         if (rc) {
             scene_free(s);
@@ -1500,6 +1664,7 @@ int32_t rtg_scene_build_stats(const rtg_scene* s, rtg_build_stats* out) {
     out->bvh_build_ms = s->bvh_build_ms;
     out->bvh_gpu_objects = s->bvh_gpu_objects;
     out->num_objects = s->num_objects;
+    out->tlas_nodes = s->tlas_count;
     return RTG_OK;
 }
 

@@ -17,6 +17,9 @@ constexpr int kMaxLights = 64;      // per-node shadow slots are statically stri
 constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
 constexpr int kTraceBlock = 64;     // threads per traversal block (LDS stack: 128 B per lane)
 constexpr int kShadeBlock = 512;    // k_shade (simple variants): one queue atomic per block
+constexpr int kTlasMinEntries = 16; // top-level BVH over objects / instances from this many entries on
+constexpr int kTlasMaxDepth = 14;   // TLAS leaves at this depth take every remaining entry ...
+constexpr int kTlasStack = 16;      // ... so a near-first walk never pushes more than this
 
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:32-73):
 // objects first, then instances.  Read with scalar loads (wave-uniform loop).
@@ -154,6 +157,11 @@ struct SceneView {
     const float* emit_cdf;         // running float sum of the triangle areas per emitter
     int num_emit;
     int pt_flags;
+    // top-level BVH over the entries (Node layout: count 0 = interior child, > 0 = leaf holding
+    // entries tlas_idx[ref .. ref+count)); tlas_root -1: the reference's linear loop
+    const Node* tlas;
+    const int* tlas_idx;
+    int tlas_root;
 };
 
 // Path state of one path-tracing ray (per level, next to RayRec / RayMeta).

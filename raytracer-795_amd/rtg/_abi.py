@@ -129,11 +129,12 @@ class Ray(C.Structure):
 
 
 class BuildOpts(C.Structure):
-    _fields_ = [("bvh_builder", C.c_int32)]
+    _fields_ = [("bvh_builder", C.c_int32), ("tlas", C.c_int32)]
 
 
 class BuildStats(C.Structure):
-    _fields_ = [("bvh_build_ms", C.c_double), ("bvh_gpu_objects", C.c_int32), ("num_objects", C.c_int32)]
+    _fields_ = [("bvh_build_ms", C.c_double), ("bvh_gpu_objects", C.c_int32), ("num_objects", C.c_int32),
+                ("tlas_nodes", C.c_int32)]
 
 
 RTG_BVH_AUTO, RTG_BVH_HOST, RTG_BVH_GPU = 0, 1, 2

@@ -244,6 +244,67 @@ def cornell(nx=1920, ny=1080, spp=64, dof=True, level=2) -> Scene:
     return sc
 
 
+def spheres(nx=1920, ny=1080, spp=64, n=1024, seed=3) -> Scene:
+    """hw3 "Spheres DOF" analogue (pages/Page3.md:61) for the top-level BVH: `n` spheres, each its
+    own object (the reference tests every object per ray, src/Helper.cpp:32-51), jittered on a
+    ground quad; some transformed (scaling / translation / rotation), a few motion-blurred, two
+    instances of a small mesh; diffuse, mirror, glass and conductor materials; DoF camera, point
+    light, Whitted depth 3."""
+    rng = np.random.default_rng(seed)
+    sc = Scene(max_depth=3, background=(20, 30, 50), ambient=(12, 12, 12))
+    cam = _cam((0, 3.0, 15.0), (0, -0.2, -1), (0, 1, 0), nx, ny, fov_deg=50, spp=spp, name="spheres.png")
+    if spp > 1:
+        cam.is_dof, cam.focus_distance, cam.aperture_size = True, 14.0, 0.3
+    sc.cameras.append(cam)
+    cols = [(0.8, 0.2, 0.2), (0.2, 0.7, 0.2), (0.2, 0.3, 0.85), (0.8, 0.7, 0.2), (0.7, 0.3, 0.7), (0.9, 0.9, 0.9)]
+    for c in cols:
+        sc.materials.append(Material(ambient=(1, 1, 1), diffuse=c, specular=(0.5, 0.5, 0.5), phong_exp=30))
+    sc.materials.append(Material(type=A.MAT_MIRROR, ambient=(0.1, 0.1, 0.1), diffuse=(0.1, 0.1, 0.1),
+                                 specular=(0.4, 0.4, 0.4), mirror=(0.8, 0.8, 0.8), phong_exp=60))
+    sc.materials.append(Material(type=A.MAT_DIELECTRIC, ambient=(0, 0, 0), diffuse=(0, 0, 0), specular=(0, 0, 0),
+                                 refraction_index=1.5, absorption_coeff=(0.05, 0.02, 0.01)))
+    sc.materials.append(Material(type=A.MAT_CONDUCTOR, ambient=(0.1, 0.1, 0.1), diffuse=(0.1, 0.1, 0.1),
+                                 specular=(0.5, 0.5, 0.5), mirror=(0.9, 0.7, 0.4), phong_exp=80,
+                                 refraction_index=0.37, absorption_index=2.82))
+    sc.materials.append(Material(ambient=(1, 1, 1), diffuse=(0.5, 0.5, 0.5), specular=(0, 0, 0), phong_exp=1))
+    side = int(math.ceil(math.sqrt(n)))
+    r = rng.uniform(0.2, 0.42, n).astype(f32)
+    gx = (np.arange(n) % side).astype(f32)
+    gz = (np.arange(n) // side).astype(f32)
+    x = (gx - side / 2 + 0.5) * (32.0 / side) + rng.uniform(-0.2, 0.2, n)
+    z = (gz - side / 2 + 0.5) * (32.0 / side) + rng.uniform(-0.2, 0.2, n) - 6.0
+    y = -1.0 + r
+    c = _add_vertices(sc, np.stack([x, y, z], -1))
+    sc.translations += [(0.0, 0.3, 0.0), (0.4, 0.0, -0.3)]
+    sc.scalings += [(1.0, 1.6, 1.0), (0.7, 0.7, 0.7)]
+    sc.rotations += [(25.0, 0.0, 0.0, 1.0)]
+    mats = rng.choice(len(sc.materials) - 1, n, p=[0.13] * 6 + [0.08, 0.08, 0.06]) + 1
+    for k in range(n):
+        xf = []
+        if k % 11 == 3:
+            xf = [(A.XF_TRANSLATION, 1), (A.XF_SCALING, 1)]
+        elif k % 13 == 5:
+            xf = [(A.XF_ROTATION, 1), (A.XF_SCALING, 2), (A.XF_TRANSLATION, 2)]
+        blur = (0.0, 0.25, 0.0) if k % 37 == 7 else (0.0, 0.0, 0.0)
+        sc.objects.append(Object(type=A.OBJ_SPHERE, id=k + 1, material=int(mats[k]), center=c + k, radius=float(r[k]),
+                                 xforms=xf, blur=blur))
+    fl = _add_vertices(sc, [(-40, -1.0, 40), (40, -1.0, 40), (40, -1.0, -40), (-40, -1.0, -40)])
+    sc.objects.append(Object(type=A.OBJ_MESH, id=n + 1, material=len(sc.materials),
+                             faces=np.array([[fl, fl + 1, fl + 2], [fl, fl + 2, fl + 3]], np.int32)))
+    iv, ifc = icosphere(1)
+    ib = _add_vertices(sc, iv * 0.6)
+    sc.objects.append(Object(type=A.OBJ_MESH, id=n + 2, material=5, faces=(ifc + ib).astype(np.int32),
+                             xforms=[(A.XF_TRANSLATION, 1)]))
+    sc.translations += [(-3.0, 0.0, 2.0), (3.0, 0.2, 1.0)]
+    base = len(sc.objects) - 1
+    sc.instances.append(Instance(base_object=base, id=n + 3, material=7, reset_transform=False,
+                                 xforms=[(A.XF_TRANSLATION, 3)]))
+    sc.instances.append(Instance(base_object=base, id=n + 4, material=8, reset_transform=True,
+                                 xforms=[(A.XF_TRANSLATION, 4), (A.XF_SCALING, 1)], blur=(0.2, 0.0, 0.0)))
+    sc.lights.append(Light(type=A.LIGHT_POINT, position=(2, 12, 8), intensity=(60000, 60000, 60000)))
+    return sc
+
+
 PT_ALL = A.PT_IMPORTANCE | A.PT_NEE | A.PT_RUSSIAN_ROULETTE
 
 
