@@ -569,12 +569,21 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         for (int i = 0; i < sv.num_tops; i++) visit(i);
         return out;
     }
-    // top-level walk: a child box is skipped when the ray line misses it, when it lies wholly
-    // behind the origin (accepted hits have t > 0) or wholly beyond the winner so far (its hits
-    // would have t > nearest).  The boxes carry the host's rounding margins; the reciprocal slab
-    // adds 2^-18 of the magnitudes, and NaN comparisons keep a box.
+    // top-level walk.  A child box is skipped when the ray line misses it (its entries' hit points
+    // lie on the line and in the box: host margins cover the rounding, the reciprocal slab adds
+    // 2^-18 of the magnitudes, NaN comparisons keep a box).  Distance pruning -- boxes wholly
+    // behind the origin or wholly beyond the winner so far -- needs gett()'s error: gett divides
+    // by the first nonzero object-space direction component a (src/Ray.cpp:21-36), so a tiny d_a
+    // makes t coarse (two spheres at different depths can get the same t).  For axis-aligned
+    // entries that error is at most 2^-22 (|t| + K_a / |d_a|) with K_a the scene's bound on
+    // |coordinate| + |translation| + |blur| along a (SceneView::tlas_k); pruning allows 16 times
+    // that.  Subtrees of other entries (rotations, shears) carry kTlasNoPrune: line test only.
     const f3 winv = mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    auto tchild = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& key) -> bool {
+    const float ka = d.x != 0.0f ? sv.tlas_k[0] : (d.y != 0.0f ? sv.tlas_k[1] : sv.tlas_k[2]);
+    const float da = d.x != 0.0f ? adx : (d.y != 0.0f ? ady : adz);
+    const float slack0 = 3.814697265625e-6f * (ka / da) + 1e-30f;        // 2^-18 K_a / |d_a|
+    auto beyond = [&](float k) { return k > nearest + (3.814697265625e-6f * nearest + slack0); };
+    auto tchild = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool prune, float& key) -> bool {
         const float ax = (mnx - o.x) * winv.x, bx = (mxx - o.x) * winv.x;
         const float ay = (mny - o.y) * winv.y, by = (mxy - o.y) * winv.y;
         const float az = (mnz - o.z) * winv.z, bz = (mxz - o.z) * winv.z;
@@ -583,8 +592,9 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         const float e = (fabsf(sl) + fabsf(le)) * 3.814697265625e-6f + 1e-30f;   // 2^-18
         key = le - e;
         if (sl + e < key) return false;
-        if (sl + e < 0.0f) return false;
-        return !(key > nearest * (1.0f + 1e-5f) + 1e-30f);
+        if (!prune) return true;
+        if (sl + e < -slack0) return false;
+        return !beyond(key);
     };
     auto tleaf = [&](int ref, int cnt) {
         for (int k = ref; k < ref + cnt; k++) visit(sv.tlas_idx[k]);
@@ -593,22 +603,23 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     int cur = sv.tlas_root;
     while (true) {
         const Node nd = sv.tlas[cur];
-        const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
+        const bool lpr = !(nd.d.x & kTlasNoPrune), rpr = !(nd.d.y & kTlasNoPrune);
+        const int lref = nd.d.x & ~kTlasNoPrune, rref = nd.d.y & ~kTlasNoPrune, lcnt = nd.d.z, rcnt = nd.d.w;
         float lk = 0.0f, rk = 0.0f;
-        bool lok = lcnt >= 0 && tchild(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lk);
-        bool rok = rcnt >= 0 && tchild(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rk);
+        bool lok = lcnt >= 0 && tchild(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lpr, lk);
+        bool rok = rcnt >= 0 && tchild(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rpr, rk);
         const bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
-        auto still = [&](float k) { return !(k > nearest * (1.0f + 1e-5f) + 1e-30f); };
+        auto still = [&](float k, bool prune) { return !prune || !beyond(k); };
         if (lleaf && rleaf && rk < lk) {
             tleaf(rref, rcnt);
-            if (still(lk)) tleaf(lref, lcnt);
+            if (still(lk, lpr)) tleaf(lref, lcnt);
             lok = rok = false;
         } else {
             if (lleaf) { tleaf(lref, lcnt); lok = false; }
-            if (rleaf) { if (still(rk)) tleaf(rref, rcnt); rok = false; }
+            if (rleaf) { if (still(rk, rpr)) tleaf(rref, rcnt); rok = false; }
         }
-        lok = lok && still(lk);
-        rok = rok && still(rk);
+        lok = lok && still(lk, lpr);
+        rok = rok && still(rk, rpr);
         if (lok && rok) {
             int nearc = lref, farc = rref;
             if (rk < lk) { nearc = rref; farc = lref; }

@@ -458,16 +458,53 @@ TlasRef tlas_rec(const std::vector<TBox>& box, std::vector<int>& idx, int s, int
     return R;
 }
 
-// Returns the TLAS root node, or -1 (a single entry: no TLAS).
-int build_tlas(const std::vector<TBox>& box, std::vector<Node>& nodes, std::vector<int>& leaves) {
+// Mark every child reference of the subtree under node `n` "no distance pruning".
+void tlas_mark_noprune(std::vector<Node>& nodes, int n) {
+    Node& nd = nodes[n];
+    const int l = nd.d.x, r = nd.d.y, lc = nd.d.z, rc = nd.d.w;
+    if (lc == 0) tlas_mark_noprune(nodes, l);
+    if (rc == 0) tlas_mark_noprune(nodes, r);
+    nd.d.x = l | kTlasNoPrune;
+    nd.d.y = r | kTlasNoPrune;
+}
+
+// Returns the TLAS root node, or -1 (a single entry: no TLAS).  Entries whose transform is
+// axis-aligned (aligned[i]) and the others go to separate subtrees under the root; the others'
+// child references carry kTlasNoPrune (their gett() error has no world-space bound, so only
+// boxes the ray line misses are skipped there).
+int build_tlas(const std::vector<TBox>& box, const std::vector<char>& aligned, std::vector<Node>& nodes,
+               std::vector<int>& leaves) {
     const int n = (int)box.size();
     if (n < 2) return -1;
-    std::vector<int> idx(n);
-    for (int i = 0; i < n; i++) idx[i] = i;
+    std::vector<int> A, B;
+    for (int i = 0; i < n; i++) (aligned[i] ? A : B).push_back(i);
     nodes.clear();
     leaves.clear();
-    const TlasRef root = tlas_rec(box, idx, 0, n, 0, nodes, leaves);
-    return root.count == 0 ? root.ref : -1;
+    auto sub = [&](std::vector<int>& idx, int depth) { return tlas_rec(box, idx, 0, (int)idx.size(), depth, nodes, leaves); };
+    if (B.empty() || A.empty()) {
+        std::vector<int>& all = B.empty() ? A : B;
+        const TlasRef root = sub(all, 0);
+        if (root.count != 0) return -1;
+        if (A.empty()) tlas_mark_noprune(nodes, root.ref);
+        return root.ref;
+    }
+    const TlasRef ra = sub(A, 1), rb = sub(B, 1);
+    if (rb.count == 0) tlas_mark_noprune(nodes, rb.ref);
+    const int me = (int)nodes.size();
+    nodes.emplace_back();
+    float b[2][6];
+    const TlasRef* ch[2] = {&ra, &rb};
+    for (int q = 0; q < 2; q++)
+        for (int z = 0; z < 3; z++) {
+            b[q][z] = std::nextafter((float)ch[q]->lo[z], -INFINITY);
+            b[q][3 + z] = std::nextafter((float)ch[q]->hi[z], INFINITY);
+        }
+    Node& nd = nodes[me];
+    nd.a = make_float4(b[0][0], b[0][1], b[0][2], b[0][3]);
+    nd.b = make_float4(b[0][4], b[0][5], b[1][0], b[1][1]);
+    nd.c = make_float4(b[1][2], b[1][3], b[1][4], b[1][5]);
+    nd.d = make_int4(ra.ref, rb.ref | kTlasNoPrune, ra.count, rb.count);
+    return me;
 }
 
 // ------------------------------------------------------------------ device buffer helper
@@ -559,6 +596,7 @@ struct rtg_scene {
     int tlas_mode = 0;                       // rtg_build_opts.tlas
     int tlas_root = -1;                      // top-level BVH root node (-1: linear object loop)
     int tlas_count = 0;                      // its nodes
+    float tlas_k[3] = {0, 0, 0};             // per axis: bound of |object-space coordinate x scale| over aligned entries
     int num_emit = 0;                        // hw7 object lights
     // render workspace
     std::vector<Lane> lanes;
@@ -983,8 +1021,10 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     s->tlas_root = -1;
     const int ntops = d->num_objects + d->num_instances;
     const bool want_tlas = s->tlas_mode == 2 ? ntops >= 2 : (s->tlas_mode == 0 && ntops >= kTlasMinEntries);
+    for (int z = 0; z < 3; z++) s->tlas_k[z] = 0.0f;
     if (want_tlas) {
         std::vector<TBox> boxes(ntops);
+        std::vector<char> aligned(ntops, 0);
         bool ok = true;
         for (int i = 0; i < ntops && ok; i++) {
             const int gi = tops[i].geom;
@@ -995,8 +1035,23 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             }
             const HNode& r = ob.nodes[ob.root];
             ok = entry_world_box(top_model[i], r.mn, r.mx, geoms[gi].prune_pad, tops[i].blur, boxes[i]);
+            // axis-aligned: the inverse's 3x3 part is diagonal (scaling / translation / blur only),
+            // so the object-space direction has the world direction's zero pattern and gett()'s
+            // error is bounded in world terms (closest_hit, TLAS pruning)
+            const Mat4& iv = s->inv[i];
+            bool al = true;
+            for (int c = 0; c < 3; c++)
+                for (int r2 = 0; r2 < 3; r2++)
+                    al = al && (c == r2 ? (std::isfinite(iv.c[c][r2]) && iv.c[c][r2] != 0.0f) : iv.c[c][r2] == 0.0f);
+            aligned[i] = al;
+            if (al && ok)
+                for (int z = 0; z < 3; z++) {
+                    const double k = std::max(std::fabs(boxes[i].lo[z]), std::fabs(boxes[i].hi[z])) +
+                                     std::fabs((double)tops[i].blur[z]) + std::fabs((double)top_model[i].c[3][z]);
+                    s->tlas_k[z] = std::max(s->tlas_k[z], (float)(k * 1.01));
+                }
         }
-        if (ok) s->tlas_root = build_tlas(boxes, tlas_nodes, tlas_idx);
+        if (ok) s->tlas_root = build_tlas(boxes, aligned, tlas_nodes, tlas_idx);
         s->tlas_count = s->tlas_root >= 0 ? (int)tlas_nodes.size() : 0;
     }
 
@@ -1118,6 +1173,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.num_lights = d->num_lights;
     sv.num_emit = s->num_emit;
     sv.tlas_root = s->tlas_root;
+    for (int z = 0; z < 3; z++) sv.tlas_k[z] = s->tlas_k[z];
     sv.pt_flags = 0;
     sv.max_depth = d->max_recursion_depth;
     sv.shadow_eps = d->shadow_ray_eps;

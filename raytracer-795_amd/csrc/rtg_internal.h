@@ -20,6 +20,7 @@ constexpr int kShadeBlock = 512;    // k_shade (simple variants): one queue atom
 constexpr int kTlasMinEntries = 16; // top-level BVH over objects / instances from this many entries on
 constexpr int kTlasMaxDepth = 14;   // TLAS leaves at this depth take every remaining entry ...
 constexpr int kTlasStack = 16;      // ... so a near-first walk never pushes more than this
+constexpr int kTlasNoPrune = 0x40000000;   // TLAS child ref flag: no distance / behind-origin pruning
 
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:32-73):
 // objects first, then instances.  Read with scalar loads (wave-uniform loop).
@@ -162,6 +163,7 @@ struct SceneView {
     const Node* tlas;
     const int* tlas_idx;
     int tlas_root;
+    float tlas_k[3];               // gett() error scale of the axis-aligned entries (closest_hit)
 };
 
 // Path state of one path-tracing ray (per level, next to RayRec / RayMeta).

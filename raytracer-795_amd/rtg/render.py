@@ -117,7 +117,7 @@ class Renderer:
     def build_stats(self) -> dict:
         b = A.BuildStats()
         A.check(self.lib.rtg_scene_build_stats(self.handle, C.byref(b)), self.lib)
-        return {"bvh_build_ms": b.bvh_build_ms, "bvh_gpu_objects": b.bvh_gpu_objects, "num_objects": b.num_objects}
+        return {k: getattr(b, k) for k, _ in A.BuildStats._fields_}
 
     def bvh(self, obj: int):
         return _bvh(self.lib.rtg_scene_object_bvh, self.handle, obj)

@@ -115,3 +115,29 @@ def test_tlas_trace_random_rays_match_oracle(gpu):
     m = ref["full"] == 1
     for k in ("t", "point", "normal"):
         assert np.array_equal(h[k][m].view(np.int32), ref[k][m].view(np.int32)), k
+
+
+def test_tlas_gett_ties_from_a_tiny_direction_component(gpu):
+    """gett() divides by the first nonzero direction component (src/Ray.cpp:21-36): with a tiny x
+    component it quantises t so coarsely that spheres at different depths tie, and the first in
+    the loop must win.  The ray below is one such case from the 1080p64 spheres frame (level-1
+    reflection, row 519); the batch around it varies the tiny component and the origin."""
+    sc = scenegen.spheres(8, 6, spp=1)
+    rng = np.random.default_rng(23)
+    n = 20000
+    o = np.float32([-1.411496639251709, -0.4932418763637543, -4.315512657165527]) + \
+        rng.uniform(-3, 3, (n, 3)).astype(np.float32) * np.float32([1, 0.1, 1])
+    d = np.empty((n, 3), np.float32)
+    d[:, 0] = rng.choice([-1, 1], n) * 10.0 ** rng.uniform(-8, -5, n)
+    ang = rng.uniform(-0.6, 0.3, n)
+    d[:, 1] = np.sin(ang)
+    d[:, 2] = -np.cos(ang)
+    d[0] = [6.705522537231445e-07, -0.2306806743144989, -0.9730295538902283]
+    o[0] = [-1.411496639251709, -0.4932418763637543, -4.315512657165527]
+    ref = pyoracle.Oracle(sc).trace(o, d)
+    with rtg.Renderer(sc, device=0, tlas=TLAS_ON) as r:
+        h = r.trace(o, d)
+    for k in ("full", "object", "prim", "material"):
+        assert np.array_equal(h[k], ref[k]), k
+    m = ref["full"] == 1
+    assert np.array_equal(h["t"][m].view(np.int32), ref["t"][m].view(np.int32))
