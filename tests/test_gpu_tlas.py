@@ -141,3 +141,15 @@ def test_tlas_gett_ties_from_a_tiny_direction_component(gpu):
         assert np.array_equal(h[k], ref[k]), k
     m = ref["full"] == 1
     assert np.array_equal(h["t"][m].view(np.int32), ref["t"][m].view(np.int32))
+
+
+def test_full_frame_tlas_equals_linear_loop(gpu):
+    """The 1080p spheres frame (8 spp): the TLAS and the linear object loop give the same image
+    bit for bit and the same ray counts (the size at which the gett() tie above was found)."""
+    sc = scenegen.spheres(1920, 1080, spp=8)
+    a, sa, _ = _render(sc, TLAS_OFF)
+    b, sb, bs = _render(sc, TLAS_ON)
+    assert bs["tlas_nodes"] > 0
+    assert np.array_equal(_bits(a), _bits(b))
+    for k in ("primary_rays", "secondary_rays", "shadow_rays"):
+        assert sa[k] == sb[k], k
