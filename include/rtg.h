@@ -321,6 +321,9 @@ typedef struct rtg_build_opts {
                                 linear object loop (src/Helper.cpp:32-73) with the same result (ties
                                 to the first entry): 0 = auto (>= 16 entries), 1 = off, 2 = on
                                 (>= 2 entries); env RTG_TLAS=0/1 overrides */
+    int32_t traversal_tree;  /* 0 = fast rays walk an SAH 4-wide tree per mesh (candidates checked for
+                                reachability in the reference tree, ties in its order: same results);
+                                1 = the reference tree only; env RTG_SAH=0/1 overrides */
 } rtg_build_opts;
 /* rtg_scene_create with build options (NULL = defaults). */
 int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rtg_build_opts* opts,

@@ -425,23 +425,38 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         }
                     }
                 };
-                // 4-wide walk over the collapsed tree (fast reciprocal path only; exhaustive
-                // traversal and rays with a zero / denormal / huge direction component use the
-                // exact BVH2 walk).  Slots of a collapsed child c need c's box hit too.  The
-                // exact slab predicate is monotone under box containment here (no zero direction
-                // component), so a slot whose own box -- or whose pair sibling's box -- is
-                // certainly hit implies c's hit; interior slots are themselves box-tested; only a
-                // leaf slot without such a witness tests the pair union (= c's range box)
-                // explicitly.  A stack that would overflow (> kStackDepth entries: up to 3
-                // pushes per level) restarts the object on the BVH2 walk, whose depth bound
-                // fits; candidates already found stay valid.
-                bool use2 = EXHAUSTIVE || !fast;
+                // Fast rays walk the mesh's traversal tree (SAH, 4-wide; rtg_host.cpp): slots are
+                // pruned by the parameter window only (boxes padded by the eps overhang), leaves are
+                // tested nearer-first as they are reached, interior slots visited nearest-first.  A
+                // candidate that would become the object's winner must be reachable in the
+                // reference tree: its reference leaf's parent box (the only ancestor box that can
+                // fail when the candidate lies outside its triangle) gets the exact slab test.
+                // Exhaustive traversal, rays with a zero / denormal / huge direction component and
+                // a stack that would overflow (> kStackDepth entries) use the reference tree's BVH2
+                // walk; candidates already accepted stay valid (they are reachable).
+                bool use2 = EXHAUSTIVE || !fast || g.sah_base < 0;
                 if (!use2) {
+                    auto test_sah = [&](const TriGeom& tg) {
+                        if (STATS) st.tris++;
+                        Cand c = tri_test(tg, o2, d2, eps);
+                        if (!c.ok) return;
+                        const float dist = norm(c.p - o2);
+                        const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
+                        if (!(dist < FLT_MAX &&
+                              (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))))
+                            return;
+                        if (__float_as_int(tg.p2.w)) {          // src/BVH.cpp:178 on the leaf's parent
+                            const float* gb = sv.gates + 6 * (size_t)k;
+                            if (!box_hit(o2, d2, inv, fast, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) return;
+                        }
+                        best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                        if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+                    };
                     int sp = 0;
-                    int cur = g.node4_base;
+                    int cur = g.sah_base;
                     while (true) {
                         if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
-                        const Node4 nd = sv.nodes4[cur];
+                        const Node4 nd = sv.snodes[cur];
                         const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
                         const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
                         const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
@@ -450,10 +465,8 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
                         const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
                         const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
-                        // branch-free slot tests: ok (reachable and inside the window), sure (box
-                        // certainly hit), gate (interior slot in the uncertain band)
                         float key[4];
-                        int okm = 0, surem = 0, gate_mask = 0, leafm = 0;
+                        int okm = 0, leafm = 0;
 #pragma unroll
                         for (int j = 0; j < 4; j++) {
                             const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
@@ -464,49 +477,11 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                             const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
                             const float lo = le - e - padt, hi = sl + e + padt;
                             key[j] = lo;
-                            const bool valid = inf[j] >= 0;
-                            const bool isleaf = (inf[j] & kSlotCount) != 0;
-                            const bool win = !(hi < lo || hi < tlo || lo > thi);
-                            const bool miss = sl < le - e;
-                            const bool sure = sl >= le + e;
-                            const bool ok = valid & win & (isleaf | !miss);
+                            const bool ok = inf[j] >= 0 && !(hi < lo || hi < tlo || lo > thi);
                             okm |= ok << j;
-                            surem |= sure << j;
-                            gate_mask |= (ok & !isleaf & !sure) << j;
-                            leafm |= (valid & isleaf) << j;
+                            leafm |= (inf[j] > 0) << j;
                         }
-                        // own exact tests of uncertain interior slots (rare)
-                        while (gate_mask) {
-                            const int j = __builtin_ctz(gate_mask);
-                            gate_mask &= gate_mask - 1;
-                            const float a0 = j == 0 ? lx[0] : j == 1 ? lx[1] : j == 2 ? lx[2] : lx[3];
-                            const float a1 = j == 0 ? ly[0] : j == 1 ? ly[1] : j == 2 ? ly[2] : ly[3];
-                            const float a2 = j == 0 ? lz[0] : j == 1 ? lz[1] : j == 2 ? lz[2] : lz[3];
-                            const float b0 = j == 0 ? hx[0] : j == 1 ? hx[1] : j == 2 ? hx[2] : hx[3];
-                            const float b1 = j == 0 ? hy[0] : j == 1 ? hy[1] : j == 2 ? hy[2] : hy[3];
-                            const float b2 = j == 0 ? hz[0] : j == 1 ? hz[1] : j == 2 ? hz[2] : hz[3];
-                            if (box_test_slow(o2, d2, a0, a1, a2, b0, b1, b2)) surem |= 1 << j;
-                            else okm &= ~(1 << j);
-                        }
-                        // collapsed-child gates (pair union box), once per pair: needed only for a
-                        // reachable leaf slot when neither slot of the pair is certainly hit
-#pragma unroll
-                        for (int q = 0; q < 4; q += 2) {
-                            const int g0 = inf[q], g1 = inf[q + 1];
-                            const bool gated = ((g0 >= 0) & ((g0 & kSlotGate) != 0)) | ((g1 >= 0) & ((g1 & kSlotGate) != 0));
-                            const int pm = 3 << q;
-                            if (gated && (okm & leafm & pm) && !(surem & pm)) {
-                                const bool b0 = g0 >= 0, b1 = g1 >= 0;
-                                const float ux = b0 && b1 ? fminf(lx[q], lx[q + 1]) : (b0 ? lx[q] : lx[q + 1]);
-                                const float uy = b0 && b1 ? fminf(ly[q], ly[q + 1]) : (b0 ? ly[q] : ly[q + 1]);
-                                const float uz = b0 && b1 ? fminf(lz[q], lz[q + 1]) : (b0 ? lz[q] : lz[q + 1]);
-                                const float vx = b0 && b1 ? fmaxf(hx[q], hx[q + 1]) : (b0 ? hx[q] : hx[q + 1]);
-                                const float vy = b0 && b1 ? fmaxf(hy[q], hy[q + 1]) : (b0 ? hy[q] : hy[q + 1]);
-                                const float vz = b0 && b1 ? fmaxf(hz[q], hz[q + 1]) : (b0 ? hz[q] : hz[q + 1]);
-                                if (!box_test_slow(o2, d2, ux, uy, uz, vx, vy, vz)) okm &= ~pm;
-                            }
-                        }
-                        // interior candidates first, so the node's boxes are dead during leaf tests
+                        // interior slots first, so the node's boxes are dead during the leaf tests
                         float k4[4];
                         int r4[4];
 #pragma unroll
@@ -516,15 +491,14 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                             r4[j] = take ? rf[j] : -1;
                         }
                         int leaf_mask = okm & leafm;
-                        // leaves now, one code site (thi may shrink between them)
-                        while (leaf_mask) {
+                        while (leaf_mask) {          // leaves now, one code site (thi may shrink between them)
                             const int j = __builtin_ctz(leaf_mask);
                             leaf_mask &= leaf_mask - 1;
                             const float kj = j == 0 ? key[0] : j == 1 ? key[1] : j == 2 ? key[2] : key[3];
                             if (kj > thi) continue;
                             const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
-                            const int info = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
-                            leaf(start, info & kSlotCount);
+                            const int cnt = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
+                            for (int q = start; q < start + cnt; q++) test_sah(sv.stris[q]);
                         }
 #pragma unroll
                         for (int j = 0; j < 4; j++)

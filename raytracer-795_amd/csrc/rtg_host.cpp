@@ -293,44 +293,150 @@ int construct(BuildCtx& B, int start, int end, int splitType, int depth) {
     return n;
 }
 
-// Collapse the BVH2 below interior node n into 4-wide nodes (pre-order, returns the index).
-int build_node4(const std::vector<HNode>& hn, int n, int prim_base, std::vector<Node4>& out) {
-    int me = (int)out.size();
-    out.emplace_back();
-    float lo[3][4], hi[3][4];
-    int ref[4], info[4];
-    int pending[4] = {-1, -1, -1, -1};    // interior grandchildren to build after this node
-    auto set_slot = [&](int j, int c, bool gated) {
-        if (c < 0) {
-            for (int z = 0; z < 3; z++) { lo[z][j] = 0.0f; hi[z][j] = 0.0f; }
-            ref[j] = 0; info[j] = -1;
-            return;
-        }
-        const HNode& h = hn[c];
-        for (int z = 0; z < 3; z++) { lo[z][j] = h.mn[z]; hi[z][j] = h.mx[z]; }
-        if (h.left < 0 && h.right < 0) {
-            int len = h.end - h.start;
-            ref[j] = prim_base + h.start;
-            info[j] = len > 0 ? (len | (gated ? kSlotGate : 0)) : -1;
-        } else {
-            ref[j] = 0;
-            info[j] = gated ? kSlotGate : 0;
-            pending[j] = c;
-        }
-    };
-    const int ch[2] = {hn[n].left, hn[n].right};
-    for (int q = 0; q < 2; q++) {
-        int c = ch[q];
-        if (c >= 0 && (hn[c].left >= 0 || hn[c].right >= 0)) {
-            set_slot(2 * q, hn[c].left, true);
-            set_slot(2 * q + 1, hn[c].right, true);
-        } else {
-            set_slot(2 * q, c, false);
-            set_slot(2 * q + 1, -1, false);
+// ------------------------------------------------------------------ traversal tree (SAH, 4-wide)
+// The reference's median-split tree (one primitive per leaf, axis = depth % 3) decides *which*
+// candidates exist -- a primitive counts only if every interior box above its leaf is hit
+// (src/BVH.cpp:137-210) -- but not how fast they are found.  Fast rays walk a second tree per
+// mesh: binned SAH over the triangle boxes, leaves of <= 4 triangles, collapsed to 4-wide nodes.
+// Its boxes only prune (padded by the eps overhang, like the reference tree's); reachability in
+// the reference tree is checked per winning candidate against its reference leaf's parent box
+// (the exact slab predicate is monotone under box containment for nonzero finite directions,
+// so that one box decides the whole ancestor chain), and ties keep the reference's order
+// (distance, rightmost reference leaf, lowest position).
+struct SahBox { float lo[3], hi[3]; };
+struct SahNode2 {
+    float lo[3], hi[3];
+    int left, right;          // children (-1 for a leaf)
+    int start, count;         // leaf range in the SAH primitive order
+};
+
+constexpr int kSahBins = 16;
+constexpr int kSahMaxLeaf = 4;
+
+inline double sah_area(const float lo[3], const float hi[3]) {
+    const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+int sah_rec(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::vector<int>& idx, int s, int e,
+            std::vector<SahNode2>& out) {
+    SahNode2 nd;
+    float clo[3], chi[3];
+    for (int z = 0; z < 3; z++) { nd.lo[z] = clo[z] = FLT_MAX; nd.hi[z] = chi[z] = -FLT_MAX; }
+    for (int k = s; k < e; k++) {
+        const SahBox& b = pb[idx[k]];
+        const float c[3] = {pc[idx[k]].x, pc[idx[k]].y, pc[idx[k]].z};
+        for (int z = 0; z < 3; z++) {
+            nd.lo[z] = std::min(nd.lo[z], b.lo[z]);
+            nd.hi[z] = std::max(nd.hi[z], b.hi[z]);
+            clo[z] = std::min(clo[z], c[z]);
+            chi[z] = std::max(chi[z], c[z]);
         }
     }
-    for (int j = 0; j < 4; j++)
-        if (pending[j] >= 0) ref[j] = build_node4(hn, pending[j], prim_base, out);
+    nd.left = nd.right = -1;
+    nd.start = s;
+    nd.count = e - s;
+    const int me = (int)out.size();
+    out.push_back(nd);
+    const int n = e - s;
+    if (n <= 1) return me;
+    int axis = 0;
+    for (int z = 1; z < 3; z++)
+        if (chi[z] - clo[z] > chi[axis] - clo[axis]) axis = z;
+    const float ext = chi[axis] - clo[axis];
+    int mid = -1;
+    if (ext > 0.0f) {
+        int cnt[kSahBins] = {};
+        float blo[kSahBins][3], bhi[kSahBins][3];
+        for (int b = 0; b < kSahBins; b++)
+            for (int z = 0; z < 3; z++) { blo[b][z] = FLT_MAX; bhi[b][z] = -FLT_MAX; }
+        const float sc = (float)kSahBins / ext;
+        auto bin_of = [&](int p) {
+            const float c = axis == 0 ? pc[p].x : (axis == 1 ? pc[p].y : pc[p].z);
+            return std::min(kSahBins - 1, std::max(0, (int)((c - clo[axis]) * sc)));
+        };
+        for (int k = s; k < e; k++) {
+            const int b = bin_of(idx[k]);
+            cnt[b]++;
+            for (int z = 0; z < 3; z++) {
+                blo[b][z] = std::min(blo[b][z], pb[idx[k]].lo[z]);
+                bhi[b][z] = std::max(bhi[b][z], pb[idx[k]].hi[z]);
+            }
+        }
+        double rcost[kSahBins];
+        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        int rc = 0;
+        for (int b = kSahBins - 1; b >= 1; b--) {
+            rc += cnt[b];
+            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], blo[b][z]); hi[z] = std::max(hi[z], bhi[b][z]); }
+            rcost[b] = rc ? sah_area(lo, hi) * rc : 0.0;
+        }
+        for (int z = 0; z < 3; z++) { lo[z] = FLT_MAX; hi[z] = -FLT_MAX; }
+        int lc = 0, best_b = -1;
+        double best = 1e300;
+        for (int b = 0; b < kSahBins - 1; b++) {
+            lc += cnt[b];
+            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], blo[b][z]); hi[z] = std::max(hi[z], bhi[b][z]); }
+            if (lc == 0 || lc == n) continue;
+            const double cost = sah_area(lo, hi) * lc + rcost[b + 1];
+            if (cost < best) { best = cost; best_b = b; }
+        }
+        // leaf when splitting does not pay (traversal step ~ one triangle test)
+        const double leaf_cost = sah_area(nd.lo, nd.hi) * n;
+        if (n <= kSahMaxLeaf && (best_b < 0 || leaf_cost <= sah_area(nd.lo, nd.hi) + best)) return me;
+        if (best_b >= 0) {
+            int* first = idx.data() + s;
+            int* pivot = std::partition(first, idx.data() + e, [&](int p) { return bin_of(p) <= best_b; });
+            mid = (int)(pivot - idx.data());
+        }
+    } else if (n <= kSahMaxLeaf) {
+        return me;
+    }
+    if (mid <= s || mid >= e) mid = s + n / 2;    // no useful split: halve by count
+    const int l = sah_rec(pb, pc, idx, s, mid, out);
+    const int r = sah_rec(pb, pc, idx, mid, e, out);
+    out[me].left = l;
+    out[me].right = r;
+    return me;
+}
+
+// Collapse the SAH BVH2 into 4-wide nodes: each node's slots are its children, the interior
+// slot with the largest surface area replaced by its own two children while slots are free.
+// Slot info: < 0 empty, 0 interior (ref = Node4 index), > 0 leaf of `info` triangles at ref
+// (absolute index into the SAH-ordered triangles).
+int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, std::vector<Node4>& out) {
+    const int me = (int)out.size();
+    out.emplace_back();
+    int slot[4] = {bn[n].left, bn[n].right, -1, -1};
+    int used = 2;
+    while (used < 4) {
+        int pick = -1;
+        double pa = -1.0;
+        for (int j = 0; j < used; j++)
+            if (bn[slot[j]].left >= 0) {
+                const double a = sah_area(bn[slot[j]].lo, bn[slot[j]].hi);
+                if (a > pa) { pa = a; pick = j; }
+            }
+        if (pick < 0) break;
+        const int c = slot[pick];
+        slot[pick] = bn[c].left;
+        slot[used++] = bn[c].right;
+    }
+    float lo[3][4], hi[3][4];
+    int ref[4], info[4];
+    for (int j = 0; j < 4; j++) {
+        if (j >= used) {
+            for (int z = 0; z < 3; z++) { lo[z][j] = 0.0f; hi[z][j] = 0.0f; }
+            ref[j] = 0; info[j] = -1;
+            continue;
+        }
+        const SahNode2& c = bn[slot[j]];
+        for (int z = 0; z < 3; z++) { lo[z][j] = c.lo[z]; hi[z][j] = c.hi[z]; }
+        if (c.left < 0) { ref[j] = tri_base + c.start; info[j] = c.count; }
+        else { ref[j] = 0; info[j] = 0; }
+    }
+    for (int j = 0; j < used; j++)
+        if (bn[slot[j]].left >= 0) ref[j] = sah_collapse(bn, slot[j], tri_base, out);
     Node4& nd = out[me];
     nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
     nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
@@ -592,7 +698,8 @@ struct rtg_scene {
     std::vector<int> orig_prim;              // absolute BVH position -> original prim index
     SceneView sv{};
     DBuf d_tops, d_geoms, d_nodes, d_nodes4, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
-        d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf, d_tlas, d_tlasidx;
+        d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf, d_tlas, d_tlasidx, d_stris, d_gates;
+    int blas_mode = 0;                       // rtg_build_opts.traversal_tree
     int tlas_mode = 0;                       // rtg_build_opts.tlas
     int tlas_root = -1;                      // top-level BVH root node (-1: linear object loop)
     int tlas_count = 0;                      // its nodes
@@ -698,7 +805,8 @@ static int validate(const rtg_scene_desc* d) {
 static std::vector<DBuf*> scene_buffers(rtg_scene* s) {
     return {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices,
             &s->d_vnormals, &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights,
-            &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_tlas, &s->d_tlasidx};
+            &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_tlas, &s->d_tlasidx, &s->d_stris,
+            &s->d_gates};
 }
 
 // Point the kernels' SceneView at this scene's device buffers.
@@ -707,7 +815,9 @@ static void bind_view(rtg_scene* s) {
     sv.tops = s->d_tops.as<TopObject>();
     sv.geoms = s->d_geoms.as<Geometry>();
     sv.nodes = s->d_nodes.as<Node>();
-    sv.nodes4 = s->d_nodes4.as<Node4>();
+    sv.snodes = s->d_nodes4.as<Node4>();
+    sv.stris = s->d_stris.as<TriGeom>();
+    sv.gates = s->d_gates.as<float>();
     sv.tris = s->d_tris.as<TriGeom>();
     sv.prim_idx = s->d_primidx.as<int4>();
     sv.vertices = s->d_vertices.as<float>();
@@ -799,7 +909,9 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     // BVHs and device geometry
     std::vector<Geometry> geoms(d->num_objects);
     std::vector<Node> dnodes;
-    std::vector<Node4> dnodes4;
+    std::vector<Node4> snodes;               // traversal trees (SAH, 4-wide)
+    std::vector<TriGeom> stris;              // their triangles, SAH leaf order (p2 = ref position / leaf / gated)
+    std::vector<float> gates;                // per reference position: its leaf's parent box
     std::vector<TriGeom> tris;
     std::vector<int4> primidx;
     s->orig_prim.clear();
@@ -923,11 +1035,6 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         g.prune_pad = pad;
         // linearise interior nodes (pre-order) into child-box nodes
         const std::vector<HNode>& hn = ob.nodes;
-        for (const HNode& h : hn) {            // leaf length travels with the leaf's first triangle
-            if (h.left >= 0 || h.right >= 0 || h.end <= h.start) continue;
-            int len = h.end - h.start;
-            memcpy(&tris[g.prim_base + h.start].p2.z, &len, 4);
-        }
         std::vector<int> dev_index(hn.size(), -1);
         int node_base = (int)dnodes.size();
         int cnt = 0;
@@ -961,9 +1068,62 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             nd.d = make_int4(ref[0], ref[1], count[0], count[1]);
             dnodes[dev_index[k]] = nd;
         }
-        g.node4_base = -1;
-        if (ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0))
-            g.node4_base = build_node4(hn, ob.root, g.prim_base, dnodes4);
+        // reference leaf of every position: its first position (tie order) and the box of the
+        // interior node above it, which gates it (none under the root: closest_hit tests the root)
+        gates.resize(6 * (size_t)(g.prim_base + np), 0.0f);
+        std::vector<int> leaf_start(np, 0);
+        std::vector<char> gated(np, 0);
+        if (ob.root >= 0 && hn[ob.root].left < 0 && hn[ob.root].right < 0)
+            for (int k = hn[ob.root].start; k < hn[ob.root].end; k++) leaf_start[k] = g.prim_base + hn[ob.root].start;
+        for (size_t n2 = 0; n2 < hn.size(); n2++) {
+            const int ch[2] = {hn[n2].left, hn[n2].right};
+            for (int c : ch) {
+                if (c < 0 || hn[c].left >= 0 || hn[c].right >= 0) continue;
+                for (int k = hn[c].start; k < hn[c].end; k++) {
+                    leaf_start[k] = g.prim_base + hn[c].start;
+                    gated[k] = (int)n2 != ob.root;
+                    for (int z = 0; z < 3; z++) {
+                        gates[6 * (size_t)(g.prim_base + k) + z] = hn[n2].mn[z];
+                        gates[6 * (size_t)(g.prim_base + k) + 3 + z] = hn[n2].mx[z];
+                    }
+                }
+            }
+        }
+        // traversal tree (SAH, 4-wide) of a triangle object with an interior reference root and
+        // finite primitives (its boxes must bound every candidate; NaN / inf objects keep the
+        // reference-tree walk)
+        g.sah_base = -1;
+        bool sah_ok = o.type != RTG_OBJ_SPHERE && np >= 2 && ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0);
+        for (int k = 0; k < np && sah_ok; k++)
+            sah_ok = std::isfinite(bmin[k].x) && std::isfinite(bmin[k].y) && std::isfinite(bmin[k].z) &&
+                     std::isfinite(bmax[k].x) && std::isfinite(bmax[k].y) && std::isfinite(bmax[k].z);
+        if (sah_ok && s->blas_mode != 1) {
+            std::vector<SahBox> pb(np);
+            std::vector<V3> pc(np);
+            std::vector<int> idx(np);
+            for (int k = 0; k < np; k++) {            // by reference position
+                const int f = ob.perm[k];
+                for (int z = 0; z < 3; z++) { pb[k].lo[z] = comp(bmin[f], z); pb[k].hi[z] = comp(bmax[f], z); }
+                pc[k] = v3(0.5f * (bmin[f].x + bmax[f].x), 0.5f * (bmin[f].y + bmax[f].y), 0.5f * (bmin[f].z + bmax[f].z));
+                idx[k] = k;
+            }
+            std::vector<SahNode2> bn;
+            bn.reserve(2 * (size_t)np / kSahMaxLeaf + 16);
+            sah_rec(pb, pc, idx, 0, np, bn);
+            if (bn[0].left >= 0) {
+                const int tri_base = (int)stris.size();
+                for (int k = 0; k < np; k++) {
+                    const int r = idx[k];
+                    TriGeom t = tris[g.prim_base + r];
+                    const int pos = g.prim_base + r, gt = gated[r];
+                    memcpy(&t.p2.y, &pos, 4);
+                    memcpy(&t.p2.z, &leaf_start[r], 4);
+                    memcpy(&t.p2.w, &gt, 4);
+                    stris.push_back(t);
+                }
+                g.sah_base = sah_collapse(bn, 0, tri_base, snodes);
+            }
+        }
         if (ob.root < 0) {
             g.node_base = -1; g.root_leaf_start = g.prim_base; g.root_leaf_count = -1;
         } else if (hn[ob.root].left < 0 && hn[ob.root].right < 0) {
@@ -1155,7 +1315,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     if (d->num_texcoords > 0) tcflat.assign(d->texcoords, d->texcoords + 2 * (size_t)d->num_texcoords);
     int rc;
     if ((rc = upload(s->d_tops, tops)) || (rc = upload(s->d_geoms, geoms)) || (rc = upload(s->d_nodes, dnodes)) ||
-        (rc = upload(s->d_nodes4, dnodes4)) ||
+        (rc = upload(s->d_nodes4, snodes)) || (rc = upload(s->d_stris, stris)) || (rc = upload(s->d_gates, gates)) ||
         (rc = upload(s->d_tris, tris)) || (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_vertices, vflat)) ||
         (rc = upload(s->d_vnormals, s->vnormals)) || (rc = upload(s->d_texcoords, tcflat)) ||
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
@@ -1213,6 +1373,7 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         if (opts && (opts->bvh_builder < RTG_BVH_AUTO || opts->bvh_builder > RTG_BVH_GPU))
             return fail(RTG_ERR_INVALID, "bvh_builder");
         if (opts && (opts->tlas < 0 || opts->tlas > 2)) return fail(RTG_ERR_INVALID, "tlas");
+        if (opts && (opts->traversal_tree < 0 || opts->traversal_tree > 1)) return fail(RTG_ERR_INVALID, "traversal_tree");
         *out = nullptr;
         int rc = validate(desc);
         if (rc) return rc;
@@ -1230,6 +1391,8 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
         s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
         s->tlas_mode = opts ? opts->tlas : 0;
+        s->blas_mode = opts ? opts->traversal_tree : 0;
+        if (const char* e = getenv("RTG_SAH")) s->blas_mode = atoi(e) == 0 ? 1 : 0;
         if (const char* e = getenv("RTG_TLAS")) s->tlas_mode = atoi(e) == 0 ? 1 : 2;
         rc = build_scene(s, desc);
         if (rc) {

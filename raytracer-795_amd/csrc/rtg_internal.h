@@ -39,7 +39,7 @@ struct TopObject {
 struct Geometry {
     int type;               // rtg_object_type
     int node_base;          // absolute index of the BVH root in the node array (-1 if root is a leaf)
-    int node4_base;         // same in the Node4 array
+    int sah_base;           // root of the traversal tree (SceneView::snodes), -1: reference-tree walk
     int root_leaf_start;    // absolute prim range when the root is a leaf (no box test)
     int root_leaf_count;    // -1: no primitives at all
     float root_min[3];      // root box (tested only when the root is interior)
@@ -69,14 +69,9 @@ struct Node {
     int4 d;
 };
 
-// 128-byte 4-wide node: the BVH2 node N with each interior child c replaced by c's two
-// children (slots 2q, 2q+1 come from N's child q).  Per-slot boxes in SoA form.
-// info: < 0 empty; 0 interior (ref = absolute Node4 index); > 0 leaf of `info & kSlotCount`
-// prims starting at ref (absolute).  kSlotGate marks a slot that came from a collapsed
-// interior child c: the reference reaches it only through c's box test, and c's box is the
-// union of the pair's two slot boxes (range boxes are unions of their children's).
-constexpr int kSlotGate = 0x40000000;
-constexpr int kSlotCount = 0x3fffffff;
+// 128-byte 4-wide node of a traversal tree (SAH over the triangle boxes, rtg_host.cpp
+// sah_collapse).  Per-slot boxes in SoA form.  info: < 0 empty; 0 interior (ref = absolute Node4
+// index); > 0 leaf of `info` triangles starting at ref (absolute index into SceneView::stris).
 struct Node4 {
     float4 lox, loy, loz, hix, hiy, hiz;
     int4 ref;
@@ -127,7 +122,10 @@ struct SceneView {
     const TopObject* tops; int num_tops; int num_objects;
     const Geometry* geoms;
     const Node* nodes;
-    const Node4* nodes4;
+    const Node4* snodes;           // traversal trees (SAH, 4-wide)
+    const TriGeom* stris;          // their triangles in leaf order; p2.y = reference position (int bits),
+                                   // p2.z = first position of its reference leaf, p2.w = 1 if gated
+    const float* gates;            // per reference position: min xyz, max xyz of its leaf's parent box
     const TriGeom* tris;
     const int4* prim_idx;          // BVH order: {v1,v2,v3 (1-based), smooth}; spheres {c,0,0,0}
     const float* vertices;         // xyz

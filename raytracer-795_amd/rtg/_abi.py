@@ -129,7 +129,7 @@ class Ray(C.Structure):
 
 
 class BuildOpts(C.Structure):
-    _fields_ = [("bvh_builder", C.c_int32), ("tlas", C.c_int32)]
+    _fields_ = [("bvh_builder", C.c_int32), ("tlas", C.c_int32), ("traversal_tree", C.c_int32)]
 
 
 class BuildStats(C.Structure):

@@ -24,12 +24,13 @@ DEFAULT_SEED = 0x5EED2026
 
 
 class Renderer:
-    def __init__(self, scene: Scene, device: int = 0, bvh_builder: int = A.RTG_BVH_AUTO, tlas: int = 0):
+    def __init__(self, scene: Scene, device: int = 0, bvh_builder: int = A.RTG_BVH_AUTO, tlas: int = 0,
+                 traversal_tree: int = 0):
         self.lib = A.load_library()
         self.scene = scene
         desc, self._keep = scene.to_desc()
         h = C.c_void_p()
-        bo = A.BuildOpts(bvh_builder, tlas)
+        bo = A.BuildOpts(bvh_builder, tlas, traversal_tree)
         A.check(self.lib.rtg_scene_create_ex(C.byref(desc), int(device), C.byref(bo), C.byref(h)), self.lib)
         self.handle = h
         self.device = device
