@@ -426,7 +426,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     }
                 };
                 // Fast rays walk the mesh's traversal tree (SAH, 4-wide; rtg_host.cpp): slots are
-                // pruned by the parameter window only (boxes padded by the eps overhang), leaves are
+                // pruned by the parameter window only (boxes widened by the eps overhang), leaves are
                 // tested nearer-first as they are reached, interior slots visited nearest-first.  A
                 // candidate that would become the object's winner must be reachable in the
                 // reference tree: its reference leaf's parent box (the only ancestor box that can
@@ -475,7 +475,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                             const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
                             const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
                             const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                            const float lo = le - e - padt, hi = sl + e + padt;
+                            const float lo = le - e, hi = sl + e;      // boxes carry the pad
                             key[j] = lo;
                             const bool ok = inf[j] >= 0 && !(hi < lo || hi < tlo || lo > thi);
                             okm |= ok << j;

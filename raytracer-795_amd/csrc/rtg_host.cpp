@@ -403,8 +403,11 @@ int sah_rec(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::vecto
 // Collapse the SAH BVH2 into 4-wide nodes: each node's slots are its children, the interior
 // slot with the largest surface area replaced by its own two children while slots are free.
 // Slot info: < 0 empty, 0 interior (ref = Node4 index), > 0 leaf of `info` triangles at ref
-// (absolute index into the SAH-ordered triangles).
-int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, std::vector<Node4>& out) {
+// (absolute index into the SAH-ordered triangles).  Slot boxes are widened by `pad` (the eps
+// overhang of a candidate beyond its triangle, rounded outwards), so the device walk needs no
+// parameter-space padding: a t-space pad of pad/|d_a| on every axis would stop pruning rays
+// with one small direction component.
+int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad, std::vector<Node4>& out) {
     const int me = (int)out.size();
     out.emplace_back();
     int slot[4] = {bn[n].left, bn[n].right, -1, -1};
@@ -431,12 +434,15 @@ int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, std::vect
             continue;
         }
         const SahNode2& c = bn[slot[j]];
-        for (int z = 0; z < 3; z++) { lo[z][j] = c.lo[z]; hi[z][j] = c.hi[z]; }
+        for (int z = 0; z < 3; z++) {
+            lo[z][j] = std::nextafter((float)((double)c.lo[z] - pad), -FLT_MAX);
+            hi[z][j] = std::nextafter((float)((double)c.hi[z] + pad), FLT_MAX);
+        }
         if (c.left < 0) { ref[j] = tri_base + c.start; info[j] = c.count; }
         else { ref[j] = 0; info[j] = 0; }
     }
     for (int j = 0; j < used; j++)
-        if (bn[slot[j]].left >= 0) ref[j] = sah_collapse(bn, slot[j], tri_base, out);
+        if (bn[slot[j]].left >= 0) ref[j] = sah_collapse(bn, slot[j], tri_base, pad, out);
     Node4& nd = out[me];
     nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
     nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
@@ -1121,7 +1127,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                     memcpy(&t.p2.w, &gt, 4);
                     stris.push_back(t);
                 }
-                g.sah_base = sah_collapse(bn, 0, tri_base, snodes);
+                g.sah_base = sah_collapse(bn, 0, tri_base, pad, snodes);
             }
         }
         if (ob.root < 0) {
