@@ -1305,15 +1305,14 @@ DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialD
 // TEX (full variant only): object texturing and BRDFs compiled in; a full scene without them
 // (area / environment lights, background texture) runs k_shade<true, *, 256, false>, which has
 // far fewer live registers.
-template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL>
-__global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
-                                               uint64_t seed,
-                                               const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
-                                               const HitRec* __restrict__ hits, const NodePlanes nodes,
-                                               const ShadowPlanes shadows, int* __restrict__ slist,
-                                               RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
-                                               unsigned long long* qcount, int n) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+// One ray's shading step (Scene::RecursiveShading for the node) plus the level's compaction of
+// child rays and shadow queries.  Called by every thread of the block (it synchronises); lanes
+// with i >= n only take part in the compaction.  h / o / d / time / mt: the traced ray and its hit.
+template <bool FULL, bool SPOT, int BLOCK, bool TEX>
+DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, int i,
+                   int n, const HitRec& h, const f3 o, const f3 d, const float time, const RayMeta& mt,
+                   const NodePlanes& nodes, const ShadowPlanes& shadows, int* __restrict__ slist,
+                   RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount) {
     int nchild = 0;
     RayRec c0r, c1r;
     RayMeta c0m, c1m;
@@ -1322,23 +1321,6 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     NodeRec nd;
     unsigned long long smask = 0;   // lights whose shadow query must be traced
     if (i < n) {
-        const HitRec h = load_hit_compact(hits, i);
-        f3 o, d;
-        float time;
-        RayMeta mt;
-        if (rays == nullptr) {          // level 0 without a ray buffer: generate the primary ray and its meta
-            primary_ray(cam, ps, seed, i, o, d, time);
-            mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
-        } else {
-            RayRec r = rays[i];
-            if (sv.meta_free && level > 0) {   // nothing below level 0 draws random numbers
-                mt.slot = 0; mt.path_lo = 0u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
-            } else {
-                mt = meta[i];
-            }
-            o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
-            time = r.o_t.w;
-        }
         uint32_t pixel, sample;
         int x, y;
         slot_pixel(cam, ps, mt.slot, pixel, sample, x, y);
@@ -1493,6 +1475,53 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
         if (need) slist[sb + __popcll(m & lt)] = i * sv.num_lights + li;
         sb += __popcll(m);
     }
+}
+
+// Level-0 ray of slot i (no ray buffer) or the queued ray i.
+DEV void level_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, const RayRec* __restrict__ rays, int i,
+                   f3& o, f3& d, float& time, float& tmax) {
+    if (rays == nullptr) {
+        primary_ray(cam, ps, seed, i, o, d, time);
+        tmax = FLT_MAX;
+    } else {
+        const RayRec r = rays[i];
+        o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
+        time = r.o_t.w; tmax = r.d.w;
+    }
+}
+DEV RayMeta level_meta(const SceneView& sv, int level, const RayRec* rays, const RayMeta* __restrict__ meta, int i) {
+    RayMeta mt;
+    if (rays == nullptr) {            // level 0: the primary ray's meta
+        mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
+    } else if (sv.meta_free && level > 0) {   // nothing below level 0 draws random numbers
+        mt.slot = 0; mt.path_lo = 0u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
+    } else {
+        mt = meta[i];
+    }
+    return mt;
+}
+
+template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL>
+__global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+                                               uint64_t seed,
+                                               const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
+                                               const HitRec* __restrict__ hits, const NodePlanes nodes,
+                                               const ShadowPlanes shadows, int* __restrict__ slist,
+                                               RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
+                                               unsigned long long* qcount, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    HitRec h;
+    h.obj = -1; h.prim = -1; h.t = 0.0f; h.pad = 0;
+    f3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+    float time = 0.0f, tmax;
+    RayMeta mt = {};
+    if (i < n) {
+        h = load_hit_compact(hits, i);
+        level_ray(cam, ps, seed, rays, i, o, d, time, tmax);
+        mt = level_meta(sv, level, rays, meta, i);
+    }
+    shade_ray<FULL, SPOT, BLOCK, TEX>(sv, cam, level, ps, seed, i, n, h, o, d, time, mt, nodes, shadows, slist,
+                                      next_rays, next_meta, qcount);
 }
 
 // ------------------------------------------------------------------ hw7 path tracer
