@@ -1169,7 +1169,7 @@ DEV f3 background(const SceneView& sv, const CameraDev& cam, int row, int col, f
 // ------------------------------------------------------------------ kernels
 // Primary ray of sample slot i of the pass (Camera::getPrimaryRay / getSampleRay).  Level 0's
 // k_trace / k_shade / k_pt_shade compute it from the slot (same function, so bit-identical)
-// instead of storing a 48-byte RayRec + RayMeta per primary ray and re-reading it twice.
+// instead of storing a queued ray + RayMeta per primary ray and re-reading it twice.
 DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int i, f3& o_out, f3& d_out,
                      float& time_out) {
     uint32_t pixel, sample;
@@ -1232,9 +1232,23 @@ DEV HitRec load_hit_compact(const HitRec* hits, int i) {
     return h;
 }
 
-// GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no RayRec buffer).
+// Queued ray i (RayQ planes).
+DEV void load_ray(const RayQ& q, int i, f3& o, f3& d, float& time) {
+    const float4 a = q.a[i];
+    const float2 b = q.b[i];
+    o = mk(a.x, a.y, a.z);
+    d = mk(a.w, b.x, b.y);
+    time = q.t ? q.t[i] : 0.0f;
+}
+DEV void store_ray(const RayQ& q, int k, f3 o, f3 d, float time) {
+    q.a[k] = make_float4(o.x, o.y, o.z, d.x);
+    q.b[k] = make_float2(d.y, d.z);
+    if (q.t) q.t[k] = time;
+}
+
+// GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no ray queue).
 template <bool EXHAUSTIVE, bool STATS, bool GEN = false, bool TLAS = false>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayRec* __restrict__ rays,
+__global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayQ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
                                                        const CameraDev cam, const PassDev ps, uint64_t seed,
                                                        bool compact) {
@@ -1249,9 +1263,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
             primary_ray(cam, ps, seed, i, o, d, time);
             tmax = FLT_MAX;
         } else {
-            const RayRec r = rays[i];
-            o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
-            time = r.o_t.w; tmax = r.d.w;
+            load_ray(rays, i, o, d, time);
+            tmax = FLT_MAX;
         }
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st,
                                                         s_tstack + (TLAS ? threadIdx.x : 0));
@@ -1276,10 +1289,10 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
     }
 }
 
-DEV RayRec make_ray(f3 o, f3 d, float time) {
-    RayRec r;
-    r.o_t = make_float4(o.x, o.y, o.z, time);
-    r.d = make_float4(d.x, d.y, d.z, FLT_MAX);
+struct QRay { f3 o, d; float time; };      // a child ray on its way to the next level's queue
+DEV QRay make_ray(f3 o, f3 d, float time) {
+    QRay r;
+    r.o = o; r.d = d; r.time = time;
     return r;
 }
 
@@ -1312,9 +1325,9 @@ template <bool FULL, bool SPOT, int BLOCK, bool TEX>
 DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, int i,
                    int n, const HitRec& h, const f3 o, const f3 d, const float time, const RayMeta& mt,
                    const NodePlanes& nodes, const ShadowPlanes& shadows, int* __restrict__ slist,
-                   RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount) {
+                   const RayQ& next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount) {
     int nchild = 0;
-    RayRec c0r, c1r;
+    QRay c0r, c1r;
     RayMeta c0m, c1m;
     bool has0 = false, has1 = false;
     bool hit = false;
@@ -1458,8 +1471,8 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
     __syncthreads();
     int idx = (int)((unsigned)s_base + s_wc[w] + coff);
     if (i < n) {
-        auto put_ray = [&](int k, const RayRec& rr, const RayMeta& mm) {
-            next_rays[k] = rr;
+        auto put_ray = [&](int k, const QRay& rr, const RayMeta& mm) {
+            store_ray(next_rays, k, rr.o, rr.d, rr.time);
             if (!sv.meta_free) next_meta[k] = mm;
         };
         if (has0) { put_ray(idx, c0r, c0m); nd.child0 = idx; idx++; }
@@ -1478,20 +1491,14 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
 }
 
 // Level-0 ray of slot i (no ray buffer) or the queued ray i.
-DEV void level_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, const RayRec* __restrict__ rays, int i,
-                   f3& o, f3& d, float& time, float& tmax) {
-    if (rays == nullptr) {
-        primary_ray(cam, ps, seed, i, o, d, time);
-        tmax = FLT_MAX;
-    } else {
-        const RayRec r = rays[i];
-        o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
-        time = r.o_t.w; tmax = r.d.w;
-    }
+DEV void level_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, const RayQ& rays, int i,
+                   f3& o, f3& d, float& time) {
+    if (rays.a == nullptr) primary_ray(cam, ps, seed, i, o, d, time);
+    else load_ray(rays, i, o, d, time);
 }
-DEV RayMeta level_meta(const SceneView& sv, int level, const RayRec* rays, const RayMeta* __restrict__ meta, int i) {
+DEV RayMeta level_meta(const SceneView& sv, int level, const RayQ& rays, const RayMeta* __restrict__ meta, int i) {
     RayMeta mt;
-    if (rays == nullptr) {            // level 0: the primary ray's meta
+    if (rays.a == nullptr) {          // level 0: the primary ray's meta
         mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
     } else if (sv.meta_free && level > 0) {   // nothing below level 0 draws random numbers
         mt.slot = 0; mt.path_lo = 0u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
@@ -1504,20 +1511,20 @@ DEV RayMeta level_meta(const SceneView& sv, int level, const RayRec* rays, const
 template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL>
 __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                uint64_t seed,
-                                               const RayRec* __restrict__ rays, const RayMeta* __restrict__ meta,
+                                               const RayQ rays, const RayMeta* __restrict__ meta,
                                                const HitRec* __restrict__ hits, const NodePlanes nodes,
                                                const ShadowPlanes shadows, int* __restrict__ slist,
-                                               RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
+                                               const RayQ next_rays, RayMeta* __restrict__ next_meta,
                                                unsigned long long* qcount, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     HitRec h;
     h.obj = -1; h.prim = -1; h.t = 0.0f; h.pad = 0;
     f3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-    float time = 0.0f, tmax;
+    float time = 0.0f;
     RayMeta mt = {};
     if (i < n) {
         h = load_hit_compact(hits, i);
-        level_ray(cam, ps, seed, rays, i, o, d, time, tmax);
+        level_ray(cam, ps, seed, rays, i, o, d, time);
         mt = level_meta(sv, level, rays, meta, i);
     }
     shade_ray<FULL, SPOT, BLOCK, TEX>(sv, cam, level, ps, seed, i, n, h, o, d, time, mt, nodes, shadows, slist,
@@ -1562,16 +1569,16 @@ constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour 
 
 template <bool FULL, bool SPOT, bool BRDF>
 __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
-                                                  uint64_t seed, const RayRec* __restrict__ rays,
+                                                  uint64_t seed, const RayQ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
                                                   PathRec* __restrict__ paths, const NodePlanes nodes,
                                                   const ShadowPlanes shadows, int* __restrict__ slist,
-                                                  RayRec* __restrict__ next_rays, RayMeta* __restrict__ next_meta,
+                                                  const RayQ next_rays, RayMeta* __restrict__ next_meta,
                                                   PathRec* __restrict__ next_paths, unsigned long long* qcount, int n) {
     constexpr int BLOCK = 256;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool has = false;
-    RayRec cr;
+    QRay cr;
     RayMeta cm;
     PathRec cp;
     NodeRec nd;
@@ -1580,14 +1587,12 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
         f3 o, d;
         float time;
         RayMeta mt;
-        if (rays == nullptr) {          // level 0 without a ray buffer: generate the primary ray and its meta
+        if (rays.a == nullptr) {        // level 0 without a ray queue: generate the primary ray and its meta
             primary_ray(cam, ps, seed, i, o, d, time);
             mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
         } else {
-            const RayRec r = rays[i];
+            load_ray(rays, i, o, d, time);
             mt = meta[i];
-            o = mk(r.o_t.x, r.o_t.y, r.o_t.z); d = mk(r.d.x, r.d.y, r.d.z);
-            time = r.o_t.w;
         }
         const HitRec h = load_hit_compact(hits, i);
         uint32_t pixel, sample;
@@ -1729,7 +1734,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
     __syncthreads();
     const int idx = (int)((unsigned)s_base + s_wc[wv] + coff);
     if (i < n) {
-        if (has) { next_rays[idx] = cr; next_meta[idx] = cm; next_paths[idx] = cp; nd.child1 = idx; }
+        if (has) { store_ray(next_rays, idx, cr.o, cr.d, cr.time); next_meta[idx] = cm; next_paths[idx] = cp; nd.child1 = idx; }
         nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
         nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
         nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, nd.slot);
@@ -2044,12 +2049,14 @@ __global__ void __launch_bounds__(256) k_place_rows(const float* __restrict__ re
     for (int q = c; q < c + 4 && q < 3 * nx; q++) dst[q] = src[q];
 }
 
-__global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const RayRec* __restrict__ rays,
+__global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const RayQ rays,
                                                      const HitRec* __restrict__ hits, rtg_hit* __restrict__ out,
                                                      const int* __restrict__ orig_prim, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    RayRec r = rays[i];
+    f3 ro, rd;
+    float rt;
+    load_ray(rays, i, ro, rd, rt);
     HitRec h = hits[i];
     rtg_hit o;
     o.full = h.obj >= 0;
@@ -2058,7 +2065,7 @@ __global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const R
     o.point[0] = o.point[1] = o.point[2] = 0.0f;
     o.normal[0] = o.normal[1] = o.normal[2] = 0.0f;
     if (h.obj >= 0) {
-        Ret ret = hit_record(sv, mk(r.o_t.x, r.o_t.y, r.o_t.z), mk(r.d.x, r.d.y, r.d.z), r.o_t.w, h);
+        Ret ret = hit_record(sv, ro, rd, rt, h);
         o.prim = orig_prim[h.prim];
         o.material = ret.matIndex;
         o.t = h.t;
@@ -2071,7 +2078,7 @@ __global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const R
 // ------------------------------------------------------------------ launchers
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 
-void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
+void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
                   hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed, bool compact) {
     if (n <= 0) return;
     dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
@@ -2095,8 +2102,8 @@ void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, 
 #undef RTG_TRACE
 }
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
-                  const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
-                  ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta,
+                  const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
+                  ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
                   unsigned long long* qcount, int n, hipStream_t st) {
     if (n <= 0) return;
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
@@ -2133,8 +2140,8 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, sp, np, n);
 }
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
-                     const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
-                     ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta, PathRec* next_paths,
+                     const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
+                     ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st) {
     if (n <= 0) return;
     dim3 g(nblk(n, 256)), b(256);
@@ -2184,7 +2191,7 @@ void launch_place_rows(const float* recv, float* frame, int nx, int ny, int nran
     hipLaunchKernelGGL(k_place_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, recv, frame, nx, ny, nranks,
                        block, pre);
 }
-void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, rtg_hit* out,
+void launch_hit_details(const SceneView& sv, const RayQ rays, const HitRec* hits, rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_hit_details, dim3(nblk(n, 256)), dim3(256), 0, st, sv, rays, hits, out, orig_prim, n);

@@ -652,6 +652,7 @@ int upload(DBuf& b, const std::vector<T>& v) {
 
 struct Level {
     DBuf rays, meta, hits, nodes, shadows, slist, paths;
+    long long rcap = 0;        // plane stride of `rays` (RayQ) as the previous level wrote them
     void release() {
         rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release();
         paths.release();
@@ -1363,6 +1364,11 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     int any_rough = 0;
     for (int i = 0; i < d->num_materials; i++) any_rough |= d->materials[i].is_rough != 0;
     sv.meta_free = !sv.full && !any_rough;
+    sv.has_blur = 0;
+    for (int i = 0; i < d->num_objects; i++)
+        for (int k = 0; k < 3; k++) sv.has_blur |= !(d->objects[i].blur[k] == 0.0f);
+    for (int i = 0; i < d->num_instances; i++)
+        for (int k = 0; k < 3; k++) sv.has_blur |= !(d->instances[i].blur[k] == 0.0f);
     sv.lean_shadow = d->num_lights == 1 &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);
@@ -1569,25 +1575,28 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             return rc2;
         const bool may_spawn = level + 1 < max_levels;
         const size_t cap = may_spawn ? 2 * (size_t)n : 1;
-        if ((rc2 = Ln.rays.grow(sizeof(RayRec) * cap)) || (rc2 = Ln.meta.grow(sizeof(RayMeta) * cap))) return rc2;
+        if ((rc2 = Ln.rays.grow(kRayBytes * cap)) || (rc2 = Ln.meta.grow(sizeof(RayMeta) * cap))) return rc2;
+        Ln.rcap = (long long)cap;
+        const RayQ cur_q = level == 0 ? RayQ{} : ray_planes(Lc.rays.p, Lc.rcap, sv.has_blur);
+        const RayQ next_q = ray_planes(Ln.rays.p, Ln.rcap, sv.has_blur);
         if (pt && ((rc2 = Lc.paths.grow(sizeof(PathRec) * (size_t)n)) || (rc2 = Ln.paths.grow(sizeof(PathRec) * cap))))
             return rc2;
         unsigned long long* qc = ln.qcnt.as<unsigned long long>() + level;
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
         // level 0: k_trace / k_shade / k_pt_shade regenerate the primary rays (no level-0 ray buffer)
         const bool gen = level == 0;
-        launch_trace(sv, gen ? nullptr : Lc.rays.as<RayRec>(), Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st,
+        launch_trace(sv, cur_q, Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st,
                      gen ? &cd : nullptr, gen ? &ps : nullptr, o.seed, /*compact=*/true);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
         if (pt)
-            launch_pt_shade(sv, cd, level, ps, o.seed, gen ? nullptr : Lc.rays.as<RayRec>(),
+            launch_pt_shade(sv, cd, level, ps, o.seed, cur_q,
                             gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                             Lc.paths.as<PathRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
-                            Ln.rays.as<RayRec>(), Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st);
+                            next_q, Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st);
         else
-            launch_shade(sv, cd, level, ps, o.seed, gen ? nullptr : Lc.rays.as<RayRec>(),
+            launch_shade(sv, cd, level, ps, o.seed, cur_q,
                          gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
-                         Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), Ln.rays.as<RayRec>(),
+                         Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), next_q,
                          Ln.meta.as<RayMeta>(), qc, n, ln.st);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
         // the next level's size is known once shade is done: read it back now, so the host can
@@ -1905,10 +1914,15 @@ int32_t rtg_trace_closest(rtg_scene* s, const rtg_ray* rays, int32_t n, rtg_hit*
         if (n == 0) return RTG_OK;
         if (s->device < 0) return fail(RTG_ERR_NO_DEVICE, "host-only scene cannot trace");
         HIP_TRY(hipSetDevice(s->device));
-        std::vector<RayRec> rr(n);
+        // the rays as RayQ planes (with times: API rays may carry any time)
+        std::vector<float> rr((size_t)7 * n);
         for (int i = 0; i < n; i++) {
-            rr[i].o_t = make_float4(rays[i].origin[0], rays[i].origin[1], rays[i].origin[2], rays[i].time);
-            rr[i].d = make_float4(rays[i].direction[0], rays[i].direction[1], rays[i].direction[2], FLT_MAX);
+            const rtg_ray& r = rays[i];
+            float* a = &rr[(size_t)4 * i];
+            float* b = &rr[(size_t)4 * n + 2 * (size_t)i];
+            a[0] = r.origin[0]; a[1] = r.origin[1]; a[2] = r.origin[2]; a[3] = r.direction[0];
+            b[0] = r.direction[1]; b[1] = r.direction[2];
+            rr[(size_t)6 * n + i] = r.time;
         }
         DBuf dr, dh, dout;
         int rc;
@@ -1916,8 +1930,9 @@ int32_t rtg_trace_closest(rtg_scene* s, const rtg_ray* rays, int32_t n, rtg_hit*
             dr.release(); dh.release(); dout.release();
             return rc;
         }
-        launch_trace(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), n, traversal == 1, nullptr, nullptr);
-        launch_hit_details(s->sv, dr.as<RayRec>(), dh.as<HitRec>(), dout.as<rtg_hit>(), s->d_origprim.as<int>(), n, nullptr);
+        const RayQ q = ray_planes(dr.p, n, true);
+        launch_trace(s->sv, q, dh.as<HitRec>(), n, traversal == 1, nullptr, nullptr);
+        launch_hit_details(s->sv, q, dh.as<HitRec>(), dout.as<rtg_hit>(), s->d_origprim.as<int>(), n, nullptr);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipMemcpy(hits, dout.p, sizeof(rtg_hit) * (size_t)n, hipMemcpyDeviceToHost);
         dr.release(); dh.release(); dout.release();

@@ -149,6 +149,8 @@ struct SceneView {
                                    // depth is max_depth - level, slot and path are unused)
     int lean_shadow;               // one point / spot / directional light: a Whitted shadow query
                                    // stores only origin + contribution (k_shadow rebuilds d, tmax, L)
+    int has_blur;                  // some object / instance has a nonzero motion-blur vector: the
+                                   // ray queues carry times (RayQ::t)
     // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
     // lights into num_lights)
     const int* top_emit;           // per top-level entry: emitter light index, -1 if not a light
@@ -164,7 +166,7 @@ struct SceneView {
     float tlas_k[3];               // gett() error scale of the axis-aligned entries (closest_hit)
 };
 
-// Path state of one path-tracing ray (per level, next to RayRec / RayMeta).
+// Path state of one path-tracing ray (per level, next to the RayQ planes / RayMeta).
 struct PathRec {       // 16 B
     float tr, tg, tb;  // throughput (after the Beer attenuation of the segment, once shaded)
     int flags;         // bit 0: previous bounce specular; bits 8..: medium material (1-based, 0 none)
@@ -202,10 +204,22 @@ struct CameraDev {
 };
 
 // Wavefront queue records -------------------------------------------------------
-struct RayRec {         // 32 B: the Ray of src/Ray.h
-    float4 o_t;         // origin.xyz, time
-    float4 d;           // direction.xyz, tmax bound (world t) for shadow queries
+// Queued rays (the Ray of src/Ray.h) as planes: a = (o.xyz, d.x), b = (d.y, d.z), t = time.  24 B
+// per ray, 28 with times: the time plane is left out (t = nullptr, every time reads 0) when no
+// object or instance has a motion-blur vector -- then the time cannot change any result, since
+// transform_ray multiplies it by a zero blur and render-path times are finite.  Every queued ray
+// is a closest-hit query without a distance bound (tmax = FLT_MAX).
+struct RayQ {
+    float4* a;
+    float2* b;
+    float* t;
 };
+constexpr size_t kRayBytes = 28;    // allocation per queued ray (the three planes)
+inline RayQ ray_planes(void* base, long long cap, bool times) {
+    char* p = static_cast<char*>(base);
+    return RayQ{reinterpret_cast<float4*>(p), reinterpret_cast<float2*>(p + 16 * cap),
+                times ? reinterpret_cast<float*>(p + 24 * cap) : nullptr};
+}
 struct RayMeta {        // 16 B
     int slot;           // sample slot in the batch
     unsigned path_lo, path_hi;
@@ -283,17 +297,17 @@ struct Counters {
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
 struct LevelBuffers;
 // gen_cam / gen_ps non-null: level 0 (either integrator), rays are generated in the kernel
-void launch_trace(const SceneView& sv, const RayRec* rays, HitRec* hits, int n, int exhaustive,
+void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
                   uint64_t seed = 0, bool compact = false);
-void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayRec* rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
-                  ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta,
+void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
+                  ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
                   unsigned long long* qcount, int n, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
                    int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted = true);
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
-                     const RayRec* rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
-                     ShadowRec* shadows, int* slist, RayRec* next_rays, RayMeta* next_meta, PathRec* next_paths,
+                     const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
+                     ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st);
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
                       int n0, int level, int n, hipStream_t st);
@@ -304,7 +318,7 @@ void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec
                        const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1);
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block, int total,
                      hipStream_t st);
-void launch_hit_details(const SceneView& sv, const RayRec* rays, const HitRec* hits, struct ::rtg_hit* out,
+void launch_hit_details(const SceneView& sv, const RayQ rays, const HitRec* hits, struct ::rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st);
 
 // Multi-GPU rows gather: shard r's compact rows start at row prefix[r] of `recv`; every frame
