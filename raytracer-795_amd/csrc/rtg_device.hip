@@ -1431,9 +1431,17 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                         // every record when there are several)
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
                             const size_t k = (size_t)i * sv.num_lights + li;
-                            shadows.o[k] = sr.o;
-                            shadows.c[k] = sr.c;
-                            if (!sv.lean_shadow) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
+                            if (sv.lean_shadow && !sv.has_blur) {
+                                // 12-byte planes: the origin, and the node colour if the light is
+                                // not blocked (ambient + contribution, the sum k_shadow would form)
+                                reinterpret_cast<float3*>(shadows.o)[k] = make_float3(sr.o.x, sr.o.y, sr.o.z);
+                                reinterpret_cast<float3*>(shadows.c)[k] =
+                                    make_float3(nd.cr + sr.c.x, nd.cg + sr.c.y, nd.cb + sr.c.z);
+                            } else {
+                                shadows.o[k] = sr.o;
+                                shadows.c[k] = sr.c;
+                                if (!sv.lean_shadow) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
+                            }
                         }
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
@@ -1799,7 +1807,16 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     if (j < (int)*scount) {
         const int idx = slist[j];
         const int i = idx / sv.num_lights;      // shading node of the query
-        const float4 so = shadows.o[idx];
+        // lean3: one point / spot / directional light and no motion blur -- 12-byte origin and
+        // lit-colour planes (k_shade), time 0, the mode follows from the light type
+        const bool lean3 = lean && !sv.has_blur;
+        float4 so;
+        if (lean3) {
+            const float3 q = reinterpret_cast<const float3*>(shadows.o)[idx];
+            so = make_float4(q.x, q.y, q.z, 0.0f);
+        } else {
+            so = shadows.o[idx];
+        }
         const f3 o = mk(so.x, so.y, so.z);
         f3 d;
         float tmax;
@@ -1822,19 +1839,24 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x,
                                                         kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0));
-        // the query's contribution / mode are re-read rather than kept live across the traversal
+        auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
+        // the query's mode is re-read rather than kept live across the traversal
         // (register pressure: 128 VGPRs for 4 waves per SIMD)
-        const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
-        const float4 sc = make_float4(__builtin_nontemporal_load(scp), __builtin_nontemporal_load(scp + 1),
-                                      __builtin_nontemporal_load(scp + 2), __builtin_nontemporal_load(scp + 3));
+        const float mode = lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f)
+                                 : ld(reinterpret_cast<const float*>(shadows.c + idx) + 3);
         bool blocked;
-        if (sc.w == 1.0f || sc.w == 3.0f) {
+        if (mode == 1.0f || mode == 3.0f) {
             blocked = false;
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
-                auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
-                const float* qo = reinterpret_cast<const float*>(shadows.o + idx);
-                const f3 o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
+                f3 o_;
+                if (lean3) {
+                    const float* qo = reinterpret_cast<const float*>(shadows.o) + 3 * (size_t)idx;
+                    o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
+                } else {
+                    const float* qo = reinterpret_cast<const float*>(shadows.o + idx);
+                    o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
+                }
                 const float* pp = reinterpret_cast<const float*>(nodes.pnt + i);
                 const f3 p_ = mk(ld(pp), ld(pp + 1), ld(pp + 2));
                 f3 d_, l_;
@@ -1848,7 +1870,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                     l_ = mk(ld(ql), ld(ql + 1), ld(ql + 2));
                 }
                 f3 hp = o_ + d_ * h.t;
-                if (sc.w == 1.0f) {             // PointLight::IsShadow: |p - L| > |p - hit|
+                if (mode == 1.0f) {             // PointLight::IsShadow: |p - L| > |p - hit|
                     blocked = norm(p_ - l_) > norm(p_ - hp);
                 } else {   // object light (hw7, Page7.md:143-147): an occluder nearer than the sample
                     const float dl = norm(p_ - l_);
@@ -1858,8 +1880,16 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         } else {
             blocked = h.obj >= 0;               // directional / environment: any hit
         }
-        if (sv.num_lights == 1) {
-            f3 add = blocked ? mk(0, 0, 0) : mk(sc.x, sc.y, sc.z);
+        if (lean3) {
+            // lit: the colour k_shade prepared (xyz only; w keeps the node's kind bits);
+            // blocked: col + 0 == col (the ambient term is never -0), nothing to store
+            if (!blocked) {
+                const float* cq = reinterpret_cast<const float*>(shadows.c) + 3 * (size_t)idx;
+                *reinterpret_cast<float3*>(nodes.col + i) = make_float3(ld(cq), ld(cq + 1), ld(cq + 2));
+            }
+        } else if (sv.num_lights == 1) {
+            const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
+            f3 add = blocked ? mk(0, 0, 0) : mk(ld(scp), ld(scp + 1), ld(scp + 2));
             float* cp = reinterpret_cast<float*>(nodes.col + i);
             cp[0] = cp[0] + add.x;
             cp[1] = cp[1] + add.y;
