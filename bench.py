@@ -147,6 +147,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=540)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tlas", choices=["auto", "off", "on"], default="auto",
+                    help="top-level BVH over objects / instances (rtg_build_opts.tlas; auto: from 16 entries)")
     args = ap.parse_args()
 
     import torch
@@ -176,7 +178,7 @@ def main():
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r = rtg.Renderer(scene, device=local)
+    r = rtg.Renderer(scene, device=local, tlas={"auto": 0, "off": 1, "on": 2}[args.tlas])
     create_ms = (time.perf_counter() - t0) * 1e3
     log(f"[rank {rank}] rtg_scene_create (BVH build + upload) {create_ms:.0f} ms")
     cam = scene.cameras[0]
@@ -328,7 +330,7 @@ def main():
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                 "data": data_text,
                 "config": {"workload": wl_text, "resolution": f"{cam.nx}x{cam.ny}", "spp": cam.num_samples,
-                           "parallelism": par},
+                           "parallelism": par, "tlas": args.tlas, "tlas_nodes": r.build_stats()["tlas_nodes"]},
                 "rays_per_frame": rays_frame,
                 "primary_msamples_s": round(cam.nx * cam.ny * cam.num_samples / (ms_per_step * 1e-3) / 1e6, 1),
                 "ms_per_frame_to_host": round(elapsed_h * 1e3 / args.steps, 2),
