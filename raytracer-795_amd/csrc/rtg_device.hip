@@ -570,9 +570,6 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         if (sl + e < -slack0) return false;
         return !beyond(key);
     };
-    auto tleaf = [&](int ref, int cnt) {
-        for (int k = ref; k < ref + cnt; k++) visit(sv.tlas_idx[k]);
-    };
     int tsp = 0;
     int cur = sv.tlas_root;
     while (true) {
@@ -584,13 +581,22 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         bool rok = rcnt >= 0 && tchild(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rpr, rk);
         const bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
         auto still = [&](float k, bool prune) { return !prune || !beyond(k); };
-        if (lleaf && rleaf && rk < lk) {
-            tleaf(rref, rcnt);
-            if (still(lk, lpr)) tleaf(lref, lcnt);
-            lok = rok = false;
-        } else {
-            if (lleaf) { tleaf(lref, lcnt); lok = false; }
-            if (rleaf) { if (still(rk, rpr)) tleaf(rref, rcnt); rok = false; }
+        // leaf children: the nearer first; the second only if the first did not push the winner
+        // in front of it.  One visit() call site (it inlines the whole per-object body).
+        {
+            const bool rfirst = lleaf && rleaf && rk < lk;
+            int q = 0;
+            if (lleaf || rleaf) {
+                while (true) {
+                    const bool take_r = (q == 0) == (rfirst || !lleaf);
+                    const int ref = take_r ? rref : lref, cnt = take_r ? rcnt : lcnt;
+                    for (int k = ref; k < ref + cnt; k++) visit(sv.tlas_idx[k]);
+                    if (++q == 2 || !(lleaf && rleaf)) break;
+                    if (!(take_r ? still(lk, lpr) : still(rk, rpr))) break;
+                }
+            }
+            if (lleaf) lok = false;
+            if (rleaf) rok = false;
         }
         lok = lok && still(lk, lpr);
         rok = rok && still(rk, rpr);
