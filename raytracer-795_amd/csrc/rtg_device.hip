@@ -539,7 +539,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
-    if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {
+    if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {   // wfast is per lane: the others walk on
         for (int i = 0; i < sv.num_tops; i++) visit(i);
         return out;
     }
@@ -570,6 +570,13 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         if (sl + e < -slack0) return false;
         return !beyond(key);
     };
+    // The walk is wave-uniform: the lanes of a wave (a pixel's samples, or a compacted run of
+    // their children) share one traversal.  A child is entered when any lane needs it, node and
+    // entry indices are uniform (scalar loads, one per-object code path per entry), and each lane
+    // visits only the entries of leaves its own ray line passes.  That is a superset of what the
+    // lane's own near-first walk would visit (pruning depends only on its own `nearest`), and
+    // visiting an extra entry is harmless: every entry is a valid visit of the linear loop, and
+    // equal t goes to the lower index in any order.
     int tsp = 0;
     int cur = sv.tlas_root;
     while (true) {
@@ -579,41 +586,41 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         float lk = 0.0f, rk = 0.0f;
         bool lok = lcnt >= 0 && tchild(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lpr, lk);
         bool rok = rcnt >= 0 && tchild(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rpr, rk);
-        const bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
         auto still = [&](float k, bool prune) { return !prune || !beyond(k); };
-        // leaf children: the nearer first; the second only if the first did not push the winner
-        // in front of it.  One visit() call site (it inlines the whole per-object body).
-        {
-            const bool rfirst = lleaf && rleaf && rk < lk;
-            int q = 0;
-            if (lleaf || rleaf) {
-                while (true) {
-                    const bool take_r = (q == 0) == (rfirst || !lleaf);
-                    const int ref = take_r ? rref : lref, cnt = take_r ? rcnt : lcnt;
-                    for (int k = ref; k < ref + cnt; k++) visit(sv.tlas_idx[k]);
-                    if (++q == 2 || !(lleaf && rleaf)) break;
-                    if (!(take_r ? still(lk, lpr) : still(rk, rpr))) break;
+        const bool lleaf = lcnt > 0, rleaf = rcnt > 0;
+        if (lleaf || rleaf) {
+            // leaf children, the nearer (for the wave's first lane) first; a lane takes the second
+            // only if the first did not push its winner in front of it.  One visit() call site.
+            const bool rfirst = rleaf && (!lleaf || __builtin_amdgcn_readfirstlane((int)(rk < lk)) != 0);
+            for (int q = 0; q < 2; q++) {
+                const bool take_r = (q == 0) == rfirst;
+                if (take_r ? !rleaf : !lleaf) continue;
+                const bool need = take_r ? (rok && still(rk, rpr)) : (lok && still(lk, lpr));
+                if (__ballot(need) == 0ull) continue;
+                const int ref = take_r ? rref : lref, cnt = take_r ? rcnt : lcnt;
+                for (int k = ref; k < ref + cnt; k++) {
+                    const int e = sv.tlas_idx[k];
+                    if (need) visit(e);
                 }
             }
             if (lleaf) lok = false;
             if (rleaf) rok = false;
         }
-        lok = lok && still(lk, lpr);
-        rok = rok && still(rk, rpr);
-        if (lok && rok) {
-            int nearc = lref, farc = rref;
-            if (rk < lk) { nearc = rref; farc = lref; }
-            tstack[tsp * sstride] = (short)farc;
+        const bool anyl = __ballot(lok && still(lk, lpr)) != 0ull;
+        const bool anyr = __ballot(rok && still(rk, rpr)) != 0ull;
+        if (anyl && anyr) {
+            const bool rnear = __builtin_amdgcn_readfirstlane((int)(rk < lk)) != 0;
+            tstack[tsp * sstride] = (short)(rnear ? lref : rref);
             tsp++;
-            cur = nearc;
-        } else if (lok) {
+            cur = rnear ? rref : lref;
+        } else if (anyl) {
             cur = lref;
-        } else if (rok) {
+        } else if (anyr) {
             cur = rref;
         } else {
             if (tsp == 0) break;
             tsp--;
-            cur = tstack[tsp * sstride];
+            cur = __builtin_amdgcn_readfirstlane((int)tstack[tsp * sstride]);
         }
     }
     return out;
