@@ -279,7 +279,7 @@ def main():
         kern = {}
         if same_wl:
             for key, name, avg, n in (("k_trace", "rtg::k_trace<false, false, *>", trace_avg, st_roof["trace_launches"]),
-                                      ("k_shadow", "rtg::k_shadow<false, false>", shadow_avg, st_roof["shadow_launches"]),
+                                      ("k_shadow", "rtg::k_shadow<false, false, false>", shadow_avg, st_roof["shadow_launches"]),
                                       ("k_shade", shade_names[0] if shade_names else "", shade_avg, st_roof["shade_launches"])):
                 kr = kernel_roof(counters, name, avg, n)
                 if kr:
