@@ -216,7 +216,9 @@ def test_full_frame_shards_sum_exactly(gpu):
 # One point / spot / directional light takes the lean shadow-record path (k_shadow rebuilds the
 # direction and t bound, SceneView::lean_shadow); a rough mirror keeps the child RayMeta
 # records (SceneView::meta_free off); two lights take the full four-plane records.
-@pytest.mark.parametrize("kind", ["point", "spot", "directional", "two_lights", "rough_mirror"])
+# "point_blur": one point light with a motion-blurred sphere -- the lean records keep their
+# time lanes (SceneView::has_blur), as do the queued rays (RayQ time plane).
+@pytest.mark.parametrize("kind", ["point", "spot", "directional", "two_lights", "rough_mirror", "point_blur"])
 def test_shadow_record_paths_match_oracle(gpu, kind):
     from rtg import _abi as A
     from rtg.scene import Light
@@ -231,6 +233,9 @@ def test_shadow_record_paths_match_oracle(gpu, kind):
         sc.lights.append(Light(type=A.LIGHT_DIRECTIONAL, direction=(0.5, -1.0, 0.2), intensity=(2, 2, 2)))
     elif kind == "rough_mirror":
         sc.materials[1].is_rough, sc.materials[1].roughness = True, 0.15
+    elif kind == "point_blur":
+        sph = next(ob for ob in sc.objects if ob.type == A.OBJ_SPHERE)
+        sph.blur = (0.0, 0.3, 0.2)
     with rtg.Renderer(sc, device=gpu) as r:
         img = r.render(0)
         st = r.stats()
@@ -240,4 +245,5 @@ def test_shadow_record_paths_match_oracle(gpu, kind):
     print(f"{kind}: Linf={linf:.3g} differing={frac:.2e} shadow={st['shadow_rays']}/{o.ray_counts()['shadow']}")
     assert nanm == 0
     assert linf < TOL
+    assert np.array_equal(np.nan_to_num(img).view(np.int32), np.nan_to_num(ref).view(np.int32)), kind
     assert 0 < st["shadow_rays"] <= o.ray_counts()["shadow"]
