@@ -453,6 +453,26 @@ def multilight(nx=320, ny=240, spp=1) -> Scene:
     return sc
 
 
+def glass_nest(nx=64, ny=48, spp=1, max_depth=6) -> Scene:
+    """Camera inside two concentric dielectric spheres inside a mirror sphere, with a point light in
+    the gap: every ray hits something and every dielectric hit spawns two children, so the ray
+    count roughly doubles per level (the device-driven level loop's overflow case)."""
+    sc = Scene(max_depth=max_depth, background=(20, 20, 30), ambient=(10, 10, 10))
+    sc.cameras.append(_cam((0, 0, 0), (0, 0, -1), (0, 1, 0), nx, ny, fov_deg=60, spp=spp, name="glass_nest.png"))
+    sc.materials += [
+        Material(type=A.MAT_DIELECTRIC, ambient=(0, 0, 0), diffuse=(0, 0, 0), specular=(0, 0, 0),
+                 refraction_index=1.5, absorption_coeff=(0.01, 0.02, 0.03)),
+        Material(type=A.MAT_MIRROR, ambient=(0.2, 0.2, 0.2), diffuse=(0.3, 0.3, 0.3), specular=(0.2, 0.2, 0.2),
+                 mirror=(0.6, 0.6, 0.6), phong_exp=20),
+    ]
+    c = _add_vertices(sc, [(0, 0, 0)])
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=1, material=1, center=c, radius=2.0))
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=2, material=1, center=c, radius=4.0))
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=3, material=2, center=c, radius=8.0))
+    sc.lights.append(Light(type=A.LIGHT_POINT, position=(1.0, 5.5, 1.0), intensity=(400, 400, 400)))
+    return sc
+
+
 def sky_texture(w=64, h=32, sun=(0.3, 0.28), sun_radiance=40.0) -> np.ndarray:
     """Linear HDR latitude-longitude sky (what an .exr environment map decodes to): a
     horizon-to-zenith gradient, a dark ground half and a small bright sun disc.  Values are

@@ -29,6 +29,7 @@ SCENES = {
     "envmap": lambda: scenegen.envmap(48, 36, spp=2),
     "bgtex": lambda: scenegen.bgtex(48, 32, spp=1),
     "bgtex_ms": lambda: scenegen.bgtex(48, 32, spp=3, interp=1),
+    "glass_nest": lambda: scenegen.glass_nest(32, 24, spp=2, max_depth=6),   # rays double per level
 }
 
 
