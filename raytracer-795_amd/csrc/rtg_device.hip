@@ -1138,27 +1138,31 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
 }
 
 // ------------------------------------------------------------------ camera / background
-// Tiled order of the owned pixels: bands of 8 owned rows, each band in blocks of 8 columns
-// (edge bands/blocks narrower), row-major inside a block.  t -> (x, k = owned-row index).
-// Pixel order of a pass: tiles of (64 / th) x th pixels over the owned rows, row-major inside a
-// tile; th = the shard's row block (<= 8), so a tile is always image-contiguous.
-DEV void tile_pixel(int t, int nx, int rows_owned, int th, int& x, int& k) {
+// Pixel order of a pass (t -> x, k = owned-row index): tiles of (64 / th) x th pixels, row-major
+// inside a tile; th = the shard's row block (<= 8), so a tile is always image-contiguous.  Bands of
+// ts tiles' height over the owned rows, each band in columns of tiles, a column's tiles top to
+// bottom (edge columns / tiles narrower or lower).  A kernel's in-flight rays are a window of
+// consecutive t; ts > 1 makes that window squarer than a one-tile-high strip.
+DEV void tile_pixel(int t, int nx, int rows_owned, int th, int ts, int& x, int& k) {
     const int tw = 64 / th;
-    const int band = t / (th * nx);
-    const int u = t - band * th * nx;
-    const int hb = min(th, rows_owned - th * band);
-    const int c = u / (tw * hb);
-    const int u2 = u - c * tw * hb;
+    const int sh = th * ts;                          // band height (rows)
+    const int band = t / (sh * nx);
+    const int u = t - band * sh * nx;
+    const int hs = min(sh, rows_owned - sh * band);  // rows in this band
+    const int c = u / (tw * hs);                     // tile column
+    const int u2 = u - c * tw * hs;
     const int wb = min(tw, nx - tw * c);
-    const int r = u2 / wb;
-    x = tw * c + (u2 - r * wb);
-    k = th * band + r;
+    const int rt = u2 / (wb * th);                   // tile in the column
+    const int u3 = u2 - rt * wb * th;
+    const int r = u3 / wb;
+    x = tw * c + (u3 - r * wb);
+    k = sh * band + th * rt + r;
 }
 DEV void slot_pixel(const CameraDev& cam, const PassDev& ps, int slot, uint32_t& pixel, uint32_t& sample, int& x,
                     int& y) {
     const int pl = slot / ps.ns, sl = slot - pl * ps.ns;
     int k;
-    tile_pixel(ps.p0 + pl, cam.nx, ps.rows_owned, ps.tile_h, x, k);
+    tile_pixel(ps.p0 + pl, cam.nx, ps.rows_owned, ps.tile_h, ps.tile_s, x, k);
     y = shard_row(k, ps.row_offset, ps.row_stride, ps.row_block);
     pixel = (uint32_t)(y * cam.nx + x);
     sample = (uint32_t)(ps.s0 + sl);
@@ -2029,7 +2033,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv,
     size_t p = 0;
     if (t < np) {
         int x, k;
-        tile_pixel(ps.p0 + p0 + t, nx, ps.rows_owned, ps.tile_h, x, k);
+        tile_pixel(ps.p0 + p0 + t, nx, ps.rows_owned, ps.tile_h, ps.tile_s, x, k);
         p = (size_t)k * nx + x;                 // acc is in natural owned-row order
         if (mode == 0) a = mk(acc[3 * p], acc[3 * p + 1], acc[3 * p + 2]);
     }

@@ -179,6 +179,7 @@ struct PassDev {
     int s0, ns, p0, npass;
     int row_offset, row_stride, rows_owned, row_block;
     int tile_h;        // pixel tile height: 8, or the shard's row block when that is smaller
+    int tile_s;        // tiles per column of a band (the band is tile_s * tile_h rows high)
 };
 
 // Shard row ownership (rtg_render_opts.row_block): owned row k <-> image row y.

@@ -27,7 +27,7 @@ for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
             torch.cuda.synchronize()
             best = min(best, r.stats()["render_ms"])
         ms.append(best)
-    print(f"loop={os.environ.get('RTG_LEVEL_LOOP', '0')} waves={os.environ.get('RTG_DD_WAVES', '2048')} batch={os.environ.get('RTG_BATCH', '0')} N={n}: per-rank render_ms max {max(ms):.2f} min {min(ms):.2f}", flush=True)
+    print(f"batch={os.environ.get('RTG_BATCH', '0')} N={n}: per-rank render_ms max {max(ms):.2f} min {min(ms):.2f}", flush=True)
 if os.environ.get("RTG_KT"):
     # per-kernel device time of one frame with the passes serialised (streams=1, HIP events)
     r.render_device(0, out.data_ptr(), collect_timing=1, streams=1)
