@@ -1106,7 +1106,8 @@ int32_t rtgh_render_scene_multi(const char* xml_path, int32_t device, int32_t nu
         int rc = rtgh_parse_xml(xml_path, &sc);
         if (rc) return rc;
         rtg_scene* gpu = nullptr;
-        rtg_build_opts bo{RTG_BVH_AUTO};
+        rtg_build_opts bo{};
+        bo.bvh_builder = RTG_BVH_AUTO;   // tlas / traversal_tree: automatic (0)
         rc = rtg_scene_create_ex(&sc->desc, device, &bo, &gpu);
         if (rc) { g_err = rtg_last_error(); rtgh_free(sc); return rc; }
         printf("BVH construction complete.\n");

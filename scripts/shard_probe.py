@@ -11,7 +11,8 @@ import rtg  # noqa: E402
 from rtg import scenegen  # noqa: E402
 from rtg.shard import shard_opts  # noqa: E402
 
-sc = scenegen.dragon1m(1920, 1080, spp=64)
+wl = os.environ.get("RTG_WORKLOAD", "dragon1m")      # dragon1m | cornell_pt | cornell | spheres
+sc = getattr(scenegen, wl)(1920, 1080) if wl != "dragon1m" else scenegen.dragon1m(1920, 1080, spp=64)
 r = rtg.Renderer(sc, 0)
 out = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda:0")
 for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
@@ -27,7 +28,7 @@ for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
             torch.cuda.synchronize()
             best = min(best, r.stats()["render_ms"])
         ms.append(best)
-    print(f"batch={os.environ.get('RTG_BATCH', '0')} N={n}: per-rank render_ms max {max(ms):.2f} min {min(ms):.2f}", flush=True)
+    print(f"{wl} batch={os.environ.get('RTG_BATCH', '0')} N={n}: per-rank render_ms max {max(ms):.2f} min {min(ms):.2f}", flush=True)
 if os.environ.get("RTG_KT"):
     # per-kernel device time of one frame with the passes serialised (streams=1, HIP events)
     r.render_device(0, out.data_ptr(), collect_timing=1, streams=1)
