@@ -22,7 +22,10 @@ namespace rtg {
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
 // 34.0 -> 29.7 ms); the simple variants already fit 4 waves (no-op for them)
-#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef RTG_SHADE_WAVES
+#define RTG_SHADE_WAVES 2
+#endif
+#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? 2 : RTG_SHADE_WAVES)))
 // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
 // spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); the full
 // variants keep the default
@@ -1533,7 +1536,9 @@ DEV RayMeta level_meta(const SceneView& sv, int level, const RayQ& rays, const R
     return mt;
 }
 
-template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL>
+// GEN: level 0 (the primary ray of slot i, regenerated), else a queued ray -- separate
+// instantiations, so neither carries the other's live ranges.
+template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL, bool GEN = false>
 __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                uint64_t seed,
                                                const RayQ rays, const RayMeta* __restrict__ meta,
@@ -1549,8 +1554,13 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     RayMeta mt = {};
     if (i < n) {
         h = load_hit_compact(hits, i);
-        level_ray(cam, ps, seed, rays, i, o, d, time);
-        mt = level_meta(sv, level, rays, meta, i);
+        if (GEN) {
+            primary_ray(cam, ps, seed, i, o, d, time);
+            mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
+        } else {
+            load_ray(rays, i, o, d, time);
+            mt = level_meta(sv, level, rays, meta, i);
+        }
     }
     shade_ray<FULL, SPOT, BLOCK, TEX>(sv, cam, level, ps, seed, i, n, h, o, d, time, mt, nodes, shadows, slist,
                                       next_rays, next_meta, qcount);
@@ -2156,18 +2166,20 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
     const NodePlanes np = node_planes(nodes, n);
     const ShadowPlanes sp = shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1));
-    if (sv.full && sv.tex)
-        hipLaunchKernelGGL((k_shade<true, true>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp,
-                           slist, next_rays, next_meta, qcount, n);
-    else if (sv.full)
-        hipLaunchKernelGGL((k_shade<true, true, 256, false>), dim3(nblk(n, 256)), dim3(256), 0, st, sv, cam, level, ps, seed, rays,
-                           meta, hits, np, sp, slist, next_rays, next_meta, qcount, n);
-    else if (sv.spot)
-        hipLaunchKernelGGL((k_shade<false, true>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np,
-                           sp, slist, next_rays, next_meta, qcount, n);
-    else
-        hipLaunchKernelGGL((k_shade<false, false>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np,
-                           sp, slist, next_rays, next_meta, qcount, n);
+#define RTG_SHADE(F, S, B, T, gr, bl)                                                                             \
+    do {                                                                                                          \
+        if (rays.a == nullptr)                                                                                    \
+            hipLaunchKernelGGL((k_shade<F, S, B, T, true>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
+                               slist, next_rays, next_meta, qcount, n);                                           \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_shade<F, S, B, T, false>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
+                               slist, next_rays, next_meta, qcount, n);                                           \
+    } while (0)
+    if (sv.full && sv.tex) RTG_SHADE(true, true, 256, true, dim3(nblk(n, 256)), dim3(256));
+    else if (sv.full) RTG_SHADE(true, true, 256, false, dim3(nblk(n, 256)), dim3(256));
+    else if (sv.spot) RTG_SHADE(false, true, kShadeBlock, false, g, b);
+    else RTG_SHADE(false, false, kShadeBlock, false, g, b);
+#undef RTG_SHADE
 }
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
                    int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted) {
