@@ -1602,7 +1602,8 @@ DEV DielSplit dielectric_split(const SceneView& sv, f3 d, const Ret& ret, const 
 
 constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour to the sample
 
-template <bool FULL, bool SPOT, bool BRDF>
+// GEN: level 0 (primary rays regenerated), else queued rays (separate instantiations, as k_shade)
+template <bool FULL, bool SPOT, bool BRDF, bool GEN = false>
 __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                   uint64_t seed, const RayQ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
@@ -1622,7 +1623,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
         f3 o, d;
         float time;
         RayMeta mt;
-        if (rays.a == nullptr) {        // level 0 without a ray queue: generate the primary ray and its meta
+        if (GEN) {                      // level 0 without a ray queue: generate the primary ray and its meta
             primary_ray(cam, ps, seed, i, o, d, time);
             mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
         } else {
@@ -1637,7 +1638,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
         const int flags = sv.pt_flags;
         f3 T = mk(1, 1, 1);
         int spec = 1, medium = 0;
-        if (level > 0) {
+        if (!GEN && level > 0) {
             const PathRec pr = paths[i];
             T = mk(pr.tr, pr.tg, pr.tb);
             spec = pr.flags & 1;
@@ -2204,16 +2205,22 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
                      unsigned long long* qcount, int n, hipStream_t st) {
     if (n <= 0) return;
     dim3 g(nblk(n, 256)), b(256);
-#define RTG_PT_LAUNCH(F, S, B)                                                                                    \
-    hipLaunchKernelGGL((k_pt_shade<F, S, B>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, \
+#define RTG_PT_LAUNCH1(F, S, B, G)                                                                                \
+    hipLaunchKernelGGL((k_pt_shade<F, S, B, G>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, \
                        node_planes(nodes, n), \
                        shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1)), slist, next_rays, next_meta, next_paths, qcount, n)
+#define RTG_PT_LAUNCH(F, S, B)                                                                                    \
+    do {                                                                                                          \
+        if (rays.a == nullptr) RTG_PT_LAUNCH1(F, S, B, true);                                                     \
+        else RTG_PT_LAUNCH1(F, S, B, false);                                                                      \
+    } while (0)
     // textures / area / environment lights need the full variant; BRDFs alone do not
     if (sv.full && !sv.brdf_only) RTG_PT_LAUNCH(true, true, true);
     else if (sv.full) { if (sv.spot) RTG_PT_LAUNCH(false, true, true); else RTG_PT_LAUNCH(false, false, true); }
     else if (sv.spot) RTG_PT_LAUNCH(false, true, false);
     else RTG_PT_LAUNCH(false, false, false);
 #undef RTG_PT_LAUNCH
+#undef RTG_PT_LAUNCH1
 }
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
                       int n0, int level, int n, hipStream_t st) {
