@@ -20,9 +20,16 @@ import sys
 
 def kname(k):
     k = k.split("(")[0].replace("void ", "")
-    # k_trace<false, false, true> (level 0) and <false, false, false> (secondary levels): one
-    # combined entry as well, the kernel bench.py times as `k_trace<false,false,*>`
     return k
+
+
+# Kernels whose level-0 and queued-level instantiations (last template argument) bench.py times
+# together: one combined entry each as well, `<prefix>, *>` (e.g. k_trace<false, false, *>).
+COMBINED = ("rtg::k_trace<false, false", "rtg::k_shade<false, false, 512, false", "rtg::k_shade<false, true, 512, false")
+
+
+def keys_of(k):
+    return {k} | {p + ", *>" for p in COMBINED if k.startswith(p + ",")}
 
 
 def main():
@@ -35,7 +42,7 @@ def main():
             k = kname(r["Kernel_Name"])
             c = r["Counter_Name"]
             v = float(r["Counter_Value"])
-            for key in {k, "rtg::k_trace<false, false, *>"} if k.startswith("rtg::k_trace<false, false") else {k}:
+            for key in keys_of(k):
                 tot[(key, c)] += v
                 cnt[(key, c)] += 1
     rows = sorted(tot)

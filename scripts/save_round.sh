@@ -18,10 +18,11 @@ for r in rows:
           f"{float(r['TotalDurationNs'])/1e6:10.2f} {float(r['AverageNs'])/1e3:9.1f} {float(r['Percentage']):6.2f}")
 # combined closest-hit line (GEN=true level-0 + GEN=false secondary launches): the kernel whose
 # average bench.py's roofline.avg_launch_ms measures
-ks = [r for r in rows if r['Name'].replace('void ', '').startswith('rtg::k_trace<false, false')]
-if ks:
-    c = sum(int(r['Calls']) for r in ks); t = sum(float(r['TotalDurationNs']) for r in ks)
-    print(f"{'rtg::k_trace<false, false, *> (combined)':48s} {c:6d} {t/1e6:10.2f} {t/c/1e3:9.1f}")
+for pre in ('rtg::k_trace<false, false', 'rtg::k_shade<false, false, 512, false'):
+    ks = [r for r in rows if r['Name'].replace('void ', '').startswith(pre + ',')]
+    if ks:
+        c = sum(int(r['Calls']) for r in ks); t = sum(float(r['TotalDurationNs']) for r in ks)
+        print(f"{pre + ', *> (combined)':48s} {c:6d} {t/1e6:10.2f} {t/c/1e3:9.1f}")
 PY
 cp $D/kt/kt_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
 python3 scripts/pmc_counters.py $D profiles/${TAG}_counters.csv profiles/${TAG}_counters.json $WL
