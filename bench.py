@@ -5,20 +5,27 @@ One step = one full frame.  With N ranks (torch.distributed.run, one process per
 renders every sample of the rows with (y // 4) % N == r compactly, and librtg gathers the
 shards' rows onto rank 0's frame with RCCL point-to-point transfers (rtg_comm_init_rank +
 rtg_render_ranked: the same shard + gather code as rtg_render_opts.num_devices and
-`rtg_cli --devices N`).  value = rays traced by all ranks / max-over-ranks frame time.
-RTG_BENCH_REHEARSE=1 rehearses the N-rank path on one GPU (every rank on cuda:0, gloo gather
-through host memory); its numbers are not a scaling measurement.
+`rtg_cli --devices N`; the fan-out it replaces is src/Scene.cpp:340-356).  value = rays traced
+by all ranks / max-over-ranks frame time.  --ranked takes that RCCL path even at N = 1 (a
+1-rank communicator).  RTG_BENCH_REHEARSE=1 rehearses the N-rank path on one GPU (every rank
+on cuda:0, gloo gather through host memory); its numbers are not a scaling measurement.
 
 Prints ONE JSON line (rank 0).  Extra objects:
   roofline     the dominant kernel (k_trace, closest hit) against the ceiling that binds it, VALU
                issue (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, one wave64 VALU instruction per 2
                cycles at 2.4 GHz = 1228.8 G wave-instructions/s), from the committed PMC counters
-               (profiles/counters_current.json: SQ_INSTS_VALU per launch) divided by the live
-               HIP-event launch time; `kernels` holds the same for k_shadow and k_shade plus each
-               kernel's measured HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) against 8 TB/s; `model`
-               holds SURVEY §8(d)'s algorithmic byte model (B = 64 + 32 N_node + 36 N_tri per ray);
-               `frame_hbm` the whole frame's measured HBM bytes over ms_per_step.
-  cpu_baseline the CPU restatement (oracle/) on a bounded row sample of the same frame.
+               (profiles/counters_<workload>.json: SQ_INSTS_VALU per launch) divided by the live
+               HIP-event launch time; `kernels` holds the same for k_shadow, k_shade, k_resolve and
+               k_accumulate plus each kernel's measured HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE)
+               against 8 TB/s, and the traversal kernels' SIMD lane efficiency (node steps / lane
+               slots of a collect_stats frame) with the lane-adjusted VALU fraction; `model` holds
+               SURVEY §8(d)'s fixed algorithmic byte model (B = 64 + 32 N_node + 36 N_tri +
+               16 N_sphere per ray, N_* from tests/golden/yardstick.json); `frame_hbm` the whole
+               frame's measured HBM bytes over ms_per_step.
+  cpu_baseline the CPU restatement (oracle/) on a bounded row sample of the same frame (N = 1).
+  parity       that row sample against the same rows of the GPU frame (bitwise).
+  multi        N > 1 (or --ranked): rank 0 renders the full frame alone after the timed loop and
+               compares it with the gathered frame (gathered_equals_single).
 """
 from __future__ import annotations
 
@@ -28,6 +35,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "raytracer-795_amd"))
 
@@ -35,20 +44,27 @@ METRIC = "Mray/s + ms/frame at 1920×1080, 64 spp; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0                       # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s (spec)
 L2_PEAK_GBS = 34500.0                       # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate
 VALU_PEAK_GIPS = 256 * 4 * 2.4 / 2          # G wave64-VALU-instructions/s (see the docstring)
-COUNTERS = os.path.join(ROOT, "profiles", "counters_current.json")
+PROFILES = os.path.join(ROOT, "profiles")
+YARDSTICK = os.path.join(ROOT, "tests", "golden", "yardstick.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def load_counters() -> dict:
-    """Per-dispatch PMC counter means of the last committed profiling run (scripts/pmc_counters.py)."""
-    try:
-        with open(COUNTERS) as f:
-            return json.load(f)
-    except (OSError, ValueError):
-        return {}
+def load_counters(workload: str) -> dict:
+    """Per-dispatch PMC counter means of the last committed profiling run of this workload
+    (scripts/pmc_counters.py): profiles/counters_<workload>.json, or counters_current.json when
+    it was taken on this workload."""
+    for f in (os.path.join(PROFILES, f"counters_{workload}.json"), os.path.join(PROFILES, "counters_current.json")):
+        try:
+            with open(f) as fh:
+                c = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if c.get("workload", "dragon1m") == workload:
+            return c
+    return {}
 
 
 def kernel_roof(counters: dict, name: str, avg_ms: float, launches: int) -> dict | None:
@@ -93,7 +109,8 @@ def frame_hbm_bytes(counters: dict, shade_name: str, shade_per_frame: int) -> fl
     return tot / frames
 
 
-def cpu_baseline(scene, rows: int, threads: int) -> dict:
+def cpu_baseline(scene, rows: int, threads: int):
+    """The oracle on rows [y0, y0+rows) of the same frame: (cpu_baseline object, rgb rows)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
@@ -101,14 +118,34 @@ def cpu_baseline(scene, rows: int, threads: int) -> dict:
     o = pyoracle.Oracle(scene)
     y0 = cam.ny // 2 - rows // 2
     t0 = time.perf_counter()
-    o.render(0, nthreads=threads, row_begin=y0, row_end=y0 + rows)
+    rgb, _, _, _ = o.render(0, nthreads=threads, row_begin=y0, row_end=y0 + rows)
     dt = time.perf_counter() - t0
     c = o.ray_counts()
     nrays = c["primary"] + c["secondary"] + c["shadow"]
     o.close()
-    return {"value": nrays / dt / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": f"rows {y0}..{y0 + rows - 1} of the same 1920x1080x{cam.num_samples}spp frame "
-                      f"({rows * cam.nx} px, {nrays} rays, {dt:.1f} s, literal visit-both-children BVH)"}
+    cpu = {"value": nrays / dt / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
+           "sample": f"rows {y0}..{y0 + rows - 1} of the same 1920x1080x{cam.num_samples}spp frame "
+                     f"({rows * cam.nx} px, {nrays} rays, {dt:.1f} s, literal visit-both-children BVH)"}
+    return cpu, (y0, y0 + rows), rgb[y0:y0 + rows]
+
+
+def compare_rows(gpu_rows: np.ndarray, ref_rows: np.ndarray, rows) -> dict:
+    g, r = np.ascontiguousarray(gpu_rows, np.float32), np.ascontiguousarray(ref_rows, np.float32)
+    nanm = int(np.sum(np.isnan(g) != np.isnan(r)))
+    d = np.abs(g.astype(np.float64) - r.astype(np.float64))
+    d = np.where(np.isnan(d), 0.0, d)
+    diff = int(np.sum(np.nan_to_num(g).view(np.int32) != np.nan_to_num(r).view(np.int32)))
+    return {"rows": [int(rows[0]), int(rows[1]) - 1], "values": int(g.size), "linf": float(d.max()) if d.size else 0.0,
+            "differing": diff, "differing_frac": diff / max(g.size, 1), "nan_mismatch": nanm,
+            "against": "oracle/ CPU restatement (cpu_baseline's rows), bitwise on the 0..255 float framebuffer"}
+
+
+def load_yardstick(workload: str) -> dict:
+    try:
+        with open(YARDSTICK) as f:
+            return json.load(f).get(workload, {})
+    except (OSError, ValueError):
+        return {}
 
 
 # BASELINE.json configs -> (rtg.scenegen factory, default spp, config.workload text, data text)
@@ -134,6 +171,93 @@ WORKLOADS = {
 }
 
 
+def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
+    """roofline.kernels: every frame kernel with a live launch time and committed counters."""
+    ks = counters.get("kernels", {})
+
+    def first(prefix):
+        names = sorted((k for k in ks if k.startswith(prefix)),
+                       key=lambda k: (not k.endswith("*>"), -ks[k].get("dispatches_SQ_INSTS_VALU", 0)))
+        return names[0] if names else ""
+
+    shade = first("rtg::k_pt_shade<" if pt else "rtg::k_shade<")
+    rows = [("k_trace", "rtg::k_trace<false, false, *>", "trace"),
+            ("k_shadow", "rtg::k_shadow<false, false, false>", "shadow"),
+            ("k_pt_shade" if pt else "k_shade", shade, "shade"),
+            ("k_accumulate", "rtg::k_accumulate", "accumulate")]
+    if not pt:
+        rows.append(("k_resolve", "rtg::k_resolve", "resolve"))
+    out = {}
+    for key, name, slot in rows:
+        n = st_roof.get(f"{slot}_launches", 0)
+        avg = st_roof.get(f"{slot}_ms", 0.0) / max(n, 1)
+        kr = kernel_roof(counters, name, avg, n)
+        if kr:
+            out[key] = kr
+    # SIMD lane efficiency of the traversal kernels (collect_stats frame): node steps / lane slots
+    for key, pre in (("k_trace", "trace"), ("k_shadow", "shadow")):
+        slots = st_stats.get(f"{pre}_lane_slots", 0)
+        if key in out and slots > 0:
+            eff = st_stats[f"{pre}_steps"] / slots
+            out[key]["simd_eff"] = round(eff, 4)
+            if "valu" in out[key]:
+                out[key]["valu"]["lane_adjusted_frac"] = round(out[key]["valu"]["frac"] * eff, 4)
+    sq = st_stats.get("shadow_rays", 0)
+    if "k_shadow" in out and sq > 0:
+        b = st_stats["shadow_blocked"]
+        ub = max(sq - b, 1)
+        out["k_shadow"]["queries"] = {
+            "blocked_frac": round(b / sq, 4),
+            "steps_per_blocked": round(st_stats["shadow_blocked_steps"] / max(b, 1), 3),
+            "steps_per_unblocked": round((st_stats["shadow_steps"] - st_stats["shadow_blocked_steps"]) / ub, 3),
+            "tris_per_blocked": round(st_stats["shadow_blocked_tris"] / max(b, 1), 3),
+            "tris_per_unblocked": round((st_stats["shadow_tri_tests"] - st_stats["shadow_blocked_tris"]) / ub, 3)}
+    return out, shade
+
+
+def roofline(counters, st_roof, st_stats, workload: str, ms_per_step: float, pt: bool) -> dict:
+    kern, shade = kernel_table(counters, st_roof, st_stats, pt)
+    # SURVEY §8(d): fixed algorithmic bytes per closest-hit ray (tests/golden/yardstick.json), priced
+    # over the k_trace launches' rays and live launch time
+    ys = load_yardstick(workload)
+    trace_avg = st_roof["trace_ms"] / max(st_roof["trace_launches"], 1)
+    traced = st_stats["primary_rays"] + st_stats["secondary_rays"]
+    model = None
+    if ys:
+        bpr = ys["bytes_per_ray"]
+        rays_per_launch = (st_roof["primary_rays"] + st_roof["secondary_rays"]) / max(st_roof["trace_launches"], 1)
+        gbs = bpr * rays_per_launch / (trace_avg * 1e-3) / 1e9 if trace_avg > 0 else 0.0
+        model = {"bytes_per_ray": bpr, "n_node": ys["n_node"], "n_tri": ys["n_tri"], "n_sphere": ys["n_sphere"],
+                 "shadow_bytes_per_ray": ys["shadow_bytes_per_ray"], "source": "tests/golden/yardstick.json (" +
+                 ys["sample"] + ", canonical ordered early-exit traversal of the reference trees)",
+                 "achieved": round(gbs, 1), "unit": "GB/s", "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                 "frac_of_l2_peak": round(gbs / L2_PEAK_GBS, 4),
+                 "note": "bytes the canonical traversal requests per ray; the vL1D / L2 / MALL serve most of "
+                         "them (compare kernels.k_trace.hbm), so this is not an HBM roofline"}
+    gpu_walk = {"node_records_per_ray": round(st_stats["node_visits"] / max(traced, 1), 3),
+                "tri_tests_per_ray": round(st_stats["tri_tests"] / max(traced, 1), 3),
+                "shadow_node_records_per_query": round(st_stats["shadow_node_visits"] / max(st_stats["shadow_rays"], 1), 3),
+                "shadow_tri_tests_per_query": round(st_stats["shadow_tri_tests"] / max(st_stats["shadow_rays"], 1), 3)}
+    tr = kern.get("k_trace", {})
+    roof = {"bound": "valu", "kernel": "k_trace<false,false,*> (closest hit; GEN=true generates the primary "
+                                       "rays at level 0, GEN=false traces secondary levels)",
+            "achieved": tr.get("valu", {}).get("achieved"), "peak": VALU_PEAK_GIPS, "unit": "G wave-inst/s",
+            "frac": tr.get("valu", {}).get("frac"),
+            "traffic": tr.get("hbm", {}).get("bytes_per_launch"),
+            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE, profiles/counters_<workload>.json)",
+            "peak_source": "MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, wave64 VALU instruction per 2 cycles, 2400 MHz",
+            "avg_launch_ms": round(trace_avg, 4), "launches": st_roof["trace_launches"],
+            "timing": "HIP events around each launch in a streams=1 frame outside the timed region",
+            "counters": counters.get("source"), "roofline_frame_ms": round(st_roof["render_ms"], 2),
+            "kernels": kern, "model": model, "gpu_walk": gpu_walk}
+    fb = frame_hbm_bytes(counters, shade, st_roof["shade_launches"]) if shade else None
+    if fb:
+        roof["frame_hbm"] = {"bytes_per_frame": round(fb), "achieved": round(fb / (ms_per_step * 1e-3) / 1e9, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(fb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +271,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=540)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ranked", action="store_true",
+                    help="render through rtg_render_ranked (RCCL shard + gather) even with one rank")
     ap.add_argument("--tlas", choices=["auto", "off", "on"], default="auto",
                     help="top-level BVH over objects / instances (rtg_build_opts.tlas; auto: from 16 entries)")
     args = ap.parse_args()
@@ -169,6 +295,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import rtg
+    from rtg import _abi as rtg_abi
     from rtg import scenegen
     from rtg.shard import ROW_BLOCK, gather_frame, max_shard_rows, shard_opts
 
@@ -182,30 +309,46 @@ def main():
     create_ms = (time.perf_counter() - t0) * 1e3
     log(f"[rank {rank}] rtg_scene_create (BVH build + upload) {create_ms:.0f} ms")
     cam = scene.cameras[0]
+    pt = cam.integrator == rtg_abi.INTEGRATOR_PATH
     frame = torch.zeros((cam.ny, cam.nx, 3), dtype=torch.float32, device=f"cuda:{local}")
     host = torch.empty((cam.ny, cam.nx, 3), dtype=torch.float32, pin_memory=True)
     stream = torch.cuda.current_stream().cuda_stream
     comm = None
     part = None
-    if world > 1 and not rehearse:
+    if (world > 1 or args.ranked) and not rehearse:
         # librtg's own RCCL communicator (ncclCommInitRank); its id travels over torch.distributed
         uid = [rtg.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
+        if dist is not None:
+            dist.broadcast_object_list(uid, src=0)
         comm = rtg.Comm(uid[0], world, rank, local)
     elif world > 1:
         part = torch.zeros((max_shard_rows(cam.ny, world), cam.nx, 3), dtype=torch.float32, device=frame.device)
+    sharded = comm is not None or part is not None
+
+    def single(buf, **kw):
+        r.render_device(0, buf.data_ptr(), stream, **kw)
+        return r.stats()
 
     def step(**kw):
-        if world == 1:
-            r.render_device(0, frame.data_ptr(), stream, **kw)
-        elif comm is not None:     # shard + RCCL gather inside librtg (rtg_render_ranked)
+        if comm is not None:       # shard + RCCL gather inside librtg (rtg_render_ranked)
             r.render_ranked(0, comm, frame.data_ptr(), stream, row_block=ROW_BLOCK, **kw)
-        else:                      # rehearsal: compact shard, gloo gather in Python
+        elif part is not None:     # rehearsal: compact shard, gloo gather in Python
             r.render_device(0, part.data_ptr(), stream, **shard_opts(rank, world), compact_rows=1, **kw)
             st = r.stats()
             gather_frame(part, frame, rank, world, dist)
             return st
+        else:
+            r.render_device(0, frame.data_ptr(), stream, **kw)
         return r.stats()
+
+    def roofline_frames(buf):
+        """traversal statistics (collect_stats) and the per-launch timing frame: passes one at a
+        time (streams=1) so every launch is timed alone by its HIP events (the timed frames overlap
+        passes on several streams, where an event pair would also count other streams' work); the
+        first streams=1 frame also grows that lane's level buffers, so it is run twice."""
+        st_stats = single(buf, collect_stats=1)
+        single(buf, collect_timing=1, streams=1)
+        return st_stats, single(buf, collect_timing=1, streams=1)
 
     # one frame to the host right after the upload: the end-to-end time of a fresh scene
     t0 = time.perf_counter()
@@ -214,14 +357,9 @@ def main():
         host.copy_(frame, non_blocking=True)
     torch.cuda.synchronize()
     first_frame_ms = (time.perf_counter() - t0) * 1e3
-    # traversal statistics for the byte model (outside the timed region)
-    st_stats = step(collect_stats=1)
-    # roofline frame (outside the timed region): passes one at a time (streams=1) so every
-    # trace / shade / shadow launch is timed alone by its HIP events; the timed frames below
-    # overlap passes on several streams, where an event pair would also count other streams'
-    # work (twice: the first streams=1 frame also grows that lane's level buffers)
-    step(collect_timing=1, streams=1)
-    st_roof = step(collect_timing=1, streams=1)
+    st_stats = st_roof = None
+    if not sharded:
+        st_stats, st_roof = roofline_frames(frame)
     for _ in range(args.warmup):
         step()
 
@@ -258,68 +396,47 @@ def main():
     value = rays / elapsed / 1e6
     rays_frame = rays // max(args.steps, 1)
 
-    if rehearse and rank == 0 and world > 1:
-        # the gathered frame must equal this rank's own single-device frame bit for bit
+    multi = None
+    if sharded and rank == 0:
+        # rank 0 alone: the full frame on its own device vs the gathered frame (bit for bit), then
+        # its single-device roofline frames (same kernels and counters as the N = 1 line)
         full = torch.zeros_like(frame)
-        r.render_device(0, full.data_ptr(), stream)
+        t0 = time.perf_counter()
+        single(full)
         torch.cuda.synchronize()
+        single_ms = (time.perf_counter() - t0) * 1e3
         same = bool(torch.equal(full.view(torch.int32), frame.view(torch.int32)))
-        log(f"[rank 0] rehearsal: gathered frame == single-device frame: {same}")
-        if not same:
+        log(f"[rank 0] gathered frame == single-device frame: {same}")
+        multi = {"gathered_equals_single": same, "ranks": world,
+                 "gather": "rehearsal: gloo gather through host memory (all ranks on one GPU)" if rehearse
+                 else "RCCL point-to-point rows gather inside librtg (rtg_render_ranked)",
+                 "single_device_frame_ms": round(single_ms, 2), "row_block": ROW_BLOCK,
+                 "gather_ms_rank0": round(st.get("gather_ms", 0.0), 3)}
+        if rehearse and not same:
             raise SystemExit("rehearsal: gathered frame differs from the single-device frame")
+        st_stats, st_roof = roofline_frames(full)
+        del full
+    if dist is not None:
+        dist.barrier()
 
     if rank == 0:
-        counters = load_counters()
-        trace_avg = st_roof["trace_ms"] / max(st_roof["trace_launches"], 1)
-        shadow_avg = st_roof["shadow_ms"] / max(st_roof["shadow_launches"], 1)
-        shade_avg = st_roof["shade_ms"] / max(st_roof["shade_launches"], 1)
-        shade_names = sorted((k for k in counters.get("kernels", {}) if k.startswith("rtg::k_shade<")),
-                             key=lambda k: -counters["kernels"][k].get("dispatches_SQ_INSTS_VALU", 0))
-        same_wl = counters.get("workload", "dragon1m") == args.workload and world == 1
-        kern = {}
-        if same_wl:
-            for key, name, avg, n in (("k_trace", "rtg::k_trace<false, false, *>", trace_avg, st_roof["trace_launches"]),
-                                      ("k_shadow", "rtg::k_shadow<false, false, false>", shadow_avg, st_roof["shadow_launches"]),
-                                      ("k_shade", shade_names[0] if shade_names else "", shade_avg, st_roof["shade_launches"])):
-                kr = kernel_roof(counters, name, avg, n)
-                if kr:
-                    kern[key] = kr
-        # SURVEY §8(d) algorithmic byte model of the closest-hit kernel
-        traced = st_stats["primary_rays"] + st_stats["secondary_rays"]
-        n_node = st_stats["node_visits"] / max(traced, 1)
-        n_tri = st_stats["tri_tests"] / max(traced, 1)
-        bytes_per_ray = 64 + 32 * n_node + 36 * n_tri
-        trace_rays = st_roof["primary_rays"] + st_roof["secondary_rays"]
-        model_gbs = (bytes_per_ray * trace_rays / max(st_roof["trace_launches"], 1)) / (trace_avg * 1e-3) / 1e9 \
-            if trace_avg > 0 else 0.0
-        model = {"bytes_per_ray": round(bytes_per_ray, 1), "n_node": round(n_node, 2), "n_tri": round(n_tri, 2),
-                 "achieved": round(model_gbs, 1), "unit": "GB/s",
-                 "frac_of_hbm_peak": round(model_gbs / HBM_PEAK_GBS, 4),
-                 "frac_of_l2_peak": round(model_gbs / L2_PEAK_GBS, 4),
-                 "note": "node / triangle bytes the traversal requests; most are served by the vL1D / L2 "
-                         "(compare kernels.k_trace.hbm), so this is not an HBM roofline"}
-        tr = kern.get("k_trace", {})
-        roof = {"bound": "valu", "kernel": "k_trace<false,false,*> (closest hit; GEN=true generates the primary "
-                                           "rays at level 0, GEN=false traces secondary levels)",
-                "achieved": tr.get("valu", {}).get("achieved"), "peak": VALU_PEAK_GIPS, "unit": "G wave-inst/s",
-                "frac": tr.get("valu", {}).get("frac"),
-                "traffic": tr.get("hbm", {}).get("bytes_per_launch"),
-                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE, profiles/counters_current.json)",
-                "peak_source": "MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, wave64 VALU instruction per 2 cycles, 2400 MHz",
-                "avg_launch_ms": round(trace_avg, 4), "launches": st_roof["trace_launches"],
-                "timing": "HIP events around each launch in a streams=1 frame outside the timed region",
-                "counters": counters.get("source"), "roofline_frame_ms": round(st_roof["render_ms"], 2),
-                "kernels": kern, "model": model}
-        fb = frame_hbm_bytes(counters, shade_names[0], st_roof["shade_launches"]) if (same_wl and shade_names) else None
-        if fb:
-            roof["frame_hbm"] = {"bytes_per_frame": round(fb), "achieved": round(fb / (ms_per_step * 1e-3) / 1e9, 1),
-                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(fb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        cpu = None
-        if not args.no_cpu and world == 1:
+        counters = load_counters(args.workload)
+        roof = roofline(counters, st_roof, st_stats, args.workload, ms_per_step, pt)
+        if sharded:
+            roof["note"] = "rank 0's single-device roofline frames after the timed loop (the sharded frame's passes " \
+                           "are smaller; the counters are per launch of the full frame)"
+        cpu = parity = None
+        cpu_note = None
+        if args.no_cpu:
+            cpu_note = "skipped (--no-cpu)"
+        elif world > 1:
+            cpu_note = "measured on the N = 1 line only (rank 0, N = 1 per the bench contract); see BENCH N=1"
+        else:
             log("[rank 0] cpu baseline ...")
-            cpu = cpu_baseline(scene, args.cpu_rows, args.cpu_threads)
-        if world == 1:
+            cpu, rows, ref_rows = cpu_baseline(scene, args.cpu_rows, args.cpu_threads)
+            parity = compare_rows(host.numpy()[rows[0]:rows[1]], ref_rows, rows)
+            log(f"[rank 0] parity rows {rows}: linf={parity['linf']} differing={parity['differing']}")
+        if world == 1 and comm is None:
             par = "single GPU"
         elif rehearse:
             par = f"{ROW_BLOCK}-row-block pixel shards x{world} + gloo gather (rehearsal, all ranks on one GPU)"
@@ -338,9 +455,11 @@ def main():
                                   "total": round(create_ms + first_frame_ms, 1),
                                   "note": "rtg_scene_create (BVH build + upload) + the first frame incl. its D2H copy"},
                 "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
-                "kernel_ms_rank0_streams1": {"trace": round(st_roof["trace_ms"], 2), "shade": round(st_roof["shade_ms"], 2),
-                                             "shadow": round(st_roof["shadow_ms"], 2)},
-                "roofline": roof, "cpu_baseline": cpu}
+                "kernel_ms_rank0_streams1": {k: round(st_roof[f"{k}_ms"], 2)
+                                             for k in ("trace", "shade", "shadow", "resolve", "accumulate")},
+                "roofline": roof, "cpu_baseline": cpu, "parity": parity, "multi": multi}
+        if cpu_note:
+            line["cpu_baseline_note"] = cpu_note
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 5
+#define RTG_ABI_VERSION 6
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -278,6 +278,13 @@ typedef struct rtg_render_stats {
     int32_t shade_launches;
     int32_t devices;         /* devices that rendered the frame (num_devices fan-out or ranks: 1 here) */
     double gather_ms;        /* multi-GPU: host wall time from the last shard's end to the gathered frame */
+    uint64_t shadow_blocked;       /* collect_stats: shadow queries found blocked ... */
+    uint64_t shadow_blocked_steps; /*   ... their node steps and triangle tests (the remainder of */
+    uint64_t shadow_blocked_tris;  /*   shadow_steps / shadow_tri_tests belongs to unblocked queries) */
+    double resolve_ms;       /* collect_timing: summed device time of the bottom-up resolve launches */
+    double accumulate_ms;    /* collect_timing: summed device time of the sample accumulation launches */
+    int32_t resolve_launches;
+    int32_t accumulate_launches;
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */

@@ -35,6 +35,8 @@ def load():
         lib.orc_render.restype = C.c_int
         lib.orc_last_ray_counts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         lib.orc_last_ray_counts.restype = None
+        lib.orc_canonical_counts.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]
+        lib.orc_canonical_counts.restype = None
         lib.orc_trace.argtypes = [C.c_void_p, C.POINTER(A.Ray), C.c_int, C.POINTER(A.Hit)]
         lib.orc_trace.restype = C.c_int
         lib.orc_object_bvh.argtypes = [C.c_void_p, C.c_int, A.PI, A.PI, A.PI, A.PI, A.PF]
@@ -93,6 +95,14 @@ class Oracle:
         c = (C.c_uint64 * 3)()
         self.lib.orc_last_ray_counts(self.handle, c)
         return {"primary": c[0], "secondary": c[1], "shadow": c[2]}
+
+    def canonical_counts(self, enable: bool = True) -> dict:
+        """SURVEY §8(d) yardstick: counts of the last render (see orc_canonical_counts), then
+        enables / disables counting for the next renders."""
+        c = (C.c_uint64 * 8)()
+        self.lib.orc_canonical_counts(self.handle, int(enable), c)
+        keys = ("rays", "nodes", "tris", "spheres", "shadow_rays", "shadow_nodes", "shadow_tris", "shadow_spheres")
+        return dict(zip(keys, list(c)))
 
     def trace(self, origins, directions, times=None):
         n = len(origins)

@@ -360,6 +360,8 @@ struct orc_scene {
     v3* etris;                /* world-space triangles of mesh emitters, 3 vertices each */
     float* ecdf;              /* running float sum of their areas, per emitter range */
     uint64_t counts[3];
+    int canon_on;             /* orc_canonical_counts enabled */
+    uint64_t canon[8];
 };
 typedef struct Emit {
     int obj;                  /* object index */
@@ -375,6 +377,7 @@ typedef struct {
     struct orc_scene* s;
     RngCtx rng;
     uint64_t n_primary, n_secondary, n_shadow;
+    uint64_t canon[8];        /* orc_canonical_counts: see canon_count() */
 } Ctx;
 
 /* ------------------------------------------------------------------ textures (src/Texture.cpp) */
@@ -971,19 +974,106 @@ static v3 specular_term(v3 LC, v3 wo, v3 wi, const RetVal* ret, const rtg_materi
     return vcw(LC, vmul(mv(m->specular), (float)pow((double)alpha, m->phong_exp)));
 }
 
-static RetVal trace(Ctx* cx, const Ray* r, int kind) {
+/* ------------------------------------------------------------------ SURVEY §8(d) yardstick
+   Not the reference's algorithm: the canonical ordered, early-exit traversal a GPU closest-hit
+   kernel would run over the SAME scene and the reference's median-split trees, used only to
+   count the algorithmic work per ray that §8(d)'s byte model prices
+   (B = 64 + 32 N_node + 36 N_tri + 16 N_sphere): N_node = 32-byte child records read (both
+   children's boxes of every interior node popped, the root box once), N_tri / N_sphere =
+   primitive tests.  Closest-hit rays (primary + secondary) keep the nearest accepted t (> 0) as
+   the far end of every box interval; shadow rays stop at the first hit in (0, tmax) (any hit).
+   The top level is the reference's object / instance loop (src/Helper.cpp:32-73). */
+static int canon_box(const Ray* r, v3 mn, v3 mx, float tmax, float* tentry) {
+    float t0 = 0.0f, t1 = tmax;
+    for (int a = 0; a < 3; a++) {
+        float o = vget(r->origin, a), d = vget(r->direction, a), lo = vget(mn, a), hi = vget(mx, a);
+        float ta = (lo - o) / d, tb = (hi - o) / d;
+        if (ta != ta || tb != tb) continue;          /* 0 * inf: the slab does not constrain */
+        if (ta > tb) { float x = ta; ta = tb; tb = x; }
+        if (ta > t0) t0 = ta;
+        if (tb < t1) t1 = tb;
+    }
+    *tentry = t0;
+    return t0 <= t1;
+}
+/* one object in its own space: returns the nearest accepted t in (0, tmax) or tmax */
+static float canon_object(const struct orc_scene* s, const Obj* o, const Ray* r, float tmax, int any, uint64_t* c) {
+    float best = tmax;
+    int done = 0;
+    if (o->type == RTG_OBJ_SPHERE) {
+        c[3]++;
+        RetVal h = prim_intersect(s, o, 0, r);
+        if (h.full) { float t = ray_gett(r, h.point); if (t > 0 && t < best) best = t; }
+        return best;
+    }
+    int stack[64], sp = 0;
+    int node = o->root;
+    if (node < 0) return best;
+    const BNode* N = &o->nodes[node];
+    if (N->left >= 0 || N->right >= 0) {
+        float te;
+        c[1]++;
+        if (!canon_box(r, N->mn, N->mx, best, &te)) return best;
+    }
+    stack[sp++] = node;
+    while (sp > 0 && !done) {
+        N = &o->nodes[stack[--sp]];
+        if (N->left < 0 && N->right < 0) {
+            for (int k = N->start; k < N->end && !done; k++) {
+                c[2]++;
+                RetVal h = prim_intersect(s, o, k, r);
+                if (!h.full) continue;
+                float t = ray_gett(r, h.point);
+                if (t > 0 && t < best) { best = t; done = any; }
+            }
+            continue;
+        }
+        int kid[2] = {N->left, N->right}, hit[2] = {0, 0};
+        float te[2] = {0, 0};
+        for (int q = 0; q < 2; q++) {
+            if (kid[q] < 0) continue;
+            c[1]++;
+            hit[q] = canon_box(r, o->nodes[kid[q]].mn, o->nodes[kid[q]].mx, best, &te[q]);
+        }
+        if (hit[0] && hit[1]) {                  /* nearer child on top */
+            int nearq = te[1] < te[0];
+            stack[sp++] = kid[1 - nearq];
+            stack[sp++] = kid[nearq];
+        } else if (hit[0]) stack[sp++] = kid[0];
+        else if (hit[1]) stack[sp++] = kid[1];
+    }
+    return best;
+}
+static void canon_count(Ctx* cx, const Ray* r, int kind, float tmax) {
+    const struct orc_scene* s = cx->s;
+    if (visnan(r->origin) || visnan(r->direction)) return;
+    uint64_t* c = cx->canon + (kind == 2 ? 4 : 0);
+    c[0]++;
+    float best = tmax;
+    for (int i = 0; i < s->nobj + s->ninst; i++) {
+        const Obj* o = i < s->nobj ? &s->objs[i] : &s->objs[s->insts[i - s->nobj].base];
+        Ray tr = i < s->nobj ? transform_ray(r, &o->inv, o->blur)
+                             : transform_ray(r, &s->insts[i - s->nobj].inv, s->insts[i - s->nobj].blur);
+        best = canon_object(s, o, &tr, best, kind == 2, c);
+        if (kind == 2 && best < tmax) return;    /* shadow: first blocker ends the query */
+    }
+}
+
+static RetVal trace_bounded(Ctx* cx, const Ray* r, int kind, float tmax) {
     if (!(visnan(r->origin) || visnan(r->direction))) {
         if (kind == 0) cx->n_primary++; else if (kind == 1) cx->n_secondary++; else cx->n_shadow++;
     }
+    if (cx->s->canon_on) canon_count(cx, r, kind, tmax);
     return find_intersection(cx->s, r);
 }
+static RetVal trace(Ctx* cx, const Ray* r, int kind) { return trace_bounded(cx, r, kind, FLT_MAX); }
 
 /* distance-compared shadow test of Point/Spot/Area lights, e.g. PointLight::IsShadow Light.cpp:188-204 */
 static int shadow_towards(Ctx* cx, const Ray* prime, const RetVal* ret, v3 L) {
     struct orc_scene* s = cx->s;
     v3 dir = vsub(L, ret->point);
     Ray ray = R(vadd(ret->point, vmul(ret->normal, s->shadowEps)), vdivs(dir, vnorm(dir)), prime->time);
-    RetVal nr = trace(cx, &ray, 2);
+    RetVal nr = trace_bounded(cx, &ray, 2, vnorm(vsub(L, ray.origin)));
     if (nr.full) return vnorm(vsub(ret->point, L)) > vnorm(vsub(ret->point, nr.point));
     return 0;
 }
@@ -1305,7 +1395,7 @@ static v3 emitter_shading(Ctx* cx, int k, const Ray* prime, const RetVal* ret, c
     v3 c = surface_response(LC, wo, wi, ret, m);
     if (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) return V(0, 0, 0);   /* nothing to shadow: no ray */
     Ray ray = R(vadd(p, vmul(ret->normal, s->shadowEps)), wi, prime->time);
-    RetVal nr = trace(cx, &ray, 2);
+    RetVal nr = trace_bounded(cx, &ray, 2, dist);
     if (nr.full && vnorm(vsub(p, nr.point)) < dist - (s->shadowEps + 1e-4f * dist)) return V(0, 0, 0);
     return c;
 }
@@ -1696,6 +1786,7 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
     if (row_end <= 0 || row_end > ny) row_end = ny;
     if (row_begin < 0) row_begin = 0;
     uint64_t np = 0, nsec = 0, nsh = 0;
+    uint64_t canon[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int pathT = cd->integrator == RTG_INTEGRATOR_PATH;
     if (pathT && pobj) for (int k = 0; k < nx * ny; k++) { pobj[k] = -1; pprim[k] = -1; pt[k] = 0; }
 #ifdef _OPENMP
@@ -1704,7 +1795,7 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : np, nsec, nsh)
     for (int y = row_begin; y < row_end; y++) {
         if ((y / row_block) % row_stride != row_offset % row_stride) continue;
-        Ctx cx = {s, {seed, 0, 0}, 0, 0, 0};
+        Ctx cx = {s, {seed, 0, 0}, 0, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
         for (int x = 0; x < nx; x++) {
             uint32_t pixel = (uint32_t)(y * nx + x);
             cx.rng.pixel = pixel;
@@ -1745,9 +1836,19 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cd, uint64_t seed, int nthre
             o[0] = color.x; o[1] = color.y; o[2] = color.z;
         }
         np += cx.n_primary; nsec += cx.n_secondary; nsh += cx.n_shadow;
+        if (s->canon_on) {
+#pragma omp critical
+            for (int k = 0; k < 8; k++) canon[k] += cx.canon[k];
+        }
     }
     s->counts[0] = np; s->counts[1] = nsec; s->counts[2] = nsh;
+    memcpy(s->canon, canon, sizeof canon);
     return RTG_OK;
+}
+
+void orc_canonical_counts(orc_scene* s, int enable, uint64_t out[8]) {
+    if (out) memcpy(out, s->canon, sizeof s->canon);
+    s->canon_on = enable;
 }
 
 void orc_last_ray_counts(const orc_scene* s, uint64_t counts[3]) {
@@ -1756,6 +1857,7 @@ void orc_last_ray_counts(const orc_scene* s, uint64_t counts[3]) {
 
 int orc_trace(orc_scene* s, const rtg_ray* rays, int n, rtg_hit* hits) {
     if (!s || (n && (!rays || !hits))) return RTG_ERR_INVALID;
+#pragma omp parallel for schedule(dynamic, 256)
     for (int i = 0; i < n; i++) {
         Ray r = R(V(rays[i].origin[0], rays[i].origin[1], rays[i].origin[2]),
                   V(rays[i].direction[0], rays[i].direction[1], rays[i].direction[2]), rays[i].time);

@@ -36,6 +36,12 @@ int orc_render(orc_scene* s, const rtg_camera_desc* cam, uint64_t seed, int nthr
 /* rays traced by the last orc_render: [0]=primary [1]=secondary [2]=shadow */
 void orc_last_ray_counts(const orc_scene* s, uint64_t counts[3]);
 
+/* SURVEY §8(d) yardstick (not the reference's algorithm): with enable = 1, later orc_render calls
+   also run the canonical ordered early-exit traversal on every ray they trace and count its work.
+   out (the last render's totals, may be NULL): [0] closest-hit rays, [1] 32-byte child records,
+   [2] triangle tests, [3] sphere tests, [4..7] the same for shadow rays (any hit up to the light). */
+void orc_canonical_counts(orc_scene* s, int enable, uint64_t out[8]);
+
 int orc_trace(orc_scene* s, const rtg_ray* rays, int n, rtg_hit* hits);
 int orc_object_bvh(const orc_scene* s, int object, int32_t* num_prims, int32_t* num_nodes,
                    int32_t* perm, int32_t* nodes, float* boxes);

@@ -1832,6 +1832,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
     Stats st = {0, 0, 0};
+    bool was_blocked = false;
     if (j < (int)*scount) {
         const int idx = slist[j];
         const int i = idx / sv.num_lights;      // shading node of the query
@@ -1908,6 +1909,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         } else {
             blocked = h.obj >= 0;               // directional / environment: any hit
         }
+        was_blocked = blocked;
         if (lean3) {
             // lit: the colour k_shade prepared (xyz only; w keeps the node's kind bits);
             // blocked: col + 0 == col (the ambient term is never -0), nothing to store
@@ -1931,11 +1933,16 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     if (nm && (threadIdx.x & 63) == 0) atomicAdd(nan_queries, (unsigned)__popcll(nm));
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
+        unsigned long long bq = was_blocked ? 1ull : 0ull, bs = was_blocked ? st.steps : 0ull,
+                           bt = was_blocked ? st.tris : 0ull;
         unsigned mx = st.steps;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
             ns += __shfl_down(ns, off);
+            bq += __shfl_down(bq, off);
+            bs += __shfl_down(bs, off);
+            bt += __shfl_down(bt, off);
             mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
         }
         if ((threadIdx.x & 63) == 0) {
@@ -1943,6 +1950,9 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             atomicAdd(&ctr->shadow_tri_tests, nt);
             atomicAdd(&ctr->shadow_lane_slots, 64ull * mx);
             atomicAdd(&ctr->shadow_steps, ns);
+            atomicAdd(&ctr->shadow_blocked, bq);
+            atomicAdd(&ctr->shadow_blocked_steps, bs);
+            atomicAdd(&ctr->shadow_blocked_tris, bt);
         }
     }
 }

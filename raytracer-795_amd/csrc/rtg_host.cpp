@@ -1690,21 +1690,42 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         ln.busy = true;
         return enqueue_level(ln);
     };
-    auto finish_pass = [&](Lane& ln) {
+    // collect_timing: one launch between two events, waited for (roofline frames only)
+    auto timed_launch = [&](Lane& ln, auto&& launch, double& ms, int& launches) -> int {
+        if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
+        launch();
+        if (timing) {
+            float a = 0.0f;
+            HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
+            HIP_TRY(hipEventSynchronize(ln.ev_t[1]));
+            HIP_TRY(hipEventElapsedTime(&a, ln.ev_t[0], ln.ev_t[1]));
+            ms += a;
+            launches++;
+        }
+        return RTG_OK;
+    };
+    auto finish_pass = [&](Lane& ln) -> int {
         const PassDev& ps = plist[ln.pass];
         const int level = ln.level;
         stt.max_level = std::max(stt.max_level, level);
+        int rc2;
         // bottom-up: levels level-1 .. 1 here, level 0 inside the accumulation
         for (int l = level - 1; l >= 1 && !pt; l--)
-            launch_resolve(sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(), ln.counts[l],
-                           ln.counts[l + 1],
-                           ln.st);
+            if ((rc2 = timed_launch(ln, [&] {
+                     launch_resolve(sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(),
+                                    ln.counts[l], ln.counts[l + 1], ln.st);
+                 }, stt.resolve_ms, stt.resolve_launches)))
+                return rc2;
         const int mode = (total == 1) ? 2 : (ps.s0 == 0 ? 1 : 0);
         const NodeRec* level1 = level >= 1 ? ln.levels[1].nodes.as<NodeRec>() : nullptr;
-        launch_accumulate(sv, ln.levels[0].nodes.as<NodeRec>(), level1, !pt && level >= 1, s->d_acc.as<float>(), ps,
-                          cam->nx, mode, ln.st, !pt, ln.counts[0], level >= 1 ? ln.counts[1] : 0);
+        if ((rc2 = timed_launch(ln, [&] {
+                 launch_accumulate(sv, ln.levels[0].nodes.as<NodeRec>(), level1, !pt && level >= 1, s->d_acc.as<float>(),
+                                   ps, cam->nx, mode, ln.st, !pt, ln.counts[0], level >= 1 ? ln.counts[1] : 0);
+             }, stt.accumulate_ms, stt.accumulate_launches)))
+            return rc2;
         stt.passes++;
         ln.busy = false;
+        return RTG_OK;
     };
     std::deque<int> waiting;           // lanes with a level in flight, in enqueue order
     // next lane to service: the first (in enqueue order) whose count read-back has landed, so a
@@ -1763,7 +1784,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             waiting.push_back(k);
             continue;
         }
-        finish_pass(ln);
+        if ((rc = finish_pass(ln))) return rc;
         if (ln.next_pass < ln.passes.size()) {
             if ((rc = start_pass(ln))) return rc;
             waiting.push_back(k);
@@ -1797,6 +1818,9 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     stt.shadow_steps = ctr.shadow_steps;
     stt.trace_lane_slots = ctr.trace_lane_slots;
     stt.shadow_lane_slots = ctr.shadow_lane_slots;
+    stt.shadow_blocked = ctr.shadow_blocked;
+    stt.shadow_blocked_steps = ctr.shadow_blocked_steps;
+    stt.shadow_blocked_tris = ctr.shadow_blocked_tris;
     stt.devices = 1;
     s->stats = stt;
     return RTG_OK;

@@ -293,6 +293,9 @@ struct Counters {
     unsigned long long node_visits, tri_tests;           // closest-hit kernel
     unsigned long long shadow_node_visits, shadow_tri_tests;
     unsigned long long trace_lane_slots, shadow_lane_slots, trace_steps, shadow_steps;
+    // shadow queries found blocked, and the node steps / triangle tests they took (the rest of
+    // shadow_steps / shadow_tri_tests went to unblocked queries)
+    unsigned long long shadow_blocked, shadow_blocked_steps, shadow_blocked_tris;
 };
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------

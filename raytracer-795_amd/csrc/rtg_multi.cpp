@@ -43,6 +43,7 @@ struct Rccl {
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
@@ -76,6 +77,7 @@ int load_rccl(const Rccl** out) {
             sym(r.CommDestroy, "ncclCommDestroy");
             sym(r.Send, "ncclSend");
             sym(r.Recv, "ncclRecv");
+            sym(r.AllReduce, "ncclAllReduce");
             sym(r.GroupStart, "ncclGroupStart");
             sym(r.GroupEnd, "ncclGroupEnd");
             sym(r.GetErrorString, "ncclGetErrorString");
@@ -190,6 +192,13 @@ void add_stats(rtg_render_stats& a, const rtg_render_stats& b) {
     a.shadow_steps += b.shadow_steps;
     a.trace_lane_slots += b.trace_lane_slots;
     a.shadow_lane_slots += b.shadow_lane_slots;
+    a.shadow_blocked += b.shadow_blocked;
+    a.shadow_blocked_steps += b.shadow_blocked_steps;
+    a.shadow_blocked_tris += b.shadow_blocked_tris;
+    a.resolve_ms += b.resolve_ms;
+    a.accumulate_ms += b.accumulate_ms;
+    a.resolve_launches += b.resolve_launches;
+    a.accumulate_launches += b.accumulate_launches;
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -296,6 +305,13 @@ int render_multi(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts
         if (n > visible) return set_error(RTG_ERR_NO_DEVICE, "num_devices exceeds the visible devices");
         for (int r = 0; r < n; r++) devs[r] = (dev0 + r) % visible;
     }
+    if (n == 1) {
+        // one device (e.g. rtg_cli --devices 1): the plain single-device render, no RCCL needed
+        rtg_render_opts so = o;
+        so.num_devices = 0;
+        so.devices = nullptr;
+        return scene_render(s, cam, &so, out_dev, st);
+    }
     MultiState*& M = scene_multi(s);
     if (M && M->devs != devs) {
         multi_free(M);
@@ -395,8 +411,28 @@ struct rtg_comm {
     const Rccl* R = nullptr;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1, device = 0;
-    DevBuf part, recv;
+    DevBuf part, recv, flag;
 };
+
+namespace rtg {
+namespace {
+// Every rank learns whether any rank failed before the gather (an allreduce-max of a failure
+// flag), so a rank that fails early cannot leave the others blocked in ncclRecv / ncclSend.
+// Returns the number of failed ranks seen (>= 1 means: do not gather), or < 0 when the
+// agreement itself failed (the communicator is then unusable).
+int agree_failures(rtg_comm* c, bool failed, hipStream_t st, std::string& why) {
+    if (c->flag.grow(c->device, sizeof(int32_t))) { why = "status buffer"; return -1; }
+    const int32_t mine = failed ? 1 : 0;
+    int32_t any = 0;
+    if (hipMemcpyAsync(c->flag.p, &mine, sizeof mine, hipMemcpyHostToDevice, st) != hipSuccess) { why = "status copy"; return -1; }
+    const ncclResult_t e = c->R->AllReduce(c->flag.p, c->flag.p, 1, ncclInt32, ncclSum, c->comm, st);
+    if (e != ncclSuccess) { why = std::string("ncclAllReduce: ") + c->R->GetErrorString(e); return -1; }
+    if (hipMemcpyAsync(&any, c->flag.p, sizeof any, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) { why = "status sync"; return -1; }
+    return any;
+}
+}  // namespace
+}  // namespace rtg
 
 extern "C" {
 
@@ -446,6 +482,7 @@ int32_t rtg_comm_destroy(rtg_comm* c) {
     if (c->comm) (void)c->R->CommDestroy(c->comm);
     c->part.release();
     c->recv.release();
+    c->flag.release();
     delete c;
     return RTG_OK;
 }
@@ -453,25 +490,42 @@ int32_t rtg_comm_destroy(rtg_comm* c) {
 int32_t rtg_render_ranked(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts* opts, rtg_comm* c,
                           float* frame_device, void* stream) {
     return guarded([&]() -> int32_t {
-        if (!s || !cam || !c) return set_error(RTG_ERR_INVALID, "null argument");
-        if (c->rank == 0 && !frame_device) return set_error(RTG_ERR_INVALID, "rank 0 needs the frame buffer");
-        if (scene_device(s) != c->device) return set_error(RTG_ERR_INVALID, "scene and communicator on different devices");
-        if (cam->nx < 1 || cam->ny < 1 || cam->num_samples < 1) return set_error(RTG_ERR_INVALID, "bad camera");
+        if (!c) return set_error(RTG_ERR_INVALID, "null communicator");
+        if (hipSetDevice(c->device) != hipSuccess) return set_error(RTG_ERR_NO_DEVICE, "hipSetDevice");
+        hipStream_t st = (hipStream_t)stream;
+        // Local checks and the shard render record a status instead of returning: every rank
+        // reaches the failure agreement below, whatever happened to it (no rank is left waiting
+        // in the gather for a rank that gave up).
+        int rc = RTG_OK;
         rtg_render_opts o{};
         if (opts) o = *opts;
-        if (o.num_devices > 1 || o.devices) return set_error(RTG_ERR_INVALID, "rtg_render_ranked: one device per rank");
-        if (hipSetDevice(c->device) != hipSuccess) return set_error(RTG_ERR_NO_DEVICE, "hipSetDevice");
-        const int nx = cam->nx, ny = cam->ny, n = c->nranks;
+        if (!s || !cam) rc = set_error(RTG_ERR_INVALID, "null argument");
+        else if (c->rank == 0 && !frame_device) rc = set_error(RTG_ERR_INVALID, "rank 0 needs the frame buffer");
+        else if (scene_device(s) != c->device) rc = set_error(RTG_ERR_INVALID, "scene and communicator on different devices");
+        else if (cam->nx < 1 || cam->ny < 1 || cam->num_samples < 1) rc = set_error(RTG_ERR_INVALID, "bad camera");
+        else if (o.num_devices > 1 || o.devices) rc = set_error(RTG_ERR_INVALID, "rtg_render_ranked: one device per rank");
+        const int n = c->nranks;
         const int block = o.row_block > 1 ? o.row_block : 4;
-        const ShardPrefix pre = shard_prefix(ny, n, block);
-        const size_t rows = (size_t)std::max(pre.rows[c->rank + 1] - pre.rows[c->rank], 1);
-        int rc;
-        if ((rc = c->part.grow(c->device, rows * nx * 3 * sizeof(float)))) return rc;
-        if (c->rank == 0 && (rc = c->recv.grow(c->device, (size_t)ny * nx * 3 * sizeof(float)))) return rc;
+        const int nx = rc == RTG_OK ? cam->nx : 0, ny = rc == RTG_OK ? cam->ny : 0;
         const auto t0 = std::chrono::steady_clock::now();
-        hipStream_t st = (hipStream_t)stream;
-        const rtg_render_opts so = shard_opts(o, c->rank, n, block);
-        if ((rc = scene_render(s, cam, &so, c->part.f(), st))) return rc;
+        if (rc == RTG_OK) {
+            const ShardPrefix pre = shard_prefix(ny, n, block);
+            const size_t rows = (size_t)std::max(pre.rows[c->rank + 1] - pre.rows[c->rank], 1);
+            rc = c->part.grow(c->device, rows * nx * 3 * sizeof(float));
+            if (rc == RTG_OK && c->rank == 0) rc = c->recv.grow(c->device, (size_t)ny * nx * 3 * sizeof(float));
+        }
+        if (rc == RTG_OK) {
+            const rtg_render_opts so = shard_opts(o, c->rank, n, block);
+            rc = scene_render(s, cam, &so, c->part.f(), st);
+        }
+        const std::string local_err = rc == RTG_OK ? std::string() : std::string(rtg_last_error());
+        std::string why;
+        const int failed = agree_failures(c, rc != RTG_OK, st, why);
+        if (failed < 0) return set_error(RTG_ERR_HIP, "rank status agreement: " + why +
+                                                         (rc != RTG_OK ? " (after: " + local_err + ")" : ""));
+        if (rc != RTG_OK) return set_error(rc, local_err);
+        if (failed > 0)
+            return set_error(RTG_ERR_HIP, std::to_string(failed) + " other rank(s) failed before the gather");
         const auto t1 = std::chrono::steady_clock::now();
         if ((rc = gather_rows(*c->R, c->comm, c->rank, n, nx, ny, block, c->part.f(), c->recv.f(), frame_device, st)))
             return rc;

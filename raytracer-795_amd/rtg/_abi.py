@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 5
+RTG_ABI_VERSION = 6
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -119,7 +119,9 @@ class RenderStats(C.Structure):
                 ("trace_steps", C.c_uint64), ("shadow_steps", C.c_uint64),
                 ("trace_lane_slots", C.c_uint64), ("shadow_lane_slots", C.c_uint64),
                 ("shade_ms", C.c_double), ("shade_launches", C.c_int32), ("devices", C.c_int32),
-                ("gather_ms", C.c_double)]
+                ("gather_ms", C.c_double), ("shadow_blocked", C.c_uint64), ("shadow_blocked_steps", C.c_uint64),
+                ("shadow_blocked_tris", C.c_uint64), ("resolve_ms", C.c_double), ("accumulate_ms", C.c_double),
+                ("resolve_launches", C.c_int32), ("accumulate_launches", C.c_int32)]
 
 RTG_COMM_ID_BYTES = 128
 

@@ -1,0 +1,109 @@
+"""Oracle parity at the BASELINE configs' real sizes (VERDICT r2 "What's missing" #1).
+
+* C3 dragon1m, the headline scene at full size (1,000,004 triangles): >= 100 K rays of every
+  kind the render loop traces (fullsize_rays.py) through rtg_trace_closest, bit-exact against
+  orc_trace -- object / primitive / material indices, t, point and normal bits -- on both
+  traversal trees (the SAH 4-wide tree with the reachability gate, and the reference
+  median-split tree), pruned and exhaustive.  Reference semantics: BVH::FindIntersectionWithBVH
+  (src/BVH.cpp:137-210) inside BVHMethods::FindIntersection (src/Helper.cpp:18-80).
+* 1920x1080 row bands of the bench frames against the oracle's rows of the same frame:
+  dragon1m 64 spp (16 rows through the glass and mirror spheres), cornell_dynamic 64 spp (C4)
+  and cornell_pt 256 spp (C5).  The oracle renders only the band (row_begin / row_end);
+  the GPU renders the whole frame exactly as bench.py does.
+"""
+import numpy as np
+import pytest
+
+import fullsize_rays
+import pyoracle
+import rtg
+from rtg import scenegen
+
+pytestmark = pytest.mark.gpu
+
+SAH, REF_TREE = 0, 1
+BAND = (800, 816)       # rows 800..815: glass sphere, mirror sphere, dragon, floor (C3)
+
+
+def _bits(a):
+    return np.nan_to_num(np.ascontiguousarray(a, np.float32)).view(np.int32)
+
+
+def _cmp(img, ref):
+    d = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    nanm = int(np.sum(np.isnan(img) != np.isnan(ref)))
+    d = np.where(np.isnan(d), 0.0, d)
+    return float(d.max()), int((_bits(img) != _bits(ref)).sum()), nanm
+
+
+@pytest.fixture(scope="module")
+def dragon():
+    sc = scenegen.dragon1m(1920, 1080, spp=64)
+    assert sc.num_triangles() == 1_000_004
+    return sc, pyoracle.Oracle(sc)
+
+
+@pytest.fixture(scope="module")
+def dragon_rays(dragon):
+    sc, orc = dragon
+    sets = fullsize_rays.build(sc, orc)
+    o = np.concatenate([v[0] for v in sets.values()])
+    d = np.concatenate([v[1] for v in sets.values()])
+    kinds = np.concatenate([np.full(len(v[0]), i) for i, v in enumerate(sets.values())])
+    t = np.zeros(len(o), np.float32)
+    return list(sets), o, d, t, kinds, orc.trace(o, d, t)
+
+
+def _assert_hits_equal(h, ref, kinds, names, tag):
+    for key in ("full", "object", "prim", "material"):
+        bad = h[key] != ref[key]
+        assert not bad.any(), f"{tag}: {key} differs on {int(bad.sum())} rays, kinds {sorted({names[k] for k in kinds[bad]})}"
+    m = ref["full"] == 1
+    for key in ("t", "point", "normal"):
+        a, b = h[key][m].view(np.int32), ref[key][m].view(np.int32)
+        bad = (a != b).reshape(len(a), -1).any(1)
+        assert not bad.any(), f"{tag}: {key} bits differ on {int(bad.sum())} rays"
+
+
+def test_dragon1m_rays_bit_exact_both_trees(gpu, dragon, dragon_rays):
+    sc, _ = dragon
+    names, o, d, t, kinds, ref = dragon_rays
+    assert len(o) >= 100_000
+    counts = {names[k]: int((kinds == k).sum()) for k in range(len(names))}
+    print(f"{len(o)} rays {counts}, oracle hits {int(ref['full'].sum())}")
+    for tree in (SAH, REF_TREE):
+        with rtg.Renderer(sc, device=gpu, traversal_tree=tree) as r:
+            for trav in (0, 1):
+                h = r.trace(o, d, t, traversal=trav)
+                _assert_hits_equal(h, ref, kinds, names, f"tree={tree} traversal={trav}")
+
+
+def test_dragon1m_1080p64_band_bit_exact(gpu, dragon):
+    """The bench frame (C3, 1920x1080x64, Whitted depth 6), rows 800..815 against the oracle."""
+    sc, orc = dragon
+    ref, obj, _, _ = orc.render(0, row_begin=BAND[0], row_end=BAND[1])
+    band = slice(*BAND)
+    assert (obj[band] == 1).any() and (obj[band] == 0).any() and (obj[band] == 3).any()
+    for tree in (SAH, REF_TREE):
+        with rtg.Renderer(sc, device=gpu, traversal_tree=tree) as r:
+            img = r.render(0)
+        linf, ndiff, nanm = _cmp(img[band], ref[band])
+        print(f"dragon1m 1080p64 rows {BAND} tree={tree}: Linf={linf:.3g} differing={ndiff} nan_mismatch={nanm}")
+        assert nanm == 0 and ndiff == 0, f"tree={tree}"
+
+
+@pytest.mark.parametrize("name,spp", [("cornell", 64), ("cornell_pt", 256)])
+def test_cornell_1080p_band_matches_oracle(gpu, name, spp):
+    """C4 (distribution ray tracing: DoF, motion blur, area light, rough mirror, instances) and
+    C5 (hw7 path tracer) at the bench resolution and spp, 16 rows against the oracle."""
+    sc = getattr(scenegen, name)(1920, 1080, spp=spp)
+    orc = pyoracle.Oracle(sc)
+    ref = orc.render(0, row_begin=BAND[0], row_end=BAND[1])[0]
+    with rtg.Renderer(sc, device=gpu) as r:
+        img = r.render(0)
+    band = slice(*BAND)
+    linf, ndiff, nanm = _cmp(img[band], ref[band])
+    print(f"{name} 1080p{spp} rows {BAND}: Linf={linf:.3g} differing={ndiff} nan_mismatch={nanm}")
+    assert nanm == 0
+    assert linf < 1e-3
+    assert ndiff == 0
