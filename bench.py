@@ -276,6 +276,10 @@ def main():
     ap.add_argument("--tlas", choices=["auto", "off", "on"], default="auto",
                     help="top-level BVH over objects / instances (rtg_build_opts.tlas; auto: from 16 entries)")
     args = ap.parse_args()
+    # stdout carries exactly the one JSON line: libraries that print banners there (RCCL's
+    # "RCCL version ..." at communicator init) are sent to stderr with everything else
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     import torch
 
@@ -460,7 +464,7 @@ def main():
                 "roofline": roof, "cpu_baseline": cpu, "parity": parity, "multi": multi}
         if cpu_note:
             line["cpu_baseline_note"] = cpu_note
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if comm is not None:
         comm.close()
     r.close()
