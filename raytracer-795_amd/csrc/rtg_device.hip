@@ -278,20 +278,34 @@ struct Stats { unsigned nodes, tris, steps; };
 // an accepted hit at t <= nearest skipped) instead of the reference's linear loop; an entry
 // replaces the winner iff t < nearest, or t == nearest and it comes earlier in the loop order
 // (objects before instances, lower index first), which is the loop's first-wins rule.
-template <bool EXHAUSTIVE, bool STATS, bool TLAS = false>
+//
+// CERT (shadow queries, linear object loop): certified early exit.  The caller's decision depends
+// only on the final nearest accepted t (src/Light.cpp:188-204 via src/Helper.cpp:39-49), and every
+// accepted t in (0, tcert] gives "blocked".  Inside an object the reference's winner is the
+// minimal-distance reachable candidate, and it is accepted only if its gett() is > 0: a
+// candidate within eps behind the origin can hide nearer-in-front hits (src/Shape.cpp:330 +
+// src/Helper.cpp:41).  So once the object's best candidate so far has gett() in (0, tcert] AND
+// no unexplored subtree can hold a candidate with t <= tau (every remaining subtree's entry key
+// is > tau, where tau bounds gett()'s rounding so that t > tau implies gett() > 0), the object's
+// winner -- the best so far or a nearer unexplored candidate, both with 0 < t <= tcert -- is
+// accepted and the query is blocked, whatever the remaining objects hold.  Stack entries whose
+// key is <= tau carry the sign bit; `nflag` counts them.  out.pad = 1 marks a certified result.
+template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool CERT = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
-                       short* tstack = nullptr) {
+                       short* tstack = nullptr, float tcert = -INFINITY) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
     float nearest = tmax;
     const float eps = sv.int_eps;
+    bool certified = false;
     auto visit = [&](const int i) {
         const TopObject& T = sv.tops[i];
         const Geometry& g = sv.geoms[T.geom];
         f3 o2, d2;
         transform_ray(T, o, d, time, o2, d2);
         bool found = false;
+        bool cert_exit = false;     // CERT: the walk stopped once its winner was certified
         int bprim = -1;
         f3 bp = mk(0, 0, 0);
         if (g.type == RTG_OBJ_SPHERE) {
@@ -439,6 +453,12 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 // walk; candidates already accepted stay valid (they are reachable).
                 bool use2 = EXHAUSTIVE || !fast || g.sah_base < 0;
                 if (!use2) {
+                    // CERT: tau bounds gett()'s rounding (4u |o_a| / |d_a|, as the object-loop bound
+                    // above) with a 4x margin: a candidate with t > tau has gett() > 0
+                    const bool cert_on = CERT && tcert > 0.0f;
+                    const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : 0.0f;
+                    bool best_cert = false;   // the best candidate so far has gett() in (0, tcert]
+                    int nflag = 0;            // stack entries whose key is <= tau (sign bit set)
                     auto test_sah = [&](const TriGeom& tg) {
                         if (STATS) st.tris++;
                         Cand c = tri_test(tg, o2, d2, eps);
@@ -454,6 +474,10 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         }
                         best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
                         if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+                        if (cert_on) {
+                            const float tg_ = gett(o2, d2, c.p);
+                            best_cert = tg_ > 0 && tg_ * (1.0f + 2e-5f) <= tcert;
+                        }
                     };
                     int sp = 0;
                     int cur = g.sah_base;
@@ -517,6 +541,29 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
                         const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
                         if (sp + npush > kStackDepth) { use2 = true; break; }
+                        if (cert_on) {
+                            // flagged pushes: subtrees that may hold a candidate with t <= tau
+#pragma unroll
+                            for (int j = 3; j >= 1; j--)
+                                if (r4[j] >= 0) {
+                                    const bool fl = !(k4[j] > tau);
+                                    nflag += fl;
+                                    stack[sp * sstride] = r4[j] | (fl ? (int)0x80000000u : 0);
+                                    sp++;
+                                }
+                            if (r4[0] >= 0) {
+                                if (best_cert && nflag == 0 && k4[0] > tau) { cert_exit = true; break; }
+                                cur = r4[0];
+                            } else {
+                                if (best_cert && nflag == 0) { cert_exit = true; break; }
+                                if (sp == 0) break;
+                                sp--;
+                                const int e = stack[sp * sstride];
+                                nflag -= e < 0;
+                                cur = e & 0x7fffffff;
+                            }
+                            continue;
+                        }
                         if (r4[3] >= 0) { stack[sp * sstride] = r4[3]; sp++; }
                         if (r4[2] >= 0) { stack[sp * sstride] = r4[2]; sp++; }
                         if (r4[1] >= 0) { stack[sp * sstride] = r4[1]; sp++; }
@@ -538,12 +585,21 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 nearest = t;
                 out.obj = i; out.prim = bprim; out.t = t;
             }
+            // a sphere's single candidate is its winner; a mesh walk that stopped early (cert_exit)
+            // proved its winner lies in (0, t]
+            if (CERT && (cert_exit || g.type == RTG_OBJ_SPHERE) && t > 0 && t * (1.0f + 2e-5f) <= tcert) {
+                certified = true;
+                out.obj = i; out.prim = bprim; out.t = t; out.pad = 1;
+            }
         }
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
     if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {   // wfast is per lane: the others walk on
-        for (int i = 0; i < sv.num_tops; i++) visit(i);
+        for (int i = 0; i < sv.num_tops; i++) {
+            visit(i);
+            if (CERT && certified) break;
+        }
         return out;
     }
     // top-level walk.  A child box is skipped when the ray line misses it (its entries' hit points
@@ -1866,15 +1922,48 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             tmax = sd.w;
         }
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x,
-                                                        kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0));
         auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
         // the query's mode is re-read rather than kept live across the traversal
         // (register pressure: 128 VGPRs for 4 waves per SIMD)
-        const float mode = lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f)
-                                 : ld(reinterpret_cast<const float*>(shadows.c + idx) + 3);
+        auto query_mode = [&]() {
+            return lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f)
+                         : ld(reinterpret_cast<const float*>(shadows.c + idx) + 3);
+        };
+        // Certified early exit (closest_hit CERT): every accepted t in (0, tcert] blocks.  With
+        // hp = o + d t, |p - hp| <= |o - p| + t |d| (|d| = 1 up to rounding), so the distance test
+        // |p - L| > |p - hp| (mode 1) or |p - hp| < dl - (eps + 1e-4 dl) (mode 3) holds for every
+        // t <= tcert below, margins (1e-5 relative) far above the rounding of both sides;
+        // directional / environment queries (mode 2) are blocked by any accepted hit.
+        float tcert = -INFINITY;
+        if (!EXHAUSTIVE && !TLAS) {
+            const float m0 = query_mode();
+            if (m0 == 2.0f) {
+                tcert = INFINITY;
+            } else if (m0 == 1.0f || m0 == 3.0f) {
+                f3 pq, lq;
+                const float4 pf = nodes.pnt[i];
+                pq = mk(pf.x, pf.y, pf.z);
+                if (lean) {
+                    lq = ld3(sv.lights[0].pos);
+                } else {
+                    const float4 lf = shadows.L[idx];
+                    lq = mk(lf.x, lf.y, lf.z);
+                }
+                const float dl = norm(pq - lq);
+                const float lim = m0 == 1.0f ? dl : dl - (sv.shadow_eps + 1e-4f * dl);
+                const float op = norm(o - pq);
+                const float tc = (lim * (1.0f - 1e-5f) - op * (1.0f + 1e-5f) - 1e-6f * (op + dl)) * (1.0f - 1e-5f);
+                if (tc > 0.0f) tcert = tc;
+            }
+        }
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, !EXHAUSTIVE && !TLAS>(
+            sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
+            s_tstack + (TLAS ? threadIdx.x : 0), tcert);
+        const float mode = query_mode();
         bool blocked;
-        if (mode == 1.0f || mode == 3.0f) {
+        if (h.pad == 1) {
+            blocked = true;                     // certified by the early exit
+        } else if (mode == 1.0f || mode == 3.0f) {
             blocked = false;
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
