@@ -19,6 +19,10 @@ namespace rtg {
 #define DEV __device__ __forceinline__
 // k_shadow: 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+// k_shadow's certified early exit (closest_hit CERT); 0 builds the plain closest-hit query (A/B)
+#ifndef RTG_SHADOW_CERT
+#define RTG_SHADOW_CERT 1
+#endif
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
 // 34.0 -> 29.7 ms); the simple variants already fit 4 waves (no-op for them)
@@ -456,7 +460,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     // CERT: tau bounds gett()'s rounding (4u |o_a| / |d_a|, as the object-loop bound
                     // above) with a 4x margin: a candidate with t > tau has gett() > 0
                     const bool cert_on = CERT && tcert > 0.0f;
-                    const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : 0.0f;
+                    const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : -INFINITY;
                     bool best_cert = false;   // the best candidate so far has gett() in (0, tcert]
                     int nflag = 0;            // stack entries whose key is <= tau (sign bit set)
                     auto test_sah = [&](const TriGeom& tg) {
@@ -541,38 +545,30 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
                         const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
                         if (sp + npush > kStackDepth) { use2 = true; break; }
-                        if (cert_on) {
-                            // flagged pushes: subtrees that may hold a candidate with t <= tau
-#pragma unroll
-                            for (int j = 3; j >= 1; j--)
-                                if (r4[j] >= 0) {
-                                    const bool fl = !(k4[j] > tau);
-                                    nflag += fl;
-                                    stack[sp * sstride] = r4[j] | (fl ? (int)0x80000000u : 0);
-                                    sp++;
-                                }
-                            if (r4[0] >= 0) {
-                                if (best_cert && nflag == 0 && k4[0] > tau) { cert_exit = true; break; }
-                                cur = r4[0];
-                            } else {
-                                if (best_cert && nflag == 0) { cert_exit = true; break; }
-                                if (sp == 0) break;
-                                sp--;
-                                const int e = stack[sp * sstride];
-                                nflag -= e < 0;
-                                cur = e & 0x7fffffff;
+                        // CERT: pushes of subtrees that may hold a candidate with t <= tau carry the
+                        // sign bit (tau = -inf when certification is off: no flags)
+                        auto push = [&](int j) {
+                            if (r4[j] < 0) return;
+                            int e = r4[j];
+                            if (CERT) {
+                                const bool fl = !(k4[j] > tau);
+                                nflag += fl;
+                                e |= fl ? (int)0x80000000u : 0;
                             }
-                            continue;
-                        }
-                        if (r4[3] >= 0) { stack[sp * sstride] = r4[3]; sp++; }
-                        if (r4[2] >= 0) { stack[sp * sstride] = r4[2]; sp++; }
-                        if (r4[1] >= 0) { stack[sp * sstride] = r4[1]; sp++; }
+                            stack[sp * sstride] = e;
+                            sp++;
+                        };
+                        push(3); push(2); push(1);
                         if (r4[0] >= 0) {
+                            if (CERT && best_cert && nflag == 0 && k4[0] > tau) { cert_exit = true; break; }
                             cur = r4[0];
                         } else {
+                            if (CERT && best_cert && nflag == 0) { cert_exit = true; break; }
                             if (sp == 0) break;
                             sp--;
-                            cur = stack[sp * sstride];
+                            const int e = stack[sp * sstride];
+                            if (CERT) nflag -= e < 0;
+                            cur = CERT ? (e & 0x7fffffff) : e;
                         }
                     }
                 }
@@ -1935,7 +1931,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         // t <= tcert below, margins (1e-5 relative) far above the rounding of both sides;
         // directional / environment queries (mode 2) are blocked by any accepted hit.
         float tcert = -INFINITY;
-        if (!EXHAUSTIVE && !TLAS) {
+        if (RTG_SHADOW_CERT && !EXHAUSTIVE && !TLAS) {
             const float m0 = query_mode();
             if (m0 == 2.0f) {
                 tcert = INFINITY;
@@ -1956,7 +1952,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 if (tc > 0.0f) tcert = tc;
             }
         }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, !EXHAUSTIVE && !TLAS>(
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, RTG_SHADOW_CERT && !EXHAUSTIVE && !TLAS>(
             sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
             s_tstack + (TLAS ? threadIdx.x : 0), tcert);
         const float mode = query_mode();

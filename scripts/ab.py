@@ -13,8 +13,17 @@ ms = []
 for _ in range(int(os.environ.get("AB_FRAMES", "5"))):
     r.render(0)
     ms.append(r.stats()["render_ms"])
+r.render(0, collect_stats=1)
+ss = r.stats()
+r.render(0, collect_timing=1, streams=1)
 r.render(0, collect_timing=1, streams=1)
 st = r.stats()
 print(json.dumps({"lib": os.environ.get("RTG_LIBRARY", "librtg"), "workload": w, "frame_ms": round(statistics.median(ms), 2),
                   "frames": [round(x, 2) for x in ms], "trace_ms": round(st["trace_ms"], 2),
-                  "shadow_ms": round(st["shadow_ms"], 2), "streams1_ms": round(st["render_ms"], 2)}), flush=True)
+                  "shadow_ms": round(st["shadow_ms"], 2), "shade_ms": round(st["shade_ms"], 2),
+                  "streams1_ms": round(st["render_ms"], 2),
+                  "trace_steps_per_ray": round(ss["trace_steps"] / max(ss["primary_rays"] + ss["secondary_rays"], 1), 3),
+                  "shadow_steps_per_query": round(ss["shadow_steps"] / max(ss["shadow_rays"], 1), 3),
+                  "shadow_blocked_steps": round(ss["shadow_blocked_steps"] / max(ss["shadow_blocked"], 1), 3),
+                  "trace_simd_eff": round(ss["trace_steps"] / max(ss["trace_lane_slots"], 1), 4),
+                  "shadow_simd_eff": round(ss["shadow_steps"] / max(ss["shadow_lane_slots"], 1), 4)}), flush=True)
