@@ -309,7 +309,6 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         f3 o2, d2;
         transform_ray(T, o, d, time, o2, d2);
         bool found = false;
-        bool cert_exit = false;     // CERT: the walk stopped once its winner was certified
         int bprim = -1;
         f3 bp = mk(0, 0, 0);
         if (g.type == RTG_OBJ_SPHERE) {
@@ -461,7 +460,9 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     // above) with a 4x margin: a candidate with t > tau has gett() > 0
                     const bool cert_on = CERT && tcert > 0.0f;
                     const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : -INFINITY;
-                    bool best_cert = false;   // the best candidate so far has gett() in (0, tcert]
+                    // > 0: the best candidate so far has gett() in (0, tcert] (a float, not a lane
+                    // mask: SGPRs are the scarce register file of this loop)
+                    float best_cert = -1.0f;
                     int nflag = 0;            // stack entries whose key is <= tau (sign bit set)
                     auto test_sah = [&](const TriGeom& tg) {
                         if (STATS) st.tris++;
@@ -478,9 +479,11 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         }
                         best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
                         if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                        if (cert_on) {
-                            const float tg_ = gett(o2, d2, c.p);
-                            best_cert = tg_ > 0 && tg_ * (1.0f + 2e-5f) <= tcert;
+                        if (CERT) {
+                            // gett() of a fast ray is its first quotient (d2.x finite, nonzero); a NaN
+                            // compares false (not certified)
+                            const float tg_ = (c.p.x - o2.x) / d2.x;
+                            best_cert = (tg_ > 0 && tg_ * (1.0f + 2e-5f) <= tcert) ? 1.0f : -1.0f;
                         }
                     };
                     int sp = 0;
@@ -560,10 +563,10 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                         };
                         push(3); push(2); push(1);
                         if (r4[0] >= 0) {
-                            if (CERT && best_cert && nflag == 0 && k4[0] > tau) { cert_exit = true; break; }
+                            if (CERT && best_cert > 0.0f && nflag == 0 && k4[0] > tau) break;
                             cur = r4[0];
                         } else {
-                            if (CERT && best_cert && nflag == 0) { cert_exit = true; break; }
+                            if (CERT && best_cert > 0.0f && nflag == 0) break;
                             if (sp == 0) break;
                             sp--;
                             const int e = stack[sp * sstride];
@@ -581,9 +584,9 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 nearest = t;
                 out.obj = i; out.prim = bprim; out.t = t;
             }
-            // a sphere's single candidate is its winner; a mesh walk that stopped early (cert_exit)
-            // proved its winner lies in (0, t]
-            if (CERT && (cert_exit || g.type == RTG_OBJ_SPHERE) && t > 0 && t * (1.0f + 2e-5f) <= tcert) {
+            // the object's winner is this candidate (a complete walk, a sphere) or, after the walk's
+            // early exit, lies in (0, t]: either way the final nearest t is in (0, tcert]
+            if (CERT && t > 0 && t * (1.0f + 2e-5f) <= tcert) {
                 certified = true;
                 out.obj = i; out.prim = bprim; out.t = t; out.pad = 1;
             }
