@@ -19,9 +19,13 @@ namespace rtg {
 #define DEV __device__ __forceinline__
 // k_shadow: 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
-// k_shadow's certified early exit (closest_hit CERT); 0 builds the plain closest-hit query (A/B)
+// k_shadow's certified early exit (closest_hit CERT), off by default: measured on the 1080p64
+// dragon (round 3, scripts/gpu_ab3.sh, same box) it cuts a blocked query's node steps 18.9 ->
+// 14.4 (all queries 8.81 -> 7.93) but k_shadow takes 12.9 instead of 12.4 ms per frame -- the
+// flag bookkeeping costs more per step than the steps it saves.  -DRTG_SHADOW_CERT=1
+// builds it (bit-identical frames: tests/test_gpu_parity.py, test_gpu_fullsize.py).
 #ifndef RTG_SHADOW_CERT
-#define RTG_SHADOW_CERT 1
+#define RTG_SHADOW_CERT 0
 #endif
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
