@@ -268,7 +268,8 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="0 = the workload's spp (64; cornell_pt 256)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="dragon1m",
                     help="dragon1m = the BASELINE metric line (C3); the others are the configs' own scenes")
-    ap.add_argument("--cpu-rows", type=int, default=540)
+    ap.add_argument("--cpu-rows", type=int, default=0,
+                    help="rows of the CPU baseline sample (0: about 10-30 s of CPU work for the workload)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--ranked", action="store_true",
@@ -305,6 +306,8 @@ def main():
 
     t0 = time.perf_counter()
     make, spp_default, wl_text, data_text = WORKLOADS[args.workload]
+    if args.cpu_rows <= 0:
+        args.cpu_rows = {"cornell_pt": 96, "spheres": 32}.get(args.workload, 540)
     scene = getattr(scenegen, make)(args.width, args.height, spp=args.spp or spp_default)
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
     torch.cuda.synchronize()

@@ -3,7 +3,8 @@
 #   <tag>_bench.json            the bench.py line
 #   <tag>_kernel_stats.{csv,txt} rocprofv3 --kernel-trace --stats of bench.py (RTG_STREAMS=1)
 #   <tag>_counters.csv          per-kernel PMC counters (dispatches, sum, per-dispatch mean)
-#   counters_current.json       the per-dispatch means bench.py's rooflines divide by live launch times
+#   counters_<workload>.json    the per-dispatch means bench.py's rooflines divide by live launch times
+#                               (counters_current.json: the same for the headline workload, dragon1m)
 set -e
 TAG=$1
 WL=${2:-dragon1m}
@@ -26,5 +27,6 @@ for pre in ('rtg::k_trace<false, false', 'rtg::k_shade<false, false, 512, false'
 PY
 cp $D/kt/kt_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
 python3 scripts/pmc_counters.py $D profiles/${TAG}_counters.csv profiles/${TAG}_counters.json $WL
-cp profiles/${TAG}_counters.json profiles/counters_current.json
+cp profiles/${TAG}_counters.json profiles/counters_${WL}.json
+[ "$WL" = dragon1m ] && cp profiles/${TAG}_counters.json profiles/counters_current.json
 echo saved $TAG
