@@ -291,16 +291,18 @@ struct Stats { unsigned nodes, tris, steps; };
 // only on the final nearest accepted t (src/Light.cpp:188-204 via src/Helper.cpp:39-49), and every
 // accepted t in (0, tcert] gives "blocked".  Inside an object the reference's winner is the
 // minimal-distance reachable candidate, and it is accepted only if its gett() is > 0: a
-// candidate within eps behind the origin can hide nearer-in-front hits (src/Shape.cpp:330 +
-// src/Helper.cpp:41).  So once the object's best candidate so far has gett() in (0, tcert] AND
+// candidate within eps behind the origin can hide nearer-in-front hits (the t >= -eps acceptance,
+// src/Shape.cpp:330, and the top-level t > 0 test, src/Helper.cpp:41).  So once the object's best candidate so far has gett() in (0, tcert] AND
 // no unexplored subtree can hold a candidate with t <= tau (every remaining subtree's entry key
 // is > tau, where tau bounds gett()'s rounding so that t > tau implies gett() > 0), the object's
 // winner -- the best so far or a nearer unexplored candidate, both with 0 < t <= tcert -- is
 // accepted and the query is blocked, whatever the remaining objects hold.  Stack entries whose
 // key is <= tau carry the sign bit; `nflag` counts them.  out.pad = 1 marks a certified result.
+// bary (optional): the winner's object-space ray parameter and barycentrics (render-path hit records).
+struct HitBary { float pt, beta, gamma; };
 template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool CERT = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
-                       short* tstack = nullptr, float tcert = -INFINITY) {
+                       short* tstack = nullptr, float tcert = -INFINITY, HitBary* bary = nullptr) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
@@ -315,6 +317,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         bool found = false;
         int bprim = -1;
         f3 bp = mk(0, 0, 0);
+        float bt = 0.0f, bb = 0.0f, bg = 0.0f;    // mesh winner: ray parameter, beta, gamma (bp = o2 + d2 bt)
         if (g.type == RTG_OBJ_SPHERE) {
             if (g.nprims > 0) {
                 f3 ip;
@@ -370,7 +373,8 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     float dist = norm(c.p - o2);
                     if (dist < FLT_MAX &&
                         (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
-                        best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                        best_d = dist; best_leaf = start; bprim = k; found = true;
+                        bt = c.t; bb = c.beta; bg = c.gamma;
                         if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                     }
                 }
@@ -481,7 +485,8 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                             const float* gb = sv.gates + 6 * (size_t)k;
                             if (!box_hit(o2, d2, inv, fast, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) return;
                         }
-                        best_d = dist; best_leaf = start; bprim = k; bp = c.p; found = true;
+                        best_d = dist; best_leaf = start; bprim = k; found = true;
+                        bt = c.t; bb = c.beta; bg = c.gamma;
                         if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                         if (CERT) {
                             // gett() of a fast ray is its first quotient (d2.x finite, nonzero); a NaN
@@ -581,12 +586,14 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 }
                 if (use2) walk2();
             }
+            bp = o2 + d2 * bt;          // the candidate's point, as tri_test formed it
         }
         if (found) {
             float t = gett(o2, d2, bp);
             if (t > 0 && (t < nearest || (t == nearest && i < out.obj))) {   // src/Helper.cpp:43, 64
                 nearest = t;
                 out.obj = i; out.prim = bprim; out.t = t;
+                if (bary) { bary->pt = bt; bary->beta = bb; bary->gamma = bg; }
             }
             // the object's winner is this candidate (a complete walk, a sphere) or, after the walk's
             // early exit, lies in (0, t]: either way the final nearest t is in (0, tcert]
@@ -886,8 +893,12 @@ DEV void triangle_texture(const SceneView& sv, const Geometry& g, int4 vi, f3 e1
 // object-space intersection (identical arithmetic), texturing, then the top-level
 // world point and TransformNormal (src/Helper.cpp:39-77).
 // FULL = false: the scene has no textures (the host checks), so texturing is compiled out.
-template <bool FULL = true>
-DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h) {
+// STORED: the render path -- the winner's ray parameter pt and barycentrics come from k_trace's
+// hit record (HitPlanes), so the point o2 + d2 pt and the normal are rebuilt without re-running the
+// test (identical operands and operations, so identical bits).
+template <bool FULL = true, bool STORED = false>
+DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h, float pt = 0.0f, float beta = 0.0f,
+                   float gamma = 0.0f) {
     const TopObject& T = sv.tops[h.obj];
     const Geometry& g = sv.geoms[T.geom];
     f3 o2, d2;
@@ -905,10 +916,18 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h)
         ret.normal = pc / norm(pc);
         if (FULL) sphere_texture(sv, g, ret);
     } else {
-        const TriGeom tg = sv.tris[h.prim];
-        Cand c = tri_test(tg, o2, d2, sv.int_eps);
         int4 vi = sv.prim_idx[h.prim];
-        f3 a = mk(tg.p0.x, tg.p0.y, tg.p0.z);
+        Cand c;
+        f3 a;
+        if (STORED) {
+            c.beta = beta; c.gamma = gamma; c.t = pt;
+            c.p = o2 + d2 * pt;
+            a = ld3(sv.vertices + 3 * (vi.x - 1));
+        } else {
+            const TriGeom tg = sv.tris[h.prim];
+            c = tri_test(tg, o2, d2, sv.int_eps);
+            a = mk(tg.p0.x, tg.p0.y, tg.p0.z);
+        }
         f3 b = ld3(sv.vertices + 3 * (vi.y - 1)), cc = ld3(sv.vertices + 3 * (vi.z - 1));
         f3 normal;
         if (vi.w) {
@@ -1298,17 +1317,21 @@ DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int
     o_out = o; d_out = d; time_out = time;
 }
 
-// Render-path hit records: k_shade / k_pt_shade rebuild the hit from (object, primitive) alone
-// (hit_record re-runs the winning test), so the wavefront stores 8 bytes per ray, not the
-// 16-byte HitRec the rtg_trace_closest path returns.
-DEV void store_hit_compact(HitRec* hits, int i, const HitRec& h) {
-    reinterpret_cast<int2*>(hits)[i] = make_int2(h.obj, h.prim);
-}
-DEV HitRec load_hit_compact(const HitRec* hits, int i) {
-    const int2 v = reinterpret_cast<const int2*>(hits)[i];
-    HitRec h;
-    h.obj = v.x; h.prim = v.y; h.t = 0.0f; h.pad = 0;
-    return h;
+// Render-path hit records (HitPlanes): k_shade / k_pt_shade rebuild the hit from (object,
+// primitive, ray parameter[, barycentrics]) -- 12 or 20 bytes per ray instead of the 16-byte HitRec
+// of the rtg_trace_closest path plus a 48-byte TriGeom re-read.
+struct HitIn { HitRec h; float pt, beta, gamma; };
+DEV HitIn load_hit_planes(const SceneView& sv, const HitRec* hits, int n, int i) {
+    const HitPlanes hp = hit_planes(const_cast<HitRec*>(hits), n);
+    const int2 v = hp.id[i];
+    HitIn r;
+    r.h.obj = v.x; r.h.prim = v.y; r.h.t = 0.0f; r.h.pad = 0;
+    r.pt = 0.0f; r.beta = 0.0f; r.gamma = 0.0f;
+    if (v.x >= 0) {
+        r.pt = hp.pt[i];
+        if (sv.bary) { const float2 bg = hp.bg[i]; r.beta = bg.x; r.gamma = bg.y; }
+    }
+    return r;
 }
 
 // Queued ray i (RayQ planes).
@@ -1345,10 +1368,17 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
             load_ray(rays, i, o, d, time);
             tmax = FLT_MAX;
         }
+        HitBary hb = {0.0f, 0.0f, 0.0f};
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st,
-                                                        s_tstack + (TLAS ? threadIdx.x : 0));
-        if (compact) store_hit_compact(hits, i, h);
-        else hits[i] = h;
+                                                        s_tstack + (TLAS ? threadIdx.x : 0), -INFINITY, &hb);
+        if (compact) {
+            const HitPlanes hp = hit_planes(hits, n);
+            hp.id[i] = make_int2(h.obj, h.prim);
+            hp.pt[i] = hb.pt;
+            if (sv.bary) hp.bg[i] = make_float2(hb.beta, hb.gamma);
+        } else {
+            hits[i] = h;
+        }
     }
     if (STATS) {
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
@@ -1402,9 +1432,11 @@ DEV void mirror_ray(const SceneView& sv, f3 dir, const Ret& ret, const MaterialD
 // with i >= n only take part in the compaction.  h / o / d / time / mt: the traced ray and its hit.
 template <bool FULL, bool SPOT, int BLOCK, bool TEX>
 DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, int i,
-                   int n, const HitRec& h, const f3 o, const f3 d, const float time, const RayMeta& mt,
+                   int n, const HitIn& hin, const f3 o, const f3 d, const float time, const RayMeta& mt,
                    const NodePlanes& nodes, const ShadowPlanes& shadows, int* __restrict__ slist,
-                   const RayQ& next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount) {
+                   const RayQ& next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount,
+                   int* __restrict__ rlist, unsigned* rcount) {
+    const HitRec& h = hin.h;
     int nchild = 0;
     QRay c0r, c1r;
     RayMeta c0m, c1m;
@@ -1434,7 +1466,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
             }
         } else {
             hit = true;
-            Ret ret = hit_record<FULL && TEX>(sv, o, d, time, h);
+            Ret ret = hit_record<FULL && TEX, true>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading Scene.cpp:230-241
@@ -1536,26 +1568,31 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
     // totals combined in LDS, ONE 64-bit atomic per block on the level's queue counter
     // (low word: rays, high word: shadow entries).  Same-address atomics serialise at the L2
     // (~11 ns each), so they are kept to one per block.
-    __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64];
+    __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64], s_wr[BLOCK / 64];
     __shared__ unsigned long long s_base;
+    __shared__ unsigned s_rbase;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long lt = __lanemask_lt();
     const unsigned long long m1 = __ballot(nchild >= 1), m2 = __ballot(nchild >= 2);
     const unsigned coff = __popcll(m1 & lt) + __popcll(m2 & lt);
+    // non-final nodes of levels >= 1: the list k_resolve walks (level 0 resolves in k_accumulate)
+    const unsigned long long mr = __ballot(level > 0 && i < n && (nd.kind & 0xFF) != NK_FINAL);
     unsigned stot = 0;
     for (int li = 0; li < sv.num_lights; li++) stot += __popcll(__ballot((smask >> li) & 1ull));
-    if (lane == 0) { s_wc[w] = __popcll(m1) + __popcll(m2); s_ws[w] = stot; }
+    if (lane == 0) { s_wc[w] = __popcll(m1) + __popcll(m2); s_ws[w] = stot; s_wr[w] = __popcll(mr); }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned c = 0, sh = 0;
+        unsigned c = 0, sh = 0, rr = 0;
         for (int k = 0; k < BLOCK / 64; k++) {
-            const unsigned a = s_wc[k], b = s_ws[k];
-            s_wc[k] = c; s_ws[k] = sh;
-            c += a; sh += b;
+            const unsigned a = s_wc[k], b = s_ws[k], e = s_wr[k];
+            s_wc[k] = c; s_ws[k] = sh; s_wr[k] = rr;
+            c += a; sh += b; rr += e;
         }
         s_base = (c | sh) ? atomicAdd(qcount, ((unsigned long long)sh << 32) | c) : 0ull;
+        s_rbase = rr ? atomicAdd(rcount, rr) : 0u;
     }
     __syncthreads();
+    if ((mr >> lane) & 1ull) rlist[s_rbase + s_wr[w] + __popcll(mr & lt)] = i;
     int idx = (int)((unsigned)s_base + s_wc[w] + coff);
     if (i < n) {
         auto put_ray = [&](int k, const QRay& rr, const RayMeta& mm) {
@@ -1564,7 +1601,11 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
         };
         if (has0) { put_ray(idx, c0r, c0m); nd.child0 = idx; idx++; }
         if (has1) { put_ray(idx, c1r, c1m); nd.child1 = idx; }
-        nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind | (hit ? kNodeHit : 0)));
+        // kNodeFar: a hit point whose distance to another could overflow (or is not finite) --
+        // k_resolve then reads it even for Beer's law with zero absorption
+        const bool far = hit && !(fabsf(nd.px) < 1e18f && fabsf(nd.py) < 1e18f && fabsf(nd.pz) < 1e18f);
+        nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb,
+                                   __int_as_float(nd.kind | (hit ? kNodeHit : 0) | (far ? kNodeFar : 0)));
         if (hit) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
         if ((nd.kind & 0xFF) != NK_FINAL) nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, 0);
     }
@@ -1604,15 +1645,17 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                                                const HitRec* __restrict__ hits, const NodePlanes nodes,
                                                const ShadowPlanes shadows, int* __restrict__ slist,
                                                const RayQ next_rays, RayMeta* __restrict__ next_meta,
-                                               unsigned long long* qcount, int n) {
+                                               unsigned long long* qcount, int* __restrict__ rlist,
+                                               unsigned* rcount, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    HitRec h;
-    h.obj = -1; h.prim = -1; h.t = 0.0f; h.pad = 0;
+    HitIn h;
+    h.h.obj = -1; h.h.prim = -1; h.h.t = 0.0f; h.h.pad = 0;
+    h.pt = h.beta = h.gamma = 0.0f;
     f3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     float time = 0.0f;
     RayMeta mt = {};
     if (i < n) {
-        h = load_hit_compact(hits, i);
+        h = load_hit_planes(sv, hits, n, i);
         if (GEN) {
             primary_ray(cam, ps, seed, i, o, d, time);
             mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
@@ -1622,7 +1665,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
         }
     }
     shade_ray<FULL, SPOT, BLOCK, TEX>(sv, cam, level, ps, seed, i, n, h, o, d, time, mt, nodes, shadows, slist,
-                                      next_rays, next_meta, qcount);
+                                      next_rays, next_meta, qcount, rlist, rcount);
 }
 
 // ------------------------------------------------------------------ hw7 path tracer
@@ -1689,7 +1732,8 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
             load_ray(rays, i, o, d, time);
             mt = meta[i];
         }
-        const HitRec h = load_hit_compact(hits, i);
+        const HitIn hin = load_hit_planes(sv, hits, n, i);
+        const HitRec& h = hin.h;
         uint32_t pixel, sample;
         int x, y;
         slot_pixel(cam, ps, mt.slot, pixel, sample, x, y);
@@ -1718,7 +1762,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
                 kind |= kContrib;
             }
         } else {
-            const Ret ret = hit_record<FULL>(sv, o, d, time, h);
+            const Ret ret = hit_record<FULL, true>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (medium) {                                              // Beer's law inside
@@ -2078,16 +2122,25 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
     if (kind == NK_FINAL) return basic;
     const int4 lk = self.link[i];
     const float4 pf = self.pnt[i];
+    const MaterialDev& m = sv.materials[lk.z - 1];
+    f3 p = mk(pf.x, pf.y, pf.z);
+    // Beer's law with zero absorption is exp(-0 * bd) = 1 for every finite distance bd, so the
+    // refracted child's hit point is read only when the material absorbs or a point is far enough
+    // (kNodeFar, or this node's own) for |q0 - p| to overflow
+    const bool absorbs = !(m.absorption[0] == 0.0f && m.absorption[1] == 0.0f && m.absorption[2] == 0.0f);
+    const bool p_far = !(fabsf(p.x) < 1e18f && fabsf(p.y) < 1e18f && fabsf(p.z) < 1e18f);
     f3 c0 = mk(0, 0, 0), c1 = mk(0, 0, 0), q0 = mk(0, 0, 0);
     if (lk.x >= 0) {
         const float4 a = child.col[lk.x];
         c0 = mk(a.x, a.y, a.z);
-        if (__float_as_int(a.w) & kNodeHit) { const float4 ap = child.pnt[lk.x]; q0 = mk(ap.x, ap.y, ap.z); }
+        const int ck = __float_as_int(a.w);
+        if ((ck & kNodeHit) && (absorbs || p_far || (ck & kNodeFar))) {
+            const float4 ap = child.pnt[lk.x];
+            q0 = mk(ap.x, ap.y, ap.z);
+        }
     }
     if (lk.y >= 0) { const float4 b = child.col[lk.y]; c1 = mk(b.x, b.y, b.z); }
     const struct { float F; } nd = {pf.w};
-    const MaterialDev& m = sv.materials[lk.z - 1];
-    f3 p = mk(pf.x, pf.y, pf.z);
     f3 res;
     if (kind == NK_MIRROR) {
         res = basic + cw(ld3(m.mirror), c1);
@@ -2117,10 +2170,12 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
 }
 
 // One level of the bottom-up pass (levels >= 1; level 0 is resolved inside k_accumulate).
+// One thread per non-final node of the level (k_shade's compacted list; final nodes are not read).
 __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodePlanes nodes, const NodePlanes child,
-                                                 int n) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+                                                 const int* __restrict__ rlist, const unsigned* rcount) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= (int)*rcount) return;
+    const int i = rlist[j];
     const float4 nc = nodes.col[i];
     if ((__float_as_int(nc.w) & 0xFF) == NK_FINAL) return;
     const f3 res = resolve_node(sv, nc, i, nodes, child);
@@ -2264,7 +2319,7 @@ void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
-                  unsigned long long* qcount, int n, hipStream_t st) {
+                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st) {
     if (n <= 0) return;
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
     const NodePlanes np = node_planes(nodes, n);
@@ -2273,10 +2328,10 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
     do {                                                                                                          \
         if (rays.a == nullptr)                                                                                    \
             hipLaunchKernelGGL((k_shade<F, S, B, T, true>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
-                               slist, next_rays, next_meta, qcount, n);                                           \
+                               slist, next_rays, next_meta, qcount, rlist, rcount, n);                            \
         else                                                                                                      \
             hipLaunchKernelGGL((k_shade<F, S, B, T, false>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
-                               slist, next_rays, next_meta, qcount, n);                                           \
+                               slist, next_rays, next_meta, qcount, rlist, rcount, n);                            \
     } while (0)
     if (sv.full && sv.tex) RTG_SHADE(true, true, 256, true, dim3(nblk(n, 256)), dim3(256));
     else if (sv.full) RTG_SHADE(true, true, 256, false, dim3(nblk(n, 256)), dim3(256));
@@ -2331,10 +2386,11 @@ void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRe
                        shadow_planes(const_cast<ShadowRec*>(shadows), (long long)n * (nL > 1 ? nL : 1)), nL,
                        node_planes(level0, n0), level, n);
 }
-void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child, hipStream_t st) {
+void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
+                    const int* rlist, const unsigned* rcount, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, node_planes(nodes, n),
-                       node_planes(const_cast<NodeRec*>(child_nodes), n_child), n);
+                       node_planes(const_cast<NodeRec*>(child_nodes), n_child), rlist, rcount);
 }
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
                        const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1) {

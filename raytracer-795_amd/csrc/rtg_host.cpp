@@ -703,11 +703,11 @@ int upload(DBuf& b, const std::vector<T>& v) {
 }
 
 struct Level {
-    DBuf rays, meta, hits, nodes, shadows, slist, paths;
+    DBuf rays, meta, hits, nodes, shadows, slist, paths, rlist;   // rlist: non-final nodes (k_resolve)
     long long rcap = 0;        // plane stride of `rays` (RayQ) as the previous level wrote them
     void release() {
         rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release();
-        paths.release();
+        paths.release(); rlist.release();
     }
 };
 
@@ -719,7 +719,8 @@ struct Lane {
     hipEvent_t ev_count = nullptr;          // recorded after the level count copy
     hipEvent_t ev_t[5] = {};                // trace start, trace end, shade end, shadow start, shadow end
     unsigned long long* h_count = nullptr;  // pinned host slot
-    DBuf qcnt;                              // 64 x u64 per pass (level -> next rays | shadow entries << 32)
+    DBuf qcnt;                              // 128 x u64 per pass: [level] next rays | shadow entries << 32,
+                                            // [64 + level] non-final nodes (k_resolve's list length)
     std::vector<Level> levels;
     // current pass
     std::vector<int> passes;                // indices into the frame's pass list (this lane's, in order)
@@ -1421,6 +1422,11 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         for (int k = 0; k < 3; k++) sv.has_blur |= !(d->objects[i].blur[k] == 0.0f);
     for (int i = 0; i < d->num_instances; i++)
         for (int k = 0; k < 3; k++) sv.has_blur |= !(d->instances[i].blur[k] == 0.0f);
+    sv.bary = 0;
+    for (int i = 0; i < d->num_objects; i++) {
+        const rtg_object_desc& o = d->objects[i];
+        if (o.type == RTG_OBJ_TRIANGLE || (o.type == RTG_OBJ_MESH && (o.smooth || o.num_textures > 0))) sv.bary = 1;
+    }
     sv.lean_shadow = d->num_lights == 1 &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);
@@ -1628,9 +1634,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         Level& Lc = ln.levels[level];
         Level& Ln = ln.levels[level + 1];
         int rc2;
-        if ((rc2 = Lc.hits.grow(sizeof(HitRec) * (size_t)n)) || (rc2 = Lc.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
+        if ((rc2 = Lc.hits.grow(std::max(sizeof(HitRec), kHitBytes) * (size_t)n)) || (rc2 = Lc.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
             (rc2 = Lc.shadows.grow(sizeof(ShadowRec) * (size_t)n * std::max(nL, 1))) ||
-            (rc2 = Lc.slist.grow(sizeof(int) * (size_t)n * std::max(nL, 1))))
+            (rc2 = Lc.slist.grow(sizeof(int) * (size_t)n * std::max(nL, 1))) ||
+            (!pt && level > 0 && (rc2 = Lc.rlist.grow(sizeof(int) * (size_t)n))))
             return rc2;
         const bool may_spawn = level + 1 < max_levels;
         const size_t cap = may_spawn ? 2 * (size_t)n : 1;
@@ -1656,7 +1663,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             launch_shade(sv, cd, level, ps, o.seed, cur_q,
                          gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                          Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), next_q,
-                         Ln.meta.as<RayMeta>(), qc, n, ln.st);
+                         Ln.meta.as<RayMeta>(), qc, level > 0 ? Lc.rlist.as<int>() : nullptr,
+                         reinterpret_cast<unsigned*>(ln.qcnt.as<unsigned long long>() + 64 + level), n, ln.st);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
         // the next level's size is known once shade is done: read it back now, so the host can
         // enqueue that level while this level's shadow queries still run (no host round trip
@@ -1680,8 +1688,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const PassDev& ps = plist[ln.pass];
         const int n0 = ps.ns * ps.npass;
         int rc2;
-        if ((rc2 = ln.qcnt.grow(sizeof(unsigned long long) * 64))) return rc2;
-        HIP_TRY(hipMemsetAsync(ln.qcnt.p, 0, sizeof(unsigned long long) * 64, ln.st));
+        if ((rc2 = ln.qcnt.grow(sizeof(unsigned long long) * 128))) return rc2;
+        HIP_TRY(hipMemsetAsync(ln.qcnt.p, 0, sizeof(unsigned long long) * 128, ln.st));
         ln.counts.assign(1, n0);
         ln.level = 0;
         if ((int)ln.levels.size() < 1) ln.levels.resize(1);
@@ -1713,7 +1721,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         for (int l = level - 1; l >= 1 && !pt; l--)
             if ((rc2 = timed_launch(ln, [&] {
                      launch_resolve(sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(),
-                                    ln.counts[l], ln.counts[l + 1], ln.st);
+                                    ln.counts[l], ln.counts[l + 1], ln.levels[l].rlist.as<int>(),
+                                    reinterpret_cast<const unsigned*>(ln.qcnt.as<unsigned long long>() + 64 + l), ln.st);
                  }, stt.resolve_ms, stt.resolve_launches)))
                 return rc2;
         const int mode = (total == 1) ? 2 : (ps.s0 == 0 ? 1 : 0);

@@ -151,6 +151,8 @@ struct SceneView {
                                    // stores only origin + contribution (k_shadow rebuilds d, tmax, L)
     int has_blur;                  // some object / instance has a nonzero motion-blur vector: the
                                    // ray queues carry times (RayQ::t)
+    int bary;                      // some triangle is smooth-shaded or textured: the render path's
+                                   // hit records carry the winner's barycentrics (HitPlanes::bg)
     // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
     // lights into num_lights)
     const int* top_emit;           // per top-level entry: emitter light index, -1 if not a light
@@ -232,6 +234,21 @@ struct HitRec {         // 16 B
     float t;            // gett distance
     int pad;
 };
+// The render path's hit records (k_trace -> k_shade / k_pt_shade) as planes over a level's n rays:
+// (object, primitive), the winning triangle test's ray parameter in object space, and -- only when
+// SceneView::bary -- its barycentrics (beta, gamma).  k_shade rebuilds the hit point and normal
+// from them instead of re-running the test on a 48-byte TriGeom gather.  kHitBytes per ray.
+struct HitPlanes {
+    int2* id;       // obj, prim
+    float* pt;      // object-space ray parameter of the winning candidate (Triangle::bvhIntersect's t)
+    float2* bg;     // beta, gamma (SceneView::bary), else unused
+};
+constexpr size_t kHitBytes = 20;
+__host__ __device__ inline HitPlanes hit_planes(void* base, long long n) {
+    char* p = static_cast<char*>(base);
+    return HitPlanes{reinterpret_cast<int2*>(p), reinterpret_cast<float*>(p + 8 * n),
+                     reinterpret_cast<float2*>(p + 12 * n)};
+}
 
 enum NodeKind : int {
     NK_FINAL = 0,       // color final (basic-only leaf, background, replace_all, miss)
@@ -263,6 +280,7 @@ struct NodePlanes {
     int4* link;     // child0, child1, material, -  (kind != NK_FINAL only)
 };
 constexpr int kNodeHit = 0x400;
+constexpr int kNodeFar = 0x800;    // hit point with a coordinate >= 1e18 or not finite (k_resolve)
 inline NodePlanes node_planes(NodeRec* base, long long n) {
     float4* b = reinterpret_cast<float4*>(base);
     return NodePlanes{b, b + n, reinterpret_cast<int4*>(b + 2 * n)};
@@ -304,9 +322,10 @@ struct LevelBuffers;
 void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
                   uint64_t seed = 0, bool compact = false);
+// rlist / rcount: the level's non-final nodes (levels >= 1), appended for k_resolve
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
-                  unsigned long long* qcount, int n, hipStream_t st);
+                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
                    int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted = true);
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
@@ -315,7 +334,8 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
                      unsigned long long* qcount, int n, hipStream_t st);
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
                       int n0, int level, int n, hipStream_t st);
-void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child, hipStream_t st);
+void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
+                    const int* rlist, const unsigned* rcount, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
 // level0 / level1 hold NodePlanes over n0 / n1 nodes; whitted: resolve level 0 against level 1
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,

@@ -1,0 +1,13 @@
+#!/bin/bash
+# One GPU call: gpu_round.sh (bench line, kernel trace, PMC passes; tests skipped) for every
+# workload in $WLS, tags <prefix>_<workload>.  Then, in the container:
+#   for w in $WLS; do scripts/save_round.sh <prefix>_$w $w; done
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+P=${1:-r3c}
+for wl in ${WLS:-dragon1m cornell cornell_pt bunny}; do
+  echo "=== $wl"
+  SKIP_TESTS=1 BENCH_ARGS="--workload $wl $EXTRA_ARGS" bash scripts/gpu_round.sh ${P}_$wl > gpurun_out/prof_${P}_$wl.txt 2>&1 \
+    || { tail -20 gpurun_out/prof_${P}_$wl.txt; exit 1; }
+  tail -1 gpurun_out/prof_${P}_$wl.txt
+done
