@@ -1594,6 +1594,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     // row strips, so each holds a mix of sky, floor and glass).  4 / 8 / 32 / 64 tiles: in between.
     int tile_s = 16;
     if (const char* e = getenv("RTG_TILE_S")) tile_s = std::max(1, std::min(1 << 12, atoi(e)));
+    // tile_pixel (device) forms band * (tile_h * tile_s * nx) in 32-bit ints: keep one band of the
+    // widest tiles (tile_h <= 8) below 2^31 pixels
+    if ((long long)8 * cam->nx >= (1LL << 31)) return fail(RTG_ERR_UNSUPPORTED, "image wider than 2^28 pixels");
+    tile_s = (int)std::min<long long>(tile_s, ((1LL << 31) - 1) / (8LL * cam->nx));
     std::vector<PassDev> plist;
     for (int p0 = 0; p0 < npix; p0 += np_pass)
         for (int s0 = 0; s0 < total; s0 += ns_chunk) {

@@ -78,3 +78,16 @@ def test_trace_empty_and_nan_batches(gpu):
         nan = np.float32(np.nan)
         h = r.trace([(0, 0, 0), (nan, 0, 0), (0, 0, 0)], [(0, 0, -1), (0, 0, -1), (nan, 0, -1)])
         assert list(h["full"]) == [1, 0, 0]
+
+
+def test_too_wide_image_is_rejected(gpu):
+    """A band of tile_pixel's widest tiles must stay below 2^31 pixels (32-bit band arithmetic):
+    an image wider than 2^28 pixels is refused before any work, not mis-tiled."""
+    import torch
+    sc = scenegen.simple(8, 1)
+    cam = sc.cameras[0]
+    cam.nx = (1 << 28) + 1
+    out = torch.zeros(3, device="cuda:0")
+    with rtg.Renderer(sc, device=0) as r:
+        with pytest.raises(A.RtgError, match="wider than"):
+            r.render_device(cam, out.data_ptr())

@@ -29,7 +29,9 @@ def cornell():
     r.close()
 
 
-def test_one_device_through_the_rccl_path_is_bit_identical(gpu, cornell):
+def test_one_device_list_renders_without_rccl(gpu, cornell):
+    """num_devices = 1 with a device list is the plain single-device render (no communicator, so
+    no RCCL library is needed for it)."""
     r, ref, st = cornell
     for _ in range(2):                      # the second call reuses the communicator
         img = r.render(0, num_devices=1, devices=[0])
@@ -81,6 +83,27 @@ def test_ranked_single_rank_gathers_through_rccl(gpu, cornell):
             torch.cuda.synchronize()
             assert np.array_equal(_bits(out.cpu().numpy()), _bits(ref))
         assert r.stats()["devices"] == 1
+    finally:
+        comm.close()
+
+
+def test_ranked_rank_failure_is_agreed_not_hung(gpu, cornell):
+    """A rank whose shard fails (here: a bad camera) still joins the ranks' failure agreement
+    (an allreduce of a failure flag before the gather), so no rank waits in the gather for it;
+    the communicator stays usable for the next frame."""
+    import copy
+    import torch
+    r, ref, _ = cornell
+    comm = rtg.Comm(rtg.Comm.unique_id(), 1, 0, 0)
+    try:
+        out = torch.zeros((ref.shape[0], ref.shape[1], 3), dtype=torch.float32, device="cuda:0")
+        bad = copy.deepcopy(r.scene.cameras[0])
+        bad.num_samples = 0
+        with pytest.raises(rtg.RtgError, match="bad camera"):
+            r.render_ranked(bad, comm, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        r.render_ranked(0, comm, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(_bits(out.cpu().numpy()), _bits(ref))
     finally:
         comm.close()
 
