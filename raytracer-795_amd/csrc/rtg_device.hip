@@ -19,6 +19,15 @@ namespace rtg {
 #define DEV __device__ __forceinline__
 // k_shadow: 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+// A/B switches of round 3's record trims: k_shade rebuilding the hit from the
+// stored ray parameter / barycentrics instead of re-running the test, and k_resolve walking a list
+// of the level's non-final nodes instead of every node.
+#ifndef RTG_HIT_STORED
+#define RTG_HIT_STORED 1
+#endif
+#ifndef RTG_RESOLVE_LIST
+#define RTG_RESOLVE_LIST 1
+#endif
 // k_shadow's certified early exit (closest_hit CERT), off by default: measured on the 1080p64
 // dragon (round 3, scripts/gpu_ab3.sh, same box) it cuts a blocked query's node steps 18.9 ->
 // 14.4 (all queries 8.81 -> 7.93) but k_shadow takes 12.9 instead of 12.4 ms per frame -- the
@@ -300,6 +309,307 @@ struct Stats { unsigned nodes, tris, steps; };
 // key is <= tau carry the sign bit; `nflag` counts them.  out.pad = 1 marks a certified result.
 // bary (optional): the winner's object-space ray parameter and barycentrics (render-path hit records).
 struct HitBary { float pt, beta, gamma; };
+// One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:32-73): the object's
+// winner (closest_hit's comments) and the top-level acceptance against `nearest` / `out`.
+template <bool EXHAUSTIVE, bool STATS, bool CERT>
+DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, const float time, float& nearest,
+                      HitRec& out, HitBary* bary, bool& certified, int* stack, int sstride, Stats& st,
+                      const float tcert) {
+    const float eps = sv.int_eps;
+    const TopObject& T = sv.tops[i];
+    const Geometry& g = sv.geoms[T.geom];
+    f3 o2, d2;
+    transform_ray(T, o, d, time, o2, d2);
+    bool found = false;
+    int bprim = -1;
+    f3 bp = mk(0, 0, 0);
+    float bt = 0.0f, bb = 0.0f, bg = 0.0f;    // mesh winner: ray parameter, beta, gamma (bp = o2 + d2 bt)
+    if (g.type == RTG_OBJ_SPHERE) {
+        if (g.nprims > 0) {
+            f3 ip;
+            if (sphere_test(o2, d2, ld3(g.center), g.radius, eps, ip)) {
+                float dist = norm(ip - o2);
+                if (dist < FLT_MAX) { found = true; bprim = g.prim_base; bp = ip; }
+            }
+        }
+    } else {
+        // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
+        // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
+        // send every box to the exact division test instead.
+        const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
+        const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
+                          adz <= 1e30f;
+        const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
+        // the root box first: an object whose root the line misses costs no further setup
+        // (small scenes are dominated by the reference's linear loop over objects)
+        const bool root_ok = g.node_base < 0 ? g.root_leaf_count > 0
+                           : box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
+                                     g.root_max[1], g.root_max[2]);
+        if (!root_ok) return;
+        // distance bound from the best hit so far (see DESIGN.md "pruning")
+        float boundD = FLT_MAX;
+        const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
+        const float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
+        if (!EXHAUSTIVE && nearest < FLT_MAX) {
+            float dl = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+            if (da != 0.0f) {
+                float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * (1.0f + 1e-5f);
+                boundD = tm * dl * (1.0f + 2e-5f) + 1e-30f;
+                if (!(boundD == boundD)) boundD = FLT_MAX;
+            }
+        }
+        const float pad = g.prune_pad;
+        float best_d = FLT_MAX;
+        int best_leaf = -1;
+        // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
+        // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
+        // skipped when its box, expanded by `pad`, meets the line only outside that window.
+        const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
+        const float tlo = -(fabsf(eps) + 1e-6f);
+        const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+        const float inv_dn = __builtin_amdgcn_rcpf(dnorm);   // 1 ulp: inside the 2e-5 margins of thi
+        float thi = INFINITY;
+        if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
+        const float thi0 = thi;     // thi never exceeds the window of the best hit so far
+        // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
+        auto test_prim = [&](const TriGeom& tg, int k, int start) {
+            if (STATS) st.tris++;
+            Cand c = tri_test(tg, o2, d2, eps);
+            if (c.ok) {
+                float dist = norm(c.p - o2);
+                if (dist < FLT_MAX &&
+                    (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
+                    best_d = dist; best_leaf = start; bprim = k; found = true;
+                    bt = c.t; bb = c.beta; bg = c.gamma;
+                    if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+                }
+            }
+        };
+        // one child box: reachability (interior, exact predicate) + window pruning + entry key
+        auto child = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool interior,
+                         float& key) -> bool {
+            key = 0.0f;
+            if (!EXHAUSTIVE && fast) {
+                float ax = (mnx - o2.x) * inv.x, bx = (mxx - o2.x) * inv.x;
+                float ay = (mny - o2.y) * inv.y, by = (mxy - o2.y) * inv.y;
+                float az = (mnz - o2.z) * inv.z, bz = (mxz - o2.z) * inv.z;
+                float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                float lo = le - e - padt, hi = sl + e + padt;
+                key = lo;
+                if (hi < lo || hi < tlo || lo > thi) return false;
+                if (!interior) return true;
+                if (sl < le - e) return false;
+                if (sl >= le + e) return true;
+                return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+            }
+            if (!interior) return true;
+            return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
+        };
+        if (g.node_base < 0) {
+            for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
+                test_prim(sv.tris[k], k, g.root_leaf_start);
+        } else {                // root box already hit (root_ok)
+            // Leaf children are resolved as soon as they are reached.
+            auto leaf = [&](int start, int count) {
+                for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
+            };
+            // BVH2 walk (ordered, pruned): the reference tree node by node.
+            auto walk2 = [&]() {
+                int sp = 0;
+                int cur = g.node_base;
+                while (true) {
+                    if (STATS) { st.nodes += 2; st.steps++; }   // one 64-B node = two 32-B child records
+                    const Node nd = sv.nodes[cur];
+                    const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
+                    float lk = 0.0f, rk = 0.0f;
+                    bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
+                    bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
+                    bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
+                    if (lleaf && rleaf && rk < lk) {
+                        leaf(rref, rcnt);
+                        if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
+                        lok = rok = false;
+                    } else {
+                        if (lleaf) { leaf(lref, lcnt); lok = false; }
+                        if (rleaf) {
+                            if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
+                            rok = false;
+                        }
+                    }
+                    if (!EXHAUSTIVE) {
+                        lok = lok && !(lk > thi);
+                        rok = rok && !(rk > thi);
+                    }
+                    if (lok && rok) {
+                        int nearc = lref, farc = rref;
+                        if (rk < lk) { nearc = rref; farc = lref; }
+                        stack[sp * sstride] = farc;
+                        sp++;
+                        cur = nearc;
+                    } else if (lok) {
+                        cur = lref;
+                    } else if (rok) {
+                        cur = rref;
+                    } else {
+                        if (sp == 0) break;
+                        sp--;
+                        cur = stack[sp * sstride];
+                    }
+                }
+            };
+            // Fast rays walk the mesh's traversal tree (SAH, 4-wide; rtg_host.cpp): slots are
+            // pruned by the parameter window only (boxes widened by the eps overhang), leaves are
+            // tested nearer-first as they are reached, interior slots visited nearest-first.  A
+            // candidate that would become the object's winner must be reachable in the
+            // reference tree: its reference leaf's parent box (the only ancestor box that can
+            // fail when the candidate lies outside its triangle) gets the exact slab test.
+            // Exhaustive traversal, rays with a zero / denormal / huge direction component and
+            // a stack that would overflow (> kStackDepth entries) use the reference tree's BVH2
+            // walk; candidates already accepted stay valid (they are reachable).
+            bool use2 = EXHAUSTIVE || !fast || g.sah_base < 0;
+            if (!use2) {
+                // CERT: tau bounds gett()'s rounding (4u |o_a| / |d_a|, as the object-loop bound
+                // above) with a 4x margin: a candidate with t > tau has gett() > 0
+                const bool cert_on = CERT && tcert > 0.0f;
+                const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : -INFINITY;
+                // > 0: the best candidate so far has gett() in (0, tcert] (a float, not a lane
+                // mask: SGPRs are the scarce register file of this loop)
+                float best_cert = -1.0f;
+                int nflag = 0;            // stack entries whose key is <= tau (sign bit set)
+                auto test_sah = [&](const TriGeom& tg) {
+                    if (STATS) st.tris++;
+                    Cand c = tri_test(tg, o2, d2, eps);
+                    if (!c.ok) return;
+                    const float dist = norm(c.p - o2);
+                    const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
+                    if (!(dist < FLT_MAX &&
+                          (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))))
+                        return;
+                    if (__float_as_int(tg.p2.w)) {          // src/BVH.cpp:178 on the leaf's parent
+                        const float* gb = sv.gates + 6 * (size_t)k;
+                        if (!box_hit(o2, d2, inv, fast, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) return;
+                    }
+                    best_d = dist; best_leaf = start; bprim = k; found = true;
+                    bt = c.t; bb = c.beta; bg = c.gamma;
+                    if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+                    if (CERT) {
+                        // gett() of a fast ray is its first quotient (d2.x finite, nonzero); a NaN
+                        // compares false (not certified)
+                        const float tg_ = (c.p.x - o2.x) / d2.x;
+                        best_cert = (tg_ > 0 && tg_ * (1.0f + 2e-5f) <= tcert) ? 1.0f : -1.0f;
+                    }
+                };
+                int sp = 0;
+                int cur = g.sah_base;
+                while (true) {
+                    if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
+                    const Node4 nd = sv.snodes[cur];
+                    const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
+                    const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
+                    const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
+                    const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
+                    const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
+                    const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
+                    const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
+                    const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
+                    float key[4];
+                    int okm = 0, leafm = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
+                        const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
+                        const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
+                        const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                        const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                        const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                        const float lo = le - e, hi = sl + e;      // boxes carry the pad
+                        key[j] = lo;
+                        const bool ok = inf[j] >= 0 && !(hi < lo || hi < tlo || lo > thi);
+                        okm |= ok << j;
+                        leafm |= (inf[j] > 0) << j;
+                    }
+                    // interior slots first, so the node's boxes are dead during the leaf tests
+                    float k4[4];
+                    int r4[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const bool take = ((okm >> j) & 1) && !((leafm >> j) & 1);
+                        k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
+                        r4[j] = take ? rf[j] : -1;
+                    }
+                    int leaf_mask = okm & leafm;
+                    while (leaf_mask) {          // leaves now, one code site (thi may shrink between them)
+                        const int j = __builtin_ctz(leaf_mask);
+                        leaf_mask &= leaf_mask - 1;
+                        const float kj = j == 0 ? key[0] : j == 1 ? key[1] : j == 2 ? key[2] : key[3];
+                        if (kj > thi) continue;
+                        const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
+                        const int cnt = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
+                        for (int q = start; q < start + cnt; q++) test_sah(sv.stris[q]);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (k4[j] > thi) { k4[j] = INFINITY; r4[j] = -1; }
+                    // interior slots, nearest first: sort (key, ref), push the others farthest first
+                    auto ce = [&](int a, int b) {
+                        const bool sw = k4[b] < k4[a];
+                        const float ka = k4[a], kb = k4[b];
+                        const int ra = r4[a], rb = r4[b];
+                        k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
+                        r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
+                    };
+                    ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+                    const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
+                    if (sp + npush > kStackDepth) { use2 = true; break; }
+                    // CERT: pushes of subtrees that may hold a candidate with t <= tau carry the
+                    // sign bit (tau = -inf when certification is off: no flags)
+                    auto push = [&](int j) {
+                        if (r4[j] < 0) return;
+                        int e = r4[j];
+                        if (CERT) {
+                            const bool fl = !(k4[j] > tau);
+                            nflag += fl;
+                            e |= fl ? (int)0x80000000u : 0;
+                        }
+                        stack[sp * sstride] = e;
+                        sp++;
+                    };
+                    push(3); push(2); push(1);
+                    if (r4[0] >= 0) {
+                        if (CERT && best_cert > 0.0f && nflag == 0 && k4[0] > tau) break;
+                        cur = r4[0];
+                    } else {
+                        if (CERT && best_cert > 0.0f && nflag == 0) break;
+                        if (sp == 0) break;
+                        sp--;
+                        const int e = stack[sp * sstride];
+                        if (CERT) nflag -= e < 0;
+                        cur = CERT ? (e & 0x7fffffff) : e;
+                    }
+                }
+            }
+            if (use2) walk2();
+        }
+        bp = o2 + d2 * bt;          // the candidate's point, as tri_test formed it
+    }
+    if (found) {
+        float t = gett(o2, d2, bp);
+        if (t > 0 && (t < nearest || (t == nearest && i < out.obj))) {   // src/Helper.cpp:43, 64
+            nearest = t;
+            out.obj = i; out.prim = bprim; out.t = t;
+            if (bary) { bary->pt = bt; bary->beta = bb; bary->gamma = bg; }
+        }
+        // the object's winner is this candidate (a complete walk, a sphere) or, after the walk's
+        // early exit, lies in (0, t]: either way the final nearest t is in (0, tcert]
+        if (CERT && t > 0 && t * (1.0f + 2e-5f) <= tcert) {
+            certified = true;
+            out.obj = i; out.prim = bprim; out.t = t; out.pad = 1;
+        }
+    }
+}
+
 template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool CERT = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
                        short* tstack = nullptr, float tcert = -INFINITY, HitBary* bary = nullptr) {
@@ -307,301 +617,9 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
     float nearest = tmax;
-    const float eps = sv.int_eps;
     bool certified = false;
     auto visit = [&](const int i) {
-        const TopObject& T = sv.tops[i];
-        const Geometry& g = sv.geoms[T.geom];
-        f3 o2, d2;
-        transform_ray(T, o, d, time, o2, d2);
-        bool found = false;
-        int bprim = -1;
-        f3 bp = mk(0, 0, 0);
-        float bt = 0.0f, bb = 0.0f, bg = 0.0f;    // mesh winner: ray parameter, beta, gamma (bp = o2 + d2 bt)
-        if (g.type == RTG_OBJ_SPHERE) {
-            if (g.nprims > 0) {
-                f3 ip;
-                if (sphere_test(o2, d2, ld3(g.center), g.radius, eps, ip)) {
-                    float dist = norm(ip - o2);
-                    if (dist < FLT_MAX) { found = true; bprim = g.prim_base; bp = ip; }
-                }
-            }
-        } else {
-            // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
-            // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
-            // send every box to the exact division test instead.
-            const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
-            const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
-                              adz <= 1e30f;
-            const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
-            // the root box first: an object whose root the line misses costs no further setup
-            // (small scenes are dominated by the reference's linear loop over objects)
-            const bool root_ok = g.node_base < 0 ? g.root_leaf_count > 0
-                               : box_hit(o2, d2, inv, fast, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
-                                         g.root_max[1], g.root_max[2]);
-            if (!root_ok) return;
-            // distance bound from the best hit so far (see DESIGN.md "pruning")
-            float boundD = FLT_MAX;
-            const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
-            const float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
-            if (!EXHAUSTIVE && nearest < FLT_MAX) {
-                float dl = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
-                if (da != 0.0f) {
-                    float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * (1.0f + 1e-5f);
-                    boundD = tm * dl * (1.0f + 2e-5f) + 1e-30f;
-                    if (!(boundD == boundD)) boundD = FLT_MAX;
-                }
-            }
-            const float pad = g.prune_pad;
-            float best_d = FLT_MAX;
-            int best_leaf = -1;
-            // Parameter window that can hold a useful candidate: t >= -eps (Triangle::bvhIntersect
-            // acceptance) and t <= min(tm, best_d/|d'|) (farther hits cannot win).  A subtree is
-            // skipped when its box, expanded by `pad`, meets the line only outside that window.
-            const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
-            const float tlo = -(fabsf(eps) + 1e-6f);
-            const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
-            const float inv_dn = __builtin_amdgcn_rcpf(dnorm);   // 1 ulp: inside the 2e-5 margins of thi
-            float thi = INFINITY;
-            if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
-            const float thi0 = thi;     // thi never exceeds the window of the best hit so far
-            // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
-            auto test_prim = [&](const TriGeom& tg, int k, int start) {
-                if (STATS) st.tris++;
-                Cand c = tri_test(tg, o2, d2, eps);
-                if (c.ok) {
-                    float dist = norm(c.p - o2);
-                    if (dist < FLT_MAX &&
-                        (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
-                        best_d = dist; best_leaf = start; bprim = k; found = true;
-                        bt = c.t; bb = c.beta; bg = c.gamma;
-                        if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                    }
-                }
-            };
-            // one child box: reachability (interior, exact predicate) + window pruning + entry key
-            auto child = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool interior,
-                             float& key) -> bool {
-                key = 0.0f;
-                if (!EXHAUSTIVE && fast) {
-                    float ax = (mnx - o2.x) * inv.x, bx = (mxx - o2.x) * inv.x;
-                    float ay = (mny - o2.y) * inv.y, by = (mxy - o2.y) * inv.y;
-                    float az = (mnz - o2.z) * inv.z, bz = (mxz - o2.z) * inv.z;
-                    float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                    float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                    float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                    float lo = le - e - padt, hi = sl + e + padt;
-                    key = lo;
-                    if (hi < lo || hi < tlo || lo > thi) return false;
-                    if (!interior) return true;
-                    if (sl < le - e) return false;
-                    if (sl >= le + e) return true;
-                    return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
-                }
-                if (!interior) return true;
-                return box_test(o2, d2, mnx, mny, mnz, mxx, mxy, mxz);
-            };
-            if (g.node_base < 0) {
-                for (int k = g.root_leaf_start; k < g.root_leaf_start + g.root_leaf_count; k++)
-                    test_prim(sv.tris[k], k, g.root_leaf_start);
-            } else {                // root box already hit (root_ok)
-                // Leaf children are resolved as soon as they are reached.
-                auto leaf = [&](int start, int count) {
-                    for (int k = start; k < start + count; k++) test_prim(sv.tris[k], k, start);
-                };
-                // BVH2 walk (ordered, pruned): the reference tree node by node.
-                auto walk2 = [&]() {
-                    int sp = 0;
-                    int cur = g.node_base;
-                    while (true) {
-                        if (STATS) { st.nodes += 2; st.steps++; }   // one 64-B node = two 32-B child records
-                        const Node nd = sv.nodes[cur];
-                        const int lref = nd.d.x, rref = nd.d.y, lcnt = nd.d.z, rcnt = nd.d.w;
-                        float lk = 0.0f, rk = 0.0f;
-                        bool lok = lcnt >= 0 && child(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, lcnt == 0, lk);
-                        bool rok = rcnt >= 0 && child(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, rcnt == 0, rk);
-                        bool lleaf = lok && lcnt > 0, rleaf = rok && rcnt > 0;
-                        if (lleaf && rleaf && rk < lk) {
-                            leaf(rref, rcnt);
-                            if (EXHAUSTIVE || !(lk > thi)) leaf(lref, lcnt);
-                            lok = rok = false;
-                        } else {
-                            if (lleaf) { leaf(lref, lcnt); lok = false; }
-                            if (rleaf) {
-                                if (EXHAUSTIVE || !(rk > thi)) leaf(rref, rcnt);
-                                rok = false;
-                            }
-                        }
-                        if (!EXHAUSTIVE) {
-                            lok = lok && !(lk > thi);
-                            rok = rok && !(rk > thi);
-                        }
-                        if (lok && rok) {
-                            int nearc = lref, farc = rref;
-                            if (rk < lk) { nearc = rref; farc = lref; }
-                            stack[sp * sstride] = farc;
-                            sp++;
-                            cur = nearc;
-                        } else if (lok) {
-                            cur = lref;
-                        } else if (rok) {
-                            cur = rref;
-                        } else {
-                            if (sp == 0) break;
-                            sp--;
-                            cur = stack[sp * sstride];
-                        }
-                    }
-                };
-                // Fast rays walk the mesh's traversal tree (SAH, 4-wide; rtg_host.cpp): slots are
-                // pruned by the parameter window only (boxes widened by the eps overhang), leaves are
-                // tested nearer-first as they are reached, interior slots visited nearest-first.  A
-                // candidate that would become the object's winner must be reachable in the
-                // reference tree: its reference leaf's parent box (the only ancestor box that can
-                // fail when the candidate lies outside its triangle) gets the exact slab test.
-                // Exhaustive traversal, rays with a zero / denormal / huge direction component and
-                // a stack that would overflow (> kStackDepth entries) use the reference tree's BVH2
-                // walk; candidates already accepted stay valid (they are reachable).
-                bool use2 = EXHAUSTIVE || !fast || g.sah_base < 0;
-                if (!use2) {
-                    // CERT: tau bounds gett()'s rounding (4u |o_a| / |d_a|, as the object-loop bound
-                    // above) with a 4x margin: a candidate with t > tau has gett() > 0
-                    const bool cert_on = CERT && tcert > 0.0f;
-                    const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : -INFINITY;
-                    // > 0: the best candidate so far has gett() in (0, tcert] (a float, not a lane
-                    // mask: SGPRs are the scarce register file of this loop)
-                    float best_cert = -1.0f;
-                    int nflag = 0;            // stack entries whose key is <= tau (sign bit set)
-                    auto test_sah = [&](const TriGeom& tg) {
-                        if (STATS) st.tris++;
-                        Cand c = tri_test(tg, o2, d2, eps);
-                        if (!c.ok) return;
-                        const float dist = norm(c.p - o2);
-                        const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
-                        if (!(dist < FLT_MAX &&
-                              (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))))
-                            return;
-                        if (__float_as_int(tg.p2.w)) {          // src/BVH.cpp:178 on the leaf's parent
-                            const float* gb = sv.gates + 6 * (size_t)k;
-                            if (!box_hit(o2, d2, inv, fast, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) return;
-                        }
-                        best_d = dist; best_leaf = start; bprim = k; found = true;
-                        bt = c.t; bb = c.beta; bg = c.gamma;
-                        if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                        if (CERT) {
-                            // gett() of a fast ray is its first quotient (d2.x finite, nonzero); a NaN
-                            // compares false (not certified)
-                            const float tg_ = (c.p.x - o2.x) / d2.x;
-                            best_cert = (tg_ > 0 && tg_ * (1.0f + 2e-5f) <= tcert) ? 1.0f : -1.0f;
-                        }
-                    };
-                    int sp = 0;
-                    int cur = g.sah_base;
-                    while (true) {
-                        if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
-                        const Node4 nd = sv.snodes[cur];
-                        const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
-                        const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
-                        const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
-                        const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
-                        const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
-                        const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
-                        const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
-                        const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
-                        float key[4];
-                        int okm = 0, leafm = 0;
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
-                            const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
-                            const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
-                            const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                            const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                            const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                            const float lo = le - e, hi = sl + e;      // boxes carry the pad
-                            key[j] = lo;
-                            const bool ok = inf[j] >= 0 && !(hi < lo || hi < tlo || lo > thi);
-                            okm |= ok << j;
-                            leafm |= (inf[j] > 0) << j;
-                        }
-                        // interior slots first, so the node's boxes are dead during the leaf tests
-                        float k4[4];
-                        int r4[4];
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const bool take = ((okm >> j) & 1) && !((leafm >> j) & 1);
-                            k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
-                            r4[j] = take ? rf[j] : -1;
-                        }
-                        int leaf_mask = okm & leafm;
-                        while (leaf_mask) {          // leaves now, one code site (thi may shrink between them)
-                            const int j = __builtin_ctz(leaf_mask);
-                            leaf_mask &= leaf_mask - 1;
-                            const float kj = j == 0 ? key[0] : j == 1 ? key[1] : j == 2 ? key[2] : key[3];
-                            if (kj > thi) continue;
-                            const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
-                            const int cnt = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
-                            for (int q = start; q < start + cnt; q++) test_sah(sv.stris[q]);
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; j++)
-                            if (k4[j] > thi) { k4[j] = INFINITY; r4[j] = -1; }
-                        // interior slots, nearest first: sort (key, ref), push the others farthest first
-                        auto ce = [&](int a, int b) {
-                            const bool sw = k4[b] < k4[a];
-                            const float ka = k4[a], kb = k4[b];
-                            const int ra = r4[a], rb = r4[b];
-                            k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
-                            r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
-                        };
-                        ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-                        const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
-                        if (sp + npush > kStackDepth) { use2 = true; break; }
-                        // CERT: pushes of subtrees that may hold a candidate with t <= tau carry the
-                        // sign bit (tau = -inf when certification is off: no flags)
-                        auto push = [&](int j) {
-                            if (r4[j] < 0) return;
-                            int e = r4[j];
-                            if (CERT) {
-                                const bool fl = !(k4[j] > tau);
-                                nflag += fl;
-                                e |= fl ? (int)0x80000000u : 0;
-                            }
-                            stack[sp * sstride] = e;
-                            sp++;
-                        };
-                        push(3); push(2); push(1);
-                        if (r4[0] >= 0) {
-                            if (CERT && best_cert > 0.0f && nflag == 0 && k4[0] > tau) break;
-                            cur = r4[0];
-                        } else {
-                            if (CERT && best_cert > 0.0f && nflag == 0) break;
-                            if (sp == 0) break;
-                            sp--;
-                            const int e = stack[sp * sstride];
-                            if (CERT) nflag -= e < 0;
-                            cur = CERT ? (e & 0x7fffffff) : e;
-                        }
-                    }
-                }
-                if (use2) walk2();
-            }
-            bp = o2 + d2 * bt;          // the candidate's point, as tri_test formed it
-        }
-        if (found) {
-            float t = gett(o2, d2, bp);
-            if (t > 0 && (t < nearest || (t == nearest && i < out.obj))) {   // src/Helper.cpp:43, 64
-                nearest = t;
-                out.obj = i; out.prim = bprim; out.t = t;
-                if (bary) { bary->pt = bt; bary->beta = bb; bary->gamma = bg; }
-            }
-            // the object's winner is this candidate (a complete walk, a sphere) or, after the walk's
-            // early exit, lies in (0, t]: either way the final nearest t is in (0, tcert]
-            if (CERT && t > 0 && t * (1.0f + 2e-5f) <= tcert) {
-                certified = true;
-                out.obj = i; out.prim = bprim; out.t = t; out.pad = 1;
-            }
-        }
+        visit_object<EXHAUSTIVE, STATS, CERT>(sv, i, o, d, time, nearest, out, bary, certified, stack, sstride, st, tcert);
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
@@ -1327,7 +1345,7 @@ DEV HitIn load_hit_planes(const SceneView& sv, const HitRec* hits, int n, int i)
     HitIn r;
     r.h.obj = v.x; r.h.prim = v.y; r.h.t = 0.0f; r.h.pad = 0;
     r.pt = 0.0f; r.beta = 0.0f; r.gamma = 0.0f;
-    if (v.x >= 0) {
+    if (RTG_HIT_STORED && v.x >= 0) {
         r.pt = hp.pt[i];
         if (sv.bary) { const float2 bg = hp.bg[i]; r.beta = bg.x; r.gamma = bg.y; }
     }
@@ -1374,8 +1392,10 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
         if (compact) {
             const HitPlanes hp = hit_planes(hits, n);
             hp.id[i] = make_int2(h.obj, h.prim);
-            hp.pt[i] = hb.pt;
-            if (sv.bary) hp.bg[i] = make_float2(hb.beta, hb.gamma);
+            if (RTG_HIT_STORED) {
+                hp.pt[i] = hb.pt;
+                if (sv.bary) hp.bg[i] = make_float2(hb.beta, hb.gamma);
+            }
         } else {
             hits[i] = h;
         }
@@ -1466,7 +1486,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
             }
         } else {
             hit = true;
-            Ret ret = hit_record<FULL && TEX, true>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+            Ret ret = hit_record<FULL && TEX, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading Scene.cpp:230-241
@@ -1576,7 +1596,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
     const unsigned long long m1 = __ballot(nchild >= 1), m2 = __ballot(nchild >= 2);
     const unsigned coff = __popcll(m1 & lt) + __popcll(m2 & lt);
     // non-final nodes of levels >= 1: the list k_resolve walks (level 0 resolves in k_accumulate)
-    const unsigned long long mr = __ballot(level > 0 && i < n && (nd.kind & 0xFF) != NK_FINAL);
+    const unsigned long long mr = __ballot(RTG_RESOLVE_LIST && level > 0 && i < n && (nd.kind & 0xFF) != NK_FINAL);
     unsigned stot = 0;
     for (int li = 0; li < sv.num_lights; li++) stot += __popcll(__ballot((smask >> li) & 1ull));
     if (lane == 0) { s_wc[w] = __popcll(m1) + __popcll(m2); s_ws[w] = stot; s_wr[w] = __popcll(mr); }
@@ -1762,7 +1782,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
                 kind |= kContrib;
             }
         } else {
-            const Ret ret = hit_record<FULL, true>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+            const Ret ret = hit_record<FULL, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (medium) {                                              // Beer's law inside
@@ -2172,10 +2192,10 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
 // One level of the bottom-up pass (levels >= 1; level 0 is resolved inside k_accumulate).
 // One thread per non-final node of the level (k_shade's compacted list; final nodes are not read).
 __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodePlanes nodes, const NodePlanes child,
-                                                 const int* __restrict__ rlist, const unsigned* rcount) {
+                                                 const int* __restrict__ rlist, const unsigned* rcount, int n) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= (int)*rcount) return;
-    const int i = rlist[j];
+    if (j >= (RTG_RESOLVE_LIST ? (int)*rcount : n)) return;
+    const int i = RTG_RESOLVE_LIST ? rlist[j] : j;
     const float4 nc = nodes.col[i];
     if ((__float_as_int(nc.w) & 0xFF) == NK_FINAL) return;
     const f3 res = resolve_node(sv, nc, i, nodes, child);
@@ -2390,7 +2410,7 @@ void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_no
                     const int* rlist, const unsigned* rcount, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, node_planes(nodes, n),
-                       node_planes(const_cast<NodeRec*>(child_nodes), n_child), rlist, rcount);
+                       node_planes(const_cast<NodeRec*>(child_nodes), n_child), rlist, rcount, n);
 }
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
                        const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1) {

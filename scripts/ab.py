@@ -21,6 +21,7 @@ st = r.stats()
 print(json.dumps({"lib": os.environ.get("RTG_LIBRARY", "librtg"), "workload": w, "frame_ms": round(statistics.median(ms), 2),
                   "frames": [round(x, 2) for x in ms], "trace_ms": round(st["trace_ms"], 2),
                   "shadow_ms": round(st["shadow_ms"], 2), "shade_ms": round(st["shade_ms"], 2),
+                  "resolve_ms": round(st["resolve_ms"], 2), "accumulate_ms": round(st["accumulate_ms"], 2),
                   "streams1_ms": round(st["render_ms"], 2),
                   "trace_steps_per_ray": round(ss["trace_steps"] / max(ss["primary_rays"] + ss["secondary_rays"], 1), 3),
                   "shadow_steps_per_query": round(ss["shadow_steps"] / max(ss["shadow_rays"], 1), 3),
