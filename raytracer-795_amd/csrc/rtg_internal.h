@@ -234,6 +234,17 @@ struct HitRec {         // 16 B
     float t;            // gett distance
     int pad;
 };
+// A/B switches of two round-3 record trims, both measured slower and off:
+// RTG_HIT_STORED -- k_shade rebuilds the hit from the stored ray parameter / barycentrics instead of
+// re-running the winning test (1080p64 dragon k_shade 9.4 -> 9.9 ms, cornell 7.6 -> 8.6 ms);
+// RTG_RESOLVE_LIST -- k_resolve walks a list of the level's non-final nodes, appended by k_shade,
+// instead of every node (k_resolve 1.76 -> 1.98 ms, k_shade +0.3 ms per frame).
+#ifndef RTG_HIT_STORED
+#define RTG_HIT_STORED 0
+#endif
+#ifndef RTG_RESOLVE_LIST
+#define RTG_RESOLVE_LIST 0
+#endif
 // The render path's hit records (k_trace -> k_shade / k_pt_shade) as planes over a level's n rays:
 // (object, primitive), the winning triangle test's ray parameter in object space, and -- only when
 // SceneView::bary -- its barycentrics (beta, gamma).  k_shade rebuilds the hit point and normal
@@ -243,7 +254,7 @@ struct HitPlanes {
     float* pt;      // object-space ray parameter of the winning candidate (Triangle::bvhIntersect's t)
     float2* bg;     // beta, gamma (SceneView::bary), else unused
 };
-constexpr size_t kHitBytes = 20;
+constexpr size_t kHitBytes = RTG_HIT_STORED ? 20 : 8;
 __host__ __device__ inline HitPlanes hit_planes(void* base, long long n) {
     char* p = static_cast<char*>(base);
     return HitPlanes{reinterpret_cast<int2*>(p), reinterpret_cast<float*>(p + 8 * n),
@@ -319,9 +330,12 @@ struct Counters {
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
 struct LevelBuffers;
 // gen_cam / gen_ps non-null: level 0 (either integrator), rays are generated in the kernel
+// refill_ctr non-null (render path, no TLAS): the persistent lane-refill kernel (RTG_REFILL experiment);
+// *refill_ctr must be 0 at launch
 void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
-                  uint64_t seed = 0, bool compact = false);
+                  uint64_t seed = 0, bool compact = false, unsigned* refill_ctr = nullptr, int refill_min = 16,
+                  int refill_waves = 4096);
 // rlist / rcount: the level's non-final nodes (levels >= 1), appended for k_resolve
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,

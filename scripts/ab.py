@@ -18,7 +18,7 @@ ss = r.stats()
 r.render(0, collect_timing=1, streams=1)
 r.render(0, collect_timing=1, streams=1)
 st = r.stats()
-print(json.dumps({"lib": os.environ.get("RTG_LIBRARY", "librtg"), "workload": w, "frame_ms": round(statistics.median(ms), 2),
+print(json.dumps({"lib": os.environ.get("AB_TAG", os.environ.get("RTG_LIBRARY", "librtg")), "workload": w, "frame_ms": round(statistics.median(ms), 2),
                   "frames": [round(x, 2) for x in ms], "trace_ms": round(st["trace_ms"], 2),
                   "shadow_ms": round(st["shadow_ms"], 2), "shade_ms": round(st["shade_ms"], 2),
                   "resolve_ms": round(st["resolve_ms"], 2), "accumulate_ms": round(st["accumulate_ms"], 2),

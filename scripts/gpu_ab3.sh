@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of librtg variants (raytracer-795_amd/rtg/<lib>.so) with scripts/ab.py, each library run
 # twice in alternation (A B A B) on $WL (default dragon1m); optional $TESTS first (default library).
-#   LIBS="librtg nocert" WL=dragon1m TESTS="tests/test_gpu_parity.py" bash scripts/gpu_ab3.sh
+#   LIBS="librtg nocert librtg:RTG_REFILL=1,RTG_REFILL_MIN=8" WL=dragon1m TESTS="..." bash scripts/gpu_ab3.sh
+# (an entry lib:VAR=val,... runs that library with those environment settings)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -13,10 +14,11 @@ if [ -n "$TESTS" ]; then
 fi
 : > gpurun_out/ab3.log
 for rep in 1 2; do
-  for lib in ${LIBS:-librtg}; do
+  for cfg in ${LIBS:-librtg}; do
+    lib=${cfg%%:*}; envs=${cfg#*:}; [ "$envs" = "$cfg" ] && envs=""
     for wl in ${WL:-dragon1m}; do
-      RTG_LIBRARY=raytracer-795_amd/rtg/$lib.so timeout -k 10 300 python3 scripts/ab.py $wl >> gpurun_out/ab3.log 2>/dev/null \
-        || { echo "ab.py failed: $lib $wl"; exit 1; }
+      env ${envs//,/ } AB_TAG="$cfg" RTG_LIBRARY=raytracer-795_amd/rtg/$lib.so timeout -k 10 300 python3 scripts/ab.py $wl \
+        >> gpurun_out/ab3.log 2>/dev/null || { echo "ab.py failed: $cfg $wl"; exit 1; }
     done
   done
 done
