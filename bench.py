@@ -54,9 +54,11 @@ def log(*a):
 
 def load_counters(workload: str) -> dict:
     """Per-dispatch PMC counter means of the last committed profiling run of this workload
-    (scripts/pmc_counters.py): profiles/counters_<workload>.json, or counters_current.json when
-    it was taken on this workload."""
-    for f in (os.path.join(PROFILES, f"counters_{workload}.json"), os.path.join(PROFILES, "counters_current.json")):
+    (scripts/pmc_counters.py): profiles/counters_<workload>.json (or, first, $RTG_COUNTERS_DIR's), or
+    counters_current.json when it was taken on this workload."""
+    dirs = [os.environ["RTG_COUNTERS_DIR"]] if os.environ.get("RTG_COUNTERS_DIR") else []
+    cands = [os.path.join(d, f"counters_{workload}.json") for d in dirs + [PROFILES]]
+    for f in cands + [os.path.join(PROFILES, "counters_current.json")]:
         try:
             with open(f) as fh:
                 c = json.load(fh)

@@ -259,9 +259,15 @@ DEV float gett(f3 o, f3 d, f3 p) {
     return t;
 }
 // Transforming::TransformRay (src/Helper.cpp:110-133)
-DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d2) {
-    if (T.ident && __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z) &&
-        __builtin_isfinite(d.x) && __builtin_isfinite(d.y) && __builtin_isfinite(d.z) && __builtin_isfinite(time)) {
+// fin: every component of o, d and time is finite (ray_finite), computed once per ray -- as seven
+// separate tests the compiler hoisted them out of the object loop as seven lane masks, and the
+// SGPRs they held were spilled in k_shadow / k_trace.
+DEV bool ray_finite(f3 o, f3 d, float time) {
+    const float s = (((o.x * 0.0f + o.y * 0.0f) + (o.z * 0.0f + d.x * 0.0f)) + (d.y * 0.0f + d.z * 0.0f)) + time * 0.0f;
+    return s == 0.0f;       // x * 0 is NaN exactly for x = +-inf or NaN
+}
+DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d2, bool fin) {
+    if (T.ident && fin) {
         // identity inverse, +0 blur: (x*1 + y*0) + (z*0 + w*0) == x + 0 for finite inputs
         // (the only effect is -0 -> +0)
         o2 = mk(o.x + 0.0f, o.y + 0.0f, o.z + 0.0f);
@@ -307,14 +313,14 @@ struct HitBary { float pt, beta, gamma; };
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:32-73): the object's
 // winner (closest_hit's comments) and the top-level acceptance against `nearest` / `out`.
 template <bool EXHAUSTIVE, bool STATS, bool CERT>
-DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, const float time, float& nearest,
-                      HitRec& out, HitBary* bary, bool& certified, int* stack, int sstride, Stats& st,
+DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, const float time, const bool fin,
+                      float& nearest, HitRec& out, HitBary* bary, bool& certified, int* stack, int sstride, Stats& st,
                       const float tcert) {
     const float eps = sv.int_eps;
     const TopObject& T = sv.tops[i];
     const Geometry& g = sv.geoms[T.geom];
     f3 o2, d2;
-    transform_ray(T, o, d, time, o2, d2);
+    transform_ray(T, o, d, time, o2, d2, fin);
     bool found = false;
     int bprim = -1;
     f3 bp = mk(0, 0, 0);
@@ -614,8 +620,10 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     if (isnan3(o) || isnan3(d)) return out;
     float nearest = tmax;
     bool certified = false;
+    const bool fin = ray_finite(o, d, time);
     auto visit = [&](const int i) {
-        visit_object<EXHAUSTIVE, STATS, CERT>(sv, i, o, d, time, nearest, out, bary, certified, stack, sstride, st, tcert);
+        visit_object<EXHAUSTIVE, STATS, CERT>(sv, i, o, d, time, fin, nearest, out, bary, certified, stack, sstride, st,
+                                              tcert);
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
@@ -916,7 +924,7 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h,
     const TopObject& T = sv.tops[h.obj];
     const Geometry& g = sv.geoms[T.geom];
     f3 o2, d2;
-    transform_ray(T, o, d, time, o2, d2);
+    transform_ray(T, o, d, time, o2, d2, ray_finite(o, d, time));
     Ret ret;
     ret.matIndex = T.material;
     ret.dm = RTG_DECAL_NONE;
@@ -1571,7 +1579,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_REFILL_ATTR k_trace_refill(co
                 const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
                 if (sp + npush > kStackDepth) {
                     // overflow: the whole entry again through visit_object (reference-tree walk)
-                    visit_object<false, STATS, false>(sv, ent, o, d, time, nearest, out, RTG_HIT_STORED ? &hb : nullptr,
+                    visit_object<false, STATS, false>(sv, ent, o, d, time, ray_finite(o, d, time), nearest, out, RTG_HIT_STORED ? &hb : nullptr,
                                                       dummy_cert, stack, ss, st, -INFINITY);
                     walking = false;
                     ent++;
@@ -1608,7 +1616,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_REFILL_ATTR k_trace_refill(co
                     const TopObject& T = sv.tops[ent];
                     const Geometry& g = sv.geoms[T.geom];
                     if (g.type != RTG_OBJ_SPHERE && g.node_base >= 0 && g.sah_base >= 0) {
-                        transform_ray(T, o, d, time, o2, d2);
+                        transform_ray(T, o, d, time, o2, d2, ray_finite(o, d, time));
                         const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
                         const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f &&
                                           adz >= 1e-30f && adz <= 1e30f;
@@ -1643,7 +1651,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_REFILL_ATTR k_trace_refill(co
                             break;
                         }
                     }
-                    visit_object<false, STATS, false>(sv, ent, o, d, time, nearest, out, RTG_HIT_STORED ? &hb : nullptr,
+                    visit_object<false, STATS, false>(sv, ent, o, d, time, ray_finite(o, d, time), nearest, out, RTG_HIT_STORED ? &hb : nullptr,
                                                       dummy_cert, stack, ss, st, -INFINITY);
                     ent++;
                 }

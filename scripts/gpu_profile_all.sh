@@ -10,4 +10,10 @@ for wl in ${WLS:-dragon1m cornell cornell_pt bunny}; do
   SKIP_TESTS=1 BENCH_ARGS="--workload $wl $EXTRA_ARGS" bash scripts/gpu_round.sh ${P}_$wl > gpurun_out/prof_${P}_$wl.txt 2>&1 \
     || { tail -20 gpurun_out/prof_${P}_$wl.txt; exit 1; }
   tail -1 gpurun_out/prof_${P}_$wl.txt
+  # the counters just measured, then the bench line again with them (frame HBM, per-kernel rooflines)
+  python3 scripts/pmc_counters.py gpurun_out/prof_${P}_$wl gpurun_out/prof_${P}_$wl/counters_$wl.csv \
+      gpurun_out/prof_${P}_$wl/counters_$wl.json $wl || exit 1
+  RTG_COUNTERS_DIR=gpurun_out/prof_${P}_$wl timeout -k 10 600 python3 bench.py --workload $wl $EXTRA_ARGS \
+      > gpurun_out/prof_${P}_$wl/bench_final.json 2> gpurun_out/prof_${P}_$wl/bench_final.err || exit 1
+  tail -c 400 gpurun_out/prof_${P}_$wl/bench_final.json
 done
