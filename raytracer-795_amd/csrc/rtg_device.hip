@@ -19,10 +19,6 @@ namespace rtg {
 #define DEV __device__ __forceinline__
 // k_shadow: 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
-#ifndef RTG_REFILL_WAVES_PER_EU
-#define RTG_REFILL_WAVES_PER_EU 4
-#endif
-#define RTG_REFILL_ATTR __attribute__((amdgpu_waves_per_eu(RTG_REFILL_WAVES_PER_EU)))
 // k_shadow's certified early exit (closest_hit CERT), off by default: measured on the 1080p64
 // dragon (round 3, scripts/gpu_ab3.sh, same box) it cuts a blocked query's node steps 18.9 ->
 // 14.4 (all queries 8.81 -> 7.93) but k_shadow takes 12.9 instead of 12.4 ms per frame -- the
@@ -1423,258 +1419,6 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
     }
 }
 
-// ------------------------------------------------------------------ closest hit with lane refill
-// Experiment (VERDICT r2 "per-lane ray refill", env RTG_REFILL=1): a persistent while-while
-// version of k_trace.  Each lane owns one ray at a time; a lane whose ray is finished takes the
-// next ray index from the launch's counter (one atomic per wave, when at least `refill_min` lanes
-// are idle) and keeps walking, so a wave no longer waits for its slowest ray before new rays
-// start.  The ray's state is resumable at SAH-node granularity: the top-level entry loop
-// (src/Helper.cpp:32-73) advances per lane; a mesh entry on the SAH traversal tree is walked one
-// node per iteration; every other entry (spheres, root leaves, non-fast rays, the reference-tree
-// walk) is visited whole by visit_object, as is an entry whose stack would overflow (restarted
-// from its root: the same winner).  Same results as k_trace bit for bit (the entry order, the
-// candidate keys and the acceptance are the same; only the interleaving across lanes changes).
-template <bool GEN, bool STATS>
-__global__ void __launch_bounds__(kTraceBlock) RTG_REFILL_ATTR k_trace_refill(const SceneView sv, const RayQ rays, HitRec* __restrict__ hits,
-                                                              int n, unsigned* next_ray, Counters* ctr,
-                                                              const CameraDev cam, const PassDev ps, uint64_t seed,
-                                                              int refill_min) {
-    __shared__ int s_stack[kStackDepth * kTraceBlock];
-    int* stack = s_stack + threadIdx.x;
-    constexpr int ss = kTraceBlock;
-    const int lane = threadIdx.x & 63;
-    const unsigned long long lt = __lanemask_lt();
-    const float eps = sv.int_eps;
-    const float tlo = -(fabsf(eps) + 1e-6f);
-    const HitPlanes hp = hit_planes(hits, n);
-    Stats st = {0, 0, 0};
-    unsigned long long slots = 0;     // STATS: wave iterations x 64 (lane slots)
-    int idx = -1;                     // this lane's ray (-1: none)
-    bool more = true;                 // wave-uniform: the counter may still hand out rays
-    f3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-    float time = 0.0f;
-    int ent = 0;                      // next top-level entry of the ray
-    float nearest = FLT_MAX;
-    HitRec out;
-    out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
-    HitBary hb = {0.0f, 0.0f, 0.0f};
-    // the SAH walk of entry `ent` in progress
-    bool walking = false;
-    f3 o2 = mk(0, 0, 0), d2 = mk(0, 0, 0), inv = mk(0, 0, 0);
-    float thi = 0.0f, thi0 = 0.0f, inv_dn = 0.0f, best_d = FLT_MAX;
-    int best_leaf = -1, bprim = -1, sp = 0, cur = 0;
-    float bt = 0.0f, bb = 0.0f, bg = 0.0f;
-    bool found = false;
-    bool dummy_cert = false;
-    auto store = [&]() {
-        hp.id[idx] = make_int2(out.obj, out.prim);
-        if (RTG_HIT_STORED) {
-            hp.pt[idx] = hb.pt;
-            if (sv.bary) hp.bg[idx] = make_float2(hb.beta, hb.gamma);
-        }
-    };
-    while (true) {
-        // refill the idle lanes (wave-uniform decision, one atomic per wave)
-        const unsigned long long idle = __ballot(idx < 0);
-        const int nidle = __popcll(idle);
-        if (more && (nidle >= refill_min || nidle == 64)) {
-            const int leader = __builtin_ctzll(idle);
-            unsigned base = 0;
-            if (lane == leader) base = atomicAdd(next_ray, (unsigned)nidle);
-            base = __shfl(base, leader);
-            if (base + (unsigned)nidle >= (unsigned)n) more = false;
-            if (idx < 0) {
-                const unsigned r = base + (unsigned)__popcll(idle & lt);
-                if (r < (unsigned)n) {
-                    idx = (int)r;
-                    if (GEN) primary_ray(cam, ps, seed, idx, o, d, time);
-                    else load_ray(rays, idx, o, d, time);
-                    ent = 0; nearest = FLT_MAX; walking = false;
-                    out.obj = -1; out.prim = -1; out.t = 0.0f;
-                    hb.pt = hb.beta = hb.gamma = 0.0f;
-                    if (isnan3(o) || isnan3(d)) { store(); idx = -1; }   // src/Helper.cpp:28-30
-                }
-            }
-        }
-        if (__ballot(idx >= 0) == 0ull) {
-            if (!more) break;
-            continue;
-        }
-        if (STATS) slots += 64;
-        if (idx >= 0) {
-            bool done_entry = false;
-            if (walking) {                          // one node of the entry's SAH walk
-                if (STATS) { st.nodes += 4; st.steps++; }
-                const Node4 nd = sv.snodes[cur];
-                const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
-                const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
-                const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
-                const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
-                const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
-                const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
-                const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
-                const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
-                float key[4];
-                int okm = 0, leafm = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
-                    const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
-                    const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
-                    const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                    const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                    const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
-                    const float lo = le - e, hi = sl + e;
-                    key[j] = lo;
-                    const bool ok = inf[j] >= 0 && !(hi < lo || hi < tlo || lo > thi);
-                    okm |= ok << j;
-                    leafm |= (inf[j] > 0) << j;
-                }
-                float k4[4];
-                int r4[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const bool take = ((okm >> j) & 1) && !((leafm >> j) & 1);
-                    k4[j] = take ? fminf(key[j], FLT_MAX) : INFINITY;
-                    r4[j] = take ? rf[j] : -1;
-                }
-                int leaf_mask = okm & leafm;
-                while (leaf_mask) {
-                    const int j = __builtin_ctz(leaf_mask);
-                    leaf_mask &= leaf_mask - 1;
-                    const float kj = j == 0 ? key[0] : j == 1 ? key[1] : j == 2 ? key[2] : key[3];
-                    if (kj > thi) continue;
-                    const int start = j == 0 ? rf[0] : j == 1 ? rf[1] : j == 2 ? rf[2] : rf[3];
-                    const int cnt = j == 0 ? inf[0] : j == 1 ? inf[1] : j == 2 ? inf[2] : inf[3];
-                    for (int q = start; q < start + cnt; q++) {
-                        const TriGeom tg = sv.stris[q];
-                        if (STATS) st.tris++;
-                        const Cand c = tri_test(tg, o2, d2, eps);
-                        if (!c.ok) continue;
-                        const float dist = norm(c.p - o2);
-                        const int k = __float_as_int(tg.p2.y), lstart = __float_as_int(tg.p2.z);
-                        if (!(dist < FLT_MAX && (dist < best_d || (dist == best_d && (lstart > best_leaf ||
-                                                                                      (lstart == best_leaf && k < bprim))))))
-                            continue;
-                        if (__float_as_int(tg.p2.w)) {          // src/BVH.cpp:178 on the leaf's parent
-                            const float* gb = sv.gates + 6 * (size_t)k;
-                            if (!box_hit(o2, d2, inv, true, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) continue;
-                        }
-                        best_d = dist; best_leaf = lstart; bprim = k; found = true;
-                        bt = c.t; bb = c.beta; bg = c.gamma;
-                        thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (k4[j] > thi) { k4[j] = INFINITY; r4[j] = -1; }
-                auto ce = [&](int a, int b) {
-                    const bool sw = k4[b] < k4[a];
-                    const float ka = k4[a], kb = k4[b];
-                    const int ra = r4[a], rb = r4[b];
-                    k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
-                    r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
-                };
-                ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-                const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
-                if (sp + npush > kStackDepth) {
-                    // overflow: the whole entry again through visit_object (reference-tree walk)
-                    visit_object<false, STATS, false>(sv, ent, o, d, time, ray_finite(o, d, time), nearest, out, RTG_HIT_STORED ? &hb : nullptr,
-                                                      dummy_cert, stack, ss, st, -INFINITY);
-                    walking = false;
-                    ent++;
-                } else {
-                    if (r4[3] >= 0) { stack[sp * ss] = r4[3]; sp++; }
-                    if (r4[2] >= 0) { stack[sp * ss] = r4[2]; sp++; }
-                    if (r4[1] >= 0) { stack[sp * ss] = r4[1]; sp++; }
-                    if (r4[0] >= 0) {
-                        cur = r4[0];
-                    } else if (sp == 0) {
-                        walking = false;
-                        done_entry = true;
-                    } else {
-                        sp--;
-                        cur = stack[sp * ss];
-                    }
-                }
-                if (done_entry) {                   // the entry's winner against the top level
-                    if (found) {
-                        const f3 bp = o2 + d2 * bt;
-                        const float t = gett(o2, d2, bp);
-                        if (t > 0 && (t < nearest || (t == nearest && ent < out.obj))) {   // src/Helper.cpp:43, 64
-                            nearest = t;
-                            out.obj = ent; out.prim = bprim; out.t = t;
-                            hb.pt = bt; hb.beta = bb; hb.gamma = bg;
-                        }
-                    }
-                    ent++;
-                }
-            }
-            if (!walking) {
-                // the next entries, until one starts a SAH walk or the ray is done
-                while (ent < sv.num_tops) {
-                    const TopObject& T = sv.tops[ent];
-                    const Geometry& g = sv.geoms[T.geom];
-                    if (g.type != RTG_OBJ_SPHERE && g.node_base >= 0 && g.sah_base >= 0) {
-                        transform_ray(T, o, d, time, o2, d2, ray_finite(o, d, time));
-                        const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
-                        const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f &&
-                                          adz >= 1e-30f && adz <= 1e30f;
-                        if (fast) {
-                            inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
-                            if (!box_hit(o2, d2, inv, true, g.root_min[0], g.root_min[1], g.root_min[2], g.root_max[0],
-                                         g.root_max[1], g.root_max[2])) {
-                                ent++;
-                                continue;
-                            }
-                            // the window of visit_object (same expressions: same pruning)
-                            float boundD = FLT_MAX;
-                            const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
-                            const float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
-                            if (nearest < FLT_MAX) {
-                                const float dl = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
-                                if (da != 0.0f) {
-                                    const float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * (1.0f + 1e-5f);
-                                    boundD = tm * dl * (1.0f + 2e-5f) + 1e-30f;
-                                    if (!(boundD == boundD)) boundD = FLT_MAX;
-                                }
-                            }
-                            const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
-                            inv_dn = __builtin_amdgcn_rcpf(dnorm);
-                            thi = INFINITY;
-                            if (boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
-                            thi0 = thi;
-                            best_d = FLT_MAX; best_leaf = -1; bprim = -1; found = false;
-                            bt = bb = bg = 0.0f;
-                            sp = 0; cur = g.sah_base;
-                            walking = true;
-                            break;
-                        }
-                    }
-                    visit_object<false, STATS, false>(sv, ent, o, d, time, ray_finite(o, d, time), nearest, out, RTG_HIT_STORED ? &hb : nullptr,
-                                                      dummy_cert, stack, ss, st, -INFINITY);
-                    ent++;
-                }
-                if (!walking) { store(); idx = -1; }
-            }
-        }
-    }
-    if (STATS) {
-        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
-        for (int off = 32; off > 0; off >>= 1) {
-            nv += __shfl_down(nv, off);
-            nt += __shfl_down(nt, off);
-            ns += __shfl_down(ns, off);
-        }
-        if (lane == 0) {
-            atomicAdd(&ctr->node_visits, nv);
-            atomicAdd(&ctr->tri_tests, nt);
-            atomicAdd(&ctr->trace_lane_slots, slots);
-            atomicAdd(&ctr->trace_steps, ns);
-        }
-    }
-}
-
 struct QRay { f3 o, d; float time; };      // a child ray on its way to the next level's queue
 DEV QRay make_ray(f3 o, f3 d, float time) {
     QRay r;
@@ -2571,24 +2315,12 @@ __global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const R
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 
 void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
-                  hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed, bool compact,
-                  unsigned* refill_ctr, int refill_min, int refill_waves) {
+                  hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed, bool compact) {
     if (n <= 0) return;
     dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
     const CameraDev cam = gen_cam ? *gen_cam : CameraDev{};
     const PassDev ps = gen_ps ? *gen_ps : PassDev{};
     const bool tl = sv.tlas_root >= 0;
-    if (refill_ctr && compact && !exhaustive && !tl) {      // persistent lane-refill experiment (RTG_REFILL)
-        const dim3 gp(std::min(nblk(n, kTraceBlock), std::max(refill_waves, 1)));
-        if (gen_cam) {
-            if (ctr) hipLaunchKernelGGL((k_trace_refill<true, true>), gp, b, 0, st, sv, rays, hits, n, refill_ctr, ctr, cam, ps, seed, refill_min);
-            else hipLaunchKernelGGL((k_trace_refill<true, false>), gp, b, 0, st, sv, rays, hits, n, refill_ctr, ctr, cam, ps, seed, refill_min);
-        } else {
-            if (ctr) hipLaunchKernelGGL((k_trace_refill<false, true>), gp, b, 0, st, sv, rays, hits, n, refill_ctr, ctr, cam, ps, seed, refill_min);
-            else hipLaunchKernelGGL((k_trace_refill<false, false>), gp, b, 0, st, sv, rays, hits, n, refill_ctr, ctr, cam, ps, seed, refill_min);
-        }
-        return;
-    }
 #define RTG_TRACE(EX, STA, GEN)                                                                                   \
     do {                                                                                                          \
         if (tl) hipLaunchKernelGGL((k_trace<EX, STA, GEN, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact); \

@@ -719,9 +719,8 @@ struct Lane {
     hipEvent_t ev_count = nullptr;          // recorded after the level count copy
     hipEvent_t ev_t[5] = {};                // trace start, trace end, shade end, shadow start, shadow end
     unsigned long long* h_count = nullptr;  // pinned host slot
-    DBuf qcnt;                              // 192 x u64 per pass: [level] next rays | shadow entries << 32,
-                                            // [64 + level] non-final nodes (k_resolve's list length),
-                                            // [128 + level] the lane-refill kernel's ray counter
+    DBuf qcnt;                              // 128 x u64 per pass: [level] next rays | shadow entries << 32,
+                                            // [64 + level] non-final nodes (k_resolve's list, RTG_RESOLVE_LIST)
     std::vector<Level> levels;
     // current pass
     std::vector<int> passes;                // indices into the frame's pass list (this lane's, in order)
@@ -1595,11 +1594,6 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     // row strips, so each holds a mix of sky, floor and glass).  4 / 8 / 32 / 64 tiles: in between.
     int tile_s = 16;
     if (const char* e = getenv("RTG_TILE_S")) tile_s = std::max(1, std::min(1 << 12, atoi(e)));
-    // persistent lane-refill closest hit (experiment): RTG_REFILL=1, idle lanes before a
-    // wave refills (RTG_REFILL_MIN), persistent waves per launch (RTG_REFILL_WAVES)
-    const bool refill = getenv("RTG_REFILL") && atoi(getenv("RTG_REFILL")) == 1;
-    const int refill_min = getenv("RTG_REFILL_MIN") ? std::max(1, std::min(64, atoi(getenv("RTG_REFILL_MIN")))) : 16;
-    const int refill_waves = getenv("RTG_REFILL_WAVES") ? std::max(1, atoi(getenv("RTG_REFILL_WAVES"))) : 4096;
     // tile_pixel (device) forms band * (tile_h * tile_s * nx) in 32-bit ints: keep one band of the
     // widest tiles (tile_h <= 8) below 2^31 pixels
     if ((long long)8 * cam->nx >= (1LL << 31)) return fail(RTG_ERR_UNSUPPORTED, "image wider than 2^28 pixels");
@@ -1662,9 +1656,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         // level 0: k_trace / k_shade / k_pt_shade regenerate the primary rays (no level-0 ray buffer)
         const bool gen = level == 0;
         launch_trace(sv, cur_q, Lc.hits.as<HitRec>(), n, exhaustive, sctr, ln.st,
-                     gen ? &cd : nullptr, gen ? &ps : nullptr, o.seed, /*compact=*/true,
-                     refill ? reinterpret_cast<unsigned*>(ln.qcnt.as<unsigned long long>() + 128 + level) : nullptr,
-                     refill_min, refill_waves);
+                     gen ? &cd : nullptr, gen ? &ps : nullptr, o.seed, /*compact=*/true);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
         if (pt)
             launch_pt_shade(sv, cd, level, ps, o.seed, cur_q,
@@ -1700,8 +1692,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const PassDev& ps = plist[ln.pass];
         const int n0 = ps.ns * ps.npass;
         int rc2;
-        if ((rc2 = ln.qcnt.grow(sizeof(unsigned long long) * 192))) return rc2;
-        HIP_TRY(hipMemsetAsync(ln.qcnt.p, 0, sizeof(unsigned long long) * 192, ln.st));
+        if ((rc2 = ln.qcnt.grow(sizeof(unsigned long long) * 128))) return rc2;
+        HIP_TRY(hipMemsetAsync(ln.qcnt.p, 0, sizeof(unsigned long long) * 128, ln.st));
         ln.counts.assign(1, n0);
         ln.level = 0;
         if ((int)ln.levels.size() < 1) ln.levels.resize(1);

@@ -330,12 +330,9 @@ struct Counters {
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
 struct LevelBuffers;
 // gen_cam / gen_ps non-null: level 0 (either integrator), rays are generated in the kernel
-// refill_ctr non-null (render path, no TLAS): the persistent lane-refill kernel (RTG_REFILL experiment);
-// *refill_ctr must be 0 at launch
 void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
-                  uint64_t seed = 0, bool compact = false, unsigned* refill_ctr = nullptr, int refill_min = 16,
-                  int refill_waves = 4096);
+                  uint64_t seed = 0, bool compact = false);
 // rlist / rcount: the level's non-final nodes (levels >= 1), appended for k_resolve
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
