@@ -467,7 +467,13 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             // Exhaustive traversal, rays with a zero / denormal / huge direction component and
             // a stack that would overflow (> kStackDepth entries) use the reference tree's BVH2
             // walk; candidates already accepted stay valid (they are reachable).
-            bool use2 = EXHAUSTIVE || !fast || g.sah_base < 0;
+            // the quantised tree also needs moderate coordinates and direction components (every t term
+            // a finite normal float, rtg_internal.h kQCoordMax / kQDirMax)
+            const bool qfast = !RTG_QNODES ||
+                               (adx >= 1.0f / kQDirMax && adx <= kQDirMax && ady >= 1.0f / kQDirMax && ady <= kQDirMax &&
+                                adz >= 1.0f / kQDirMax && adz <= kQDirMax && fabsf(o2.x) < kQCoordMax &&
+                                fabsf(o2.y) < kQCoordMax && fabsf(o2.z) < kQCoordMax);
+            bool use2 = EXHAUSTIVE || !fast || !qfast || g.sah_base < 0;
             if (!use2) {
                 // CERT: tau bounds gett()'s rounding (4u |o_a| / |d_a|, as the object-loop bound
                 // above) with a 4x margin: a candidate with t > tau has gett() > 0
@@ -503,7 +509,25 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                 int sp = 0;
                 int cur = g.sah_base;
                 while (true) {
-                    if (STATS) { st.nodes += 4; st.steps++; }   // one 128-B node = four 32-B child records
+                    if (STATS) { st.nodes += 4; st.steps++; }   // one node = four 32-B child records (the model's unit)
+#if RTG_QNODES
+                    // 64-byte quantised node: t of slot j's plane q on axis a = fma(q, s_a / d_a, (o_a - O_a) / d_a)
+                    const Node4q nq = sv.qnodes[cur];
+                    const float Ax = (__uint_as_float(nq.a.x) - o2.x) * inv.x;
+                    const float Ay = (__uint_as_float(nq.a.y) - o2.y) * inv.y;
+                    const float Az = (__uint_as_float(nq.a.z) - o2.z) * inv.z;
+                    const float Sx = __uint_as_float((nq.a.w & 0xFFu) << 23) * inv.x;
+                    const float Sy = __uint_as_float(((nq.a.w >> 8) & 0xFFu) << 23) * inv.y;
+                    const float Sz = __uint_as_float(((nq.a.w >> 16) & 0xFFu) << 23) * inv.z;
+                    const int rf[4] = {(int)nq.d.x, (int)nq.d.y, (int)nq.d.z, (int)nq.d.w};
+                    int inf[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int b8 = (int)((nq.c.z >> (8 * j)) & 0xFFu);
+                        inf[j] = b8 == 255 ? -1 : b8;
+                    }
+                    auto qb = [](unsigned w, int j) { return (float)((w >> (8 * j)) & 0xFFu); };
+#else
                     const Node4 nd = sv.snodes[cur];
                     const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
                     const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
@@ -513,13 +537,20 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
                     const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
                     const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
+#endif
                     float key[4];
                     int okm = 0, leafm = 0;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
+#if RTG_QNODES
+                        const float ax = __builtin_fmaf(qb(nq.b.x, j), Sx, Ax), bx = __builtin_fmaf(qb(nq.b.w, j), Sx, Ax);
+                        const float ay = __builtin_fmaf(qb(nq.b.y, j), Sy, Ay), by = __builtin_fmaf(qb(nq.c.x, j), Sy, Ay);
+                        const float az = __builtin_fmaf(qb(nq.b.z, j), Sz, Az), bz = __builtin_fmaf(qb(nq.c.y, j), Sz, Az);
+#else
                         const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
                         const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
                         const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
+#endif
                         const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
                         const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
                         const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20

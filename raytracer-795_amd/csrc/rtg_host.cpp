@@ -507,6 +507,73 @@ int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad
     return me;
 }
 
+// Node4 -> Node4q (rtg_internal.h).  Per axis: step s = the smallest power of 2 with
+// s >= extent / 251, s >= max|coordinate| * 2^-21 (the device's float rounding stays far below one
+// step) and s >= 2^-60; origin = (float) <= min - 2 s; then each slot's plane is rounded outwards to
+// the grid and moved one further step out: qlo = floor((lo - origin) / s) - 1,
+// qhi = ceil((hi - origin) / s) + 1 (exact in double: the values are floats, s a power of 2).
+// That extra step covers the device's error in t = fma(q, s / d, (origin - O) / d), which is below
+// 4 ulp of |t| + 255 |s / d| (the 2^-20 relative margin of the slab test covers the first term, the
+// step the second).  False when a coordinate is not finite, exceeds kQCoordMax or needs a step
+// beyond 2^50: the mesh then keeps the reference-tree walk.
+bool quantize_node4(const Node4& n, Node4q& out) {
+    const float lo[3][4] = {{n.lox.x, n.lox.y, n.lox.z, n.lox.w}, {n.loy.x, n.loy.y, n.loy.z, n.loy.w},
+                            {n.loz.x, n.loz.y, n.loz.z, n.loz.w}};
+    const float hi[3][4] = {{n.hix.x, n.hix.y, n.hix.z, n.hix.w}, {n.hiy.x, n.hiy.y, n.hiy.z, n.hiy.w},
+                            {n.hiz.x, n.hiz.y, n.hiz.z, n.hiz.w}};
+    const int info[4] = {n.info.x, n.info.y, n.info.z, n.info.w};
+    uint32_t w[16] = {};
+    uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0}, inf8 = 0, exps = 0;
+    for (int j = 0; j < 4; j++) {
+        const uint32_t b = info[j] < 0 ? 255u : (uint32_t)info[j];
+        if (info[j] > 254) return false;
+        inf8 |= b << (8 * j);
+    }
+    for (int z = 0; z < 3; z++) {
+        double mn = 1e300, mx = -1e300;
+        for (int j = 0; j < 4; j++) {
+            if (info[j] < 0) continue;
+            if (!std::isfinite(lo[z][j]) || !std::isfinite(hi[z][j])) return false;
+            if (std::fabs(lo[z][j]) > kQCoordMax || std::fabs(hi[z][j]) > kQCoordMax) return false;
+            mn = std::min(mn, (double)lo[z][j]);
+            mx = std::max(mx, (double)hi[z][j]);
+        }
+        if (mn > mx) { mn = 0.0; mx = 0.0; }            // no slot in use
+        const double need = std::max({(mx - mn) / 251.0, std::max(std::fabs(mn), std::fabs(mx)) * std::ldexp(1.0, -21),
+                                      std::ldexp(1.0, -60)});
+        int e = 0;
+        std::frexp(need, &e);                           // need < 2^e
+        if (e > 50) return false;
+        const double step = std::ldexp(1.0, e);
+        float org = (float)(mn - 2.0 * step);
+        if ((double)org > mn - 2.0 * step) org = std::nextafter(org, -FLT_MAX);
+        for (int j = 0; j < 4; j++) {
+            uint32_t ql = 255u, qh = 0u;               // empty slot: an inverted box
+            if (info[j] >= 0) {
+                const double a = std::floor(((double)lo[z][j] - org) / step) - 1.0;
+                const double b = std::ceil(((double)hi[z][j] - org) / step) + 1.0;
+                if (a < 0.0 || b > 255.0) return false;
+                ql = (uint32_t)a; qh = (uint32_t)b;
+            }
+            qlo[z] |= ql << (8 * j);
+            qhi[z] |= qh << (8 * j);
+        }
+        memcpy(&w[z], &org, 4);
+        exps |= (uint32_t)(e + 127) << (8 * z);      // float exponent field of 2^e
+    }
+    w[3] = exps;
+    w[4] = qlo[0]; w[5] = qlo[1]; w[6] = qlo[2];
+    w[7] = qhi[0]; w[8] = qhi[1]; w[9] = qhi[2];
+    w[10] = inf8;
+    const int ref[4] = {n.ref.x, n.ref.y, n.ref.z, n.ref.w};
+    memcpy(&w[12], ref, 16);
+    out.a = make_uint4(w[0], w[1], w[2], w[3]);
+    out.b = make_uint4(w[4], w[5], w[6], w[7]);
+    out.c = make_uint4(w[8], w[9], w[10], w[11]);
+    out.d = make_uint4(w[12], w[13], w[14], w[15]);
+    return true;
+}
+
 // ------------------------------------------------------------------ top-level BVH (TLAS)
 // World box of one top-level entry: its geometry's root range box expanded by the eps overhang
 // of its candidates (prune_pad: an accepted triangle point may lie outside its triangle), mapped
@@ -875,7 +942,8 @@ static void bind_view(rtg_scene* s) {
     sv.tops = s->d_tops.as<TopObject>();
     sv.geoms = s->d_geoms.as<Geometry>();
     sv.nodes = s->d_nodes.as<Node>();
-    sv.snodes = s->d_nodes4.as<Node4>();
+    sv.snodes = s->d_nodes4.as<Node4>();      // one of the two, per RTG_QNODES
+    sv.qnodes = s->d_nodes4.as<Node4q>();
     sv.stris = s->d_stris.as<TriGeom>();
     sv.gates = s->d_gates.as<float>();
     sv.tris = s->d_tris.as<TriGeom>();
@@ -970,6 +1038,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     std::vector<Geometry> geoms(d->num_objects);
     std::vector<Node> dnodes;
     std::vector<Node4> snodes;               // traversal trees (SAH, 4-wide)
+    std::vector<Node4q> qnodes;              // ... quantised (RTG_QNODES; uploaded instead of snodes)
     std::vector<TriGeom> stris;              // their triangles, SAH leaf order (p2 = ref position / leaf / gated)
     std::vector<float> gates;                // per reference position: its leaf's parent box
     std::vector<TriGeom> tris;
@@ -1181,7 +1250,23 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                     memcpy(&t.p2.w, &gt, 4);
                     stris.push_back(t);
                 }
+                const size_t first = snodes.size();
                 g.sah_base = sah_collapse(bn, 0, tri_base, pad, snodes);
+                if (RTG_QNODES) {
+                    // the quantised copy; a node that cannot be quantised drops the mesh's tree
+                    bool qok = true;
+                    for (size_t k = first; k < snodes.size() && qok; k++) {
+                        Node4q q;
+                        qok = quantize_node4(snodes[k], q);
+                        if (qok) qnodes.push_back(q);
+                    }
+                    if (!qok) {
+                        qnodes.resize(first);
+                        snodes.resize(first);
+                        stris.resize(tri_base);
+                        g.sah_base = -1;
+                    }
+                }
             }
         }
         if (ob.root < 0) {
@@ -1375,7 +1460,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     if (d->num_texcoords > 0) tcflat.assign(d->texcoords, d->texcoords + 2 * (size_t)d->num_texcoords);
     int rc;
     if ((rc = upload(s->d_tops, tops)) || (rc = upload(s->d_geoms, geoms)) || (rc = upload(s->d_nodes, dnodes)) ||
-        (rc = upload(s->d_nodes4, snodes)) || (rc = upload(s->d_stris, stris)) || (rc = upload(s->d_gates, gates)) ||
+        (rc = (RTG_QNODES ? upload(s->d_nodes4, qnodes) : upload(s->d_nodes4, snodes))) || (rc = upload(s->d_stris, stris)) || (rc = upload(s->d_gates, gates)) ||
         (rc = upload(s->d_tris, tris)) || (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_vertices, vflat)) ||
         (rc = upload(s->d_vnormals, s->vnormals)) || (rc = upload(s->d_texcoords, tcflat)) ||
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||

@@ -78,6 +78,26 @@ struct Node4 {
     int4 info;
 };
 
+// The same node quantised to 64 bytes (RTG_QNODES, rtg_host.cpp quantize_node4): per axis a power-of-2
+// step s_a (biased exponent byte) and an origin o_a; slot j's box on axis a is
+// [o_a + qlo_aj s_a, o_a + qhi_aj s_a] with 8-bit qlo / qhi, rounded outwards on the host by one
+// more step than needed, which covers the rounding of the device's t = fma(q, s_a / d_a, (o_a - O_a) / d_a)
+// (DESIGN.md §4).  Boxes are pruning filters only (reachability uses the exact gates[]), so a
+// conservative box keeps every result bit-identical.
+//   w[0..2] origin xyz (float bits), w[3] bytes 0-2: step exponents (float exponent field)
+//   w[4..6] qlo per axis (byte j = slot j), w[7] qhi x, w[8..9] qhi y, z
+//   w[10] info per slot (byte: 0 interior, 1..254 leaf count, 255 empty), w[11] unused, w[12..15] ref
+struct Node4q {
+    uint4 a, b, c, d;
+};
+#ifndef RTG_QNODES
+#define RTG_QNODES 1
+#endif
+// quantised-tree eligibility: object-space coordinates below this, direction components within
+// [1/kQDirMax, kQDirMax], steps within [2^-60, 2^50] (so every t term stays a finite normal float)
+constexpr float kQCoordMax = 1e15f;
+constexpr float kQDirMax = 1e16f;
+
 // Triangle in BVH order: the Cramer-rule operands of Triangle::bvhIntersect
 // (src/Shape.cpp:299-316): a, a-b, a-c.  w lanes: x = original face index.
 struct TriGeom {
@@ -123,6 +143,7 @@ struct SceneView {
     const Geometry* geoms;
     const Node* nodes;
     const Node4* snodes;           // traversal trees (SAH, 4-wide)
+    const Node4q* qnodes;          // the same trees quantised (RTG_QNODES)
     const TriGeom* stris;          // their triangles in leaf order; p2.y = reference position (int bits),
                                    // p2.z = first position of its reference leaf, p2.w = 1 if gated
     const float* gates;            // per reference position: min xyz, max xyz of its leaf's parent box
