@@ -90,8 +90,11 @@ struct Node4 {
 struct Node4q {
     uint4 a, b, c, d;
 };
+// Off: measured bit-identical but slower (1080p64 dragon k_trace 13.1 -> 14.1, k_shadow 12.3 -> 12.6 ms;
+// cornell k_shadow 6.4 -> 7.9 ms; profiles/r3_ab_qnodes.jsonl) -- the looser boxes add 4-6 % node steps
+// and the decode VALU work, while the halved node bytes buy nothing: the walk is not bound by node traffic.
 #ifndef RTG_QNODES
-#define RTG_QNODES 1
+#define RTG_QNODES 0
 #endif
 // quantised-tree eligibility: object-space coordinates below this, direction components within
 // [1/kQDirMax, kQDirMax], steps within [2^-60, 2^50] (so every t term stays a finite normal float)
