@@ -1,5 +1,5 @@
 """Ray sets for the full-size parity tests (tests/test_gpu_fullsize.py): rays of the kinds the
-render loop traces on the BASELINE headline scene (C3 dragon1m, 1,000,004 triangles), built from
+render loop traces on the BASELINE headline scene (C3 dragon1m, 1,000,002 triangles + 2 spheres), built from
 the scene's own camera, light and the oracle's hit records:
 
   camera     pixel centres + jitter of the 1920x1080 camera (Camera::getPrimaryRay /

@@ -1,6 +1,6 @@
 """Oracle parity at the BASELINE configs' real sizes (VERDICT r2 "What's missing" #1).
 
-* C3 dragon1m, the headline scene at full size (1,000,004 triangles): >= 100 K rays of every
+* C3 dragon1m, the headline scene at full size (1,000,002 triangles + 2 spheres): >= 100 K rays of every
   kind the render loop traces (fullsize_rays.py) through rtg_trace_closest, bit-exact against
   orc_trace -- object / primitive / material indices, t, point and normal bits -- on both
   traversal trees (the SAH 4-wide tree with the reachability gate, and the reference
