@@ -27,6 +27,25 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT
 #define RTG_SHADOW_CERT 0
 #endif
+// Traversal blocks (one wave each) are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+// "Workgroup dispatch"), so consecutive ray blocks -- neighbouring pixels, whose rays walk the same
+// nodes -- land on different L2s.  RTG_XCD_CHUNK = G > 1 renumbers them so the blocks sharing an
+// XCD take runs of G consecutive ray blocks while the eight XCDs still work inside one window of
+// 8G blocks (dispatch order); bijective (the last partial window keeps its own numbering).
+#ifndef RTG_XCD_CHUNK
+#define RTG_XCD_CHUNK 1
+#endif
+__device__ __forceinline__ int ray_block() {
+#if RTG_XCD_CHUNK > 1
+    constexpr int G = RTG_XCD_CHUNK;
+    const int w = blockIdx.x, full = (int)gridDim.x / (8 * G) * (8 * G);
+    if (w >= full) return w;
+    const int q = w >> 3, x = w & 7;
+    return ((q / G) * 8 + x) * G + q % G;
+#else
+    return blockIdx.x;
+#endif
+}
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
 // 34.0 -> 29.7 ms); the simple variants already fit 4 waves (no-op for them)
@@ -1405,7 +1424,7 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const
                                                        bool compact) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int i = ray_block() * kTraceBlock + threadIdx.x;
     Stats st = {0, 0, 0};
     if (i < n) {
         f3 o, d;
@@ -1984,7 +2003,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        unsigned* nan_queries, Counters* ctr) {
     __shared__ int s_stack[kStackDepth * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = ray_block() * kTraceBlock + threadIdx.x;
     unsigned nanq = 0;
     Stats st = {0, 0, 0};
     bool was_blocked = false;

@@ -13,6 +13,9 @@ for wl in ${WLS:-dragon1m cornell cornell_pt bunny}; do
   # the counters just measured, then the bench line again with them (frame HBM, per-kernel rooflines)
   python3 scripts/pmc_counters.py gpurun_out/prof_${P}_$wl gpurun_out/prof_${P}_$wl/counters_$wl.csv \
       gpurun_out/prof_${P}_$wl/counters_$wl.json $wl || exit 1
+  # the raw per-dispatch CSVs are tens of MB per workload (gpurun copies back <= 64 MiB): keep the
+  # per-kernel summaries only
+  rm -rf gpurun_out/prof_${P}_$wl/p[1-9] gpurun_out/prof_${P}_$wl/kt/kt_kernel_trace.csv
   RTG_COUNTERS_DIR=gpurun_out/prof_${P}_$wl timeout -k 10 600 python3 bench.py --workload $wl $EXTRA_ARGS \
       > gpurun_out/prof_${P}_$wl/bench_final.json 2> gpurun_out/prof_${P}_$wl/bench_final.err || exit 1
   tail -c 400 gpurun_out/prof_${P}_$wl/bench_final.json

@@ -26,7 +26,11 @@ for pre in ('rtg::k_trace<false, false', 'rtg::k_shade<false, false, 512, false'
         print(f"{pre + ', *> (combined)':48s} {c:6d} {t/1e6:10.2f} {t/c/1e3:9.1f}")
 PY
 cp $D/kt/kt_kernel_stats.csv profiles/${TAG}_kernel_stats.csv
-python3 scripts/pmc_counters.py $D profiles/${TAG}_counters.csv profiles/${TAG}_counters.json $WL
+if [ -f $D/counters_$WL.json ]; then     # extracted on the GPU box (gpu_profile_all.sh drops the raw CSVs)
+  cp $D/counters_$WL.csv profiles/${TAG}_counters.csv; cp $D/counters_$WL.json profiles/${TAG}_counters.json
+else
+  python3 scripts/pmc_counters.py $D profiles/${TAG}_counters.csv profiles/${TAG}_counters.json $WL
+fi
 cp profiles/${TAG}_counters.json profiles/counters_${WL}.json
 [ "$WL" = dragon1m ] && cp profiles/${TAG}_counters.json profiles/counters_current.json
 echo saved $TAG
