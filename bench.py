@@ -183,8 +183,10 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
         return names[0] if names else ""
 
     shade = first("rtg::k_pt_shade<" if pt else "rtg::k_shade<")
+    # the shadow kernel's TLAS instantiation (k_shadow<false, false, true>) runs on scenes with a
+    # top-level BVH (spheres)
     rows = [("k_trace", "rtg::k_trace<false, false, *>", "trace"),
-            ("k_shadow", "rtg::k_shadow<false, false, false>", "shadow"),
+            ("k_shadow", first("rtg::k_shadow<false, false"), "shadow"),
             ("k_pt_shade" if pt else "k_shade", shade, "shade"),
             ("k_accumulate", "rtg::k_accumulate", "accumulate")]
     if not pt:

@@ -6,7 +6,8 @@ sys.path.insert(0, os.path.join(ROOT, "raytracer-795_amd"))
 import rtg
 from rtg import scenegen
 w = sys.argv[1] if len(sys.argv) > 1 else "dragon1m"
-sc = getattr(scenegen, w)(1920, 1080, spp=256 if w == "cornell_pt" else 64)
+fn, spp = {"bunny": ("bunny5k", 1), "cornell_pt": ("cornell_pt", 256)}.get(w, (w, 64))   # bench.py's workloads
+sc = getattr(scenegen, fn)(1920, 1080, spp=spp)
 r = rtg.Renderer(sc, 0)
 r.render(0)
 ms = []

@@ -25,7 +25,7 @@ def kname(k):
 
 # Kernels whose level-0 and queued-level instantiations (last template argument) bench.py times
 # together: one combined entry each as well, `<prefix>, *>` (e.g. k_trace<false, false, *>).
-COMBINED = ("rtg::k_trace<false, false", "rtg::k_shade<false, false, 512, false", "rtg::k_shade<false, true, 512, false",
+COMBINED = ("rtg::k_trace<false, false", "rtg::k_shadow<false, false", "rtg::k_shade<false, false, 512, false", "rtg::k_shade<false, true, 512, false",
             "rtg::k_shade<true, true, 256, false", "rtg::k_shade<true, true, 256, true",
             "rtg::k_pt_shade<false, false, true", "rtg::k_pt_shade<false, false, false", "rtg::k_pt_shade<false, true, true",
             "rtg::k_pt_shade<true, true, true")
