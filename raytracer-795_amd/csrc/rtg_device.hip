@@ -27,42 +27,6 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT
 #define RTG_SHADOW_CERT 0
 #endif
-// Diagnostic builds only (DESIGN.md §4 "Compiler note"): built with packed-f32 ops enabled and
-// -DRTG_PK_ONLY=n, every kernel family but n (1 k_trace, 2 k_shadow, 3 k_shade, 4 the others)
-// is compiled without them, to find the kernel the packed form breaks.  Empty in normal builds.
-#ifdef __HIP_DEVICE_COMPILE__
-#define RTG_NOPK_ATTR __attribute__((target("no-packed-fp32-ops")))
-#else
-#define RTG_NOPK_ATTR      // a device-only feature: the host pass would warn and ignore it
-#endif
-#if defined(RTG_PK_ONLY) && RTG_PK_ONLY != 1
-#define RTG_NOPK_1 RTG_NOPK_ATTR
-#else
-#define RTG_NOPK_1
-#endif
-#if defined(RTG_PK_ONLY) && RTG_PK_ONLY != 2
-#define RTG_NOPK_2 RTG_NOPK_ATTR
-#else
-#define RTG_NOPK_2
-#endif
-#if defined(RTG_PK_ONLY) && RTG_PK_ONLY != 3
-#define RTG_NOPK_3 RTG_NOPK_ATTR
-#else
-#define RTG_NOPK_3
-#endif
-#if defined(RTG_PK_ONLY) && RTG_PK_ONLY != 4
-#define RTG_NOPK_4 RTG_NOPK_ATTR
-#else
-#define RTG_NOPK_4
-#endif
-// Diagnostic builds only: -DRTG_PK_FENCE=r puts an empty asm register fence on the values of code
-// region r (1 box_hit's fast slabs, 2 the traversal-tree node slabs, 3 tri_test, 4 box_test) so
-// the compiler cannot pair them into packed-f32 instructions there.  Empty in normal builds.
-#ifdef RTG_PK_FENCE
-#define RTG_PKF(r, x) do { if (RTG_PK_FENCE == (r)) asm volatile("" : "+v"(x)); } while (0)
-#else
-#define RTG_PKF(r, x) do { } while (0)
-#endif
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
 // 34.0 -> 29.7 ms); the simple variants already fit 4 waves (no-op for them)
@@ -178,7 +142,6 @@ DEV bool box_test(f3 o, f3 d, float mnx, float mny, float mnz, float mxx, float 
     else { tye = (mxy - o.y) / d.y; tyl = (mny - o.y) / d.y; }
     if (d.z > 0) { tze = (mnz - o.z) / d.z; tzl = (mxz - o.z) / d.z; }
     else { tze = (mxz - o.z) / d.z; tzl = (mnz - o.z) / d.z; }
-    RTG_PKF(4, txe); RTG_PKF(4, txl); RTG_PKF(4, tye); RTG_PKF(4, tyl); RTG_PKF(4, tze); RTG_PKF(4, tzl);
     float sl = min3(txl, tyl, tzl);
     float le = max3(txe, tye, tze);
     return !(sl < le);
@@ -198,7 +161,6 @@ DEV bool box_hit(f3 o, f3 d, f3 inv, bool fast_ok, float mnx, float mny, float m
         float ax = (mnx - o.x) * inv.x, bx = (mxx - o.x) * inv.x;
         float ay = (mny - o.y) * inv.y, by = (mxy - o.y) * inv.y;
         float az = (mnz - o.z) * inv.z, bz = (mxz - o.z) * inv.z;
-        RTG_PKF(1, ax); RTG_PKF(1, bx); RTG_PKF(1, ay); RTG_PKF(1, by); RTG_PKF(1, az); RTG_PKF(1, bz);
         float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
         float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
         float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
@@ -241,10 +203,8 @@ DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps) {
     f3 amc = mk(g.p1.z, g.p1.w, g.p2.x);
     f3 amo = a - o;
     Cand c;
-    RTG_PKF(3, amo.x); RTG_PKF(3, amo.y); RTG_PKF(3, amo.z);
     float det = det3(amb, amc, d);
     float nb = det3(amo, amc, d), ng = det3(amb, amo, d), nt = det3(amb, amc, amo);
-    RTG_PKF(3, det); RTG_PKF(3, nb); RTG_PKF(3, ng); RTG_PKF(3, nt);
     // Fast rejection: quotients formed with v_rcp_f32 (1 ulp) lie within 2^-21 (relative) of
     // the correctly rounded ones, so a quotient that misses the acceptance bounds by more than
     // 2^-20 of its magnitude is rejected by the exact test too.  Everything else (and any
@@ -587,10 +547,9 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                         const float ay = __builtin_fmaf(qb(nq.b.y, j), Sy, Ay), by = __builtin_fmaf(qb(nq.c.x, j), Sy, Ay);
                         const float az = __builtin_fmaf(qb(nq.b.z, j), Sz, Az), bz = __builtin_fmaf(qb(nq.c.y, j), Sz, Az);
 #else
-                        float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
-                        float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
-                        float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
-                        RTG_PKF(2, ax); RTG_PKF(2, bx); RTG_PKF(2, ay); RTG_PKF(2, by); RTG_PKF(2, az); RTG_PKF(2, bz);
+                        const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
+                        const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
+                        const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
 #endif
                         const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
                         const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
@@ -1440,7 +1399,7 @@ DEV void store_ray(const RayQ& q, int k, f3 o, f3 d, float time) {
 
 // GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no ray queue).
 template <bool EXHAUSTIVE, bool STATS, bool GEN = false, bool TLAS = false>
-__global__ void __launch_bounds__(kTraceBlock) RTG_NOPK_1 k_trace(const SceneView sv, const RayQ rays,
+__global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayQ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
                                                        const CameraDev cam, const PassDev ps, uint64_t seed,
                                                        bool compact) {
@@ -1732,7 +1691,7 @@ DEV RayMeta level_meta(const SceneView& sv, int level, const RayQ& rays, const R
 // GEN: level 0 (the primary ray of slot i, regenerated), else a queued ray -- separate
 // instantiations, so neither carries the other's live ranges.
 template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL, bool GEN = false>
-__global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR RTG_NOPK_3 k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+__global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                uint64_t seed,
                                                const RayQ rays, const RayMeta* __restrict__ meta,
                                                const HitRec* __restrict__ hits, const NodePlanes nodes,
@@ -1799,7 +1758,7 @@ constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour 
 
 // GEN: level 0 (primary rays regenerated), else queued rays (separate instantiations, as k_shade)
 template <bool FULL, bool SPOT, bool BRDF, bool GEN = false>
-__global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR RTG_NOPK_4 k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+__global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                   uint64_t seed, const RayQ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
                                                   PathRec* __restrict__ paths, const NodePlanes nodes,
@@ -1983,7 +1942,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR RTG_NOPK_4 k_pt_shade(c
 // L[slot] += T (x) v of every contributing vertex, one level at a time (stream order keeps
 // the oracle's per-sample summation order).  Level 0 starts the sum: L = (0,0,0) [+ T (x) v].
 // With several lights the in-order light sum of k_light_sum is folded in here.
-__global__ void __launch_bounds__(256) RTG_NOPK_4 k_pt_gather(const NodePlanes nodes, const PathRec* __restrict__ paths,
+__global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const PathRec* __restrict__ paths,
                                                    const ShadowPlanes shadows, int nL,
                                                    const NodePlanes level0, int level, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2018,7 +1977,7 @@ __global__ void __launch_bounds__(256) RTG_NOPK_4 k_pt_gather(const NodePlanes n
 // Each query is a full closest-hit FindIntersection, as Light::IsShadow does
 // (src/Light.cpp:188-204): the distance test below decides blocking.
 template <bool EXHAUSTIVE, bool STATS, bool TLAS = false>
-__global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR RTG_NOPK_2 k_shadow(const SceneView sv,
+__global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const SceneView sv,
                                                                        const ShadowPlanes shadows, bool lean,
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount, const NodePlanes nodes,
@@ -2187,7 +2146,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR RTG_NOPK_2 k_shad
 }
 
 // Several lights: Scene::RecursiveShading's in-order sum col = ((amb + L0) + L1) + ...
-__global__ void __launch_bounds__(256) RTG_NOPK_4 k_light_sum(const SceneView sv, const ShadowPlanes shadows,
+__global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const ShadowPlanes shadows,
                                                    const NodePlanes nodes, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -2264,7 +2223,7 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
 
 // One level of the bottom-up pass (levels >= 1; level 0 is resolved inside k_accumulate).
 // One thread per non-final node of the level (k_shade's compacted list; final nodes are not read).
-__global__ void __launch_bounds__(256) RTG_NOPK_4 k_resolve(const SceneView sv, const NodePlanes nodes, const NodePlanes child,
+__global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodePlanes nodes, const NodePlanes child,
                                                  const int* __restrict__ rlist, const unsigned* rcount, int n) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= (RTG_RESOLVE_LIST ? (int)*rcount : n)) return;
@@ -2283,7 +2242,7 @@ __global__ void __launch_bounds__(256) RTG_NOPK_4 k_resolve(const SceneView sv, 
 constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
 // Colours are read from the level-0 NodePlanes colour plane; `resolve` (Whitted only) evaluates
 // non-final level-0 nodes against level 1 first.
-__global__ void __launch_bounds__(256) RTG_NOPK_4 k_accumulate(const SceneView sv,
+__global__ void __launch_bounds__(256) k_accumulate(const SceneView sv,
                                                     const NodePlanes level0, const NodePlanes level1, bool resolve,
                                                     float* __restrict__ acc, const PassDev ps, int nx, int mode) {
     __shared__ float sr[kAccPix * kAccStride], sg[kAccPix * kAccStride], sb[kAccPix * kAccStride];
@@ -2327,7 +2286,7 @@ __global__ void __launch_bounds__(256) RTG_NOPK_4 k_accumulate(const SceneView s
     if (t < np) { acc[3 * p] = a.x; acc[3 * p + 1] = a.y; acc[3 * p + 2] = a.z; }
 }
 
-__global__ void __launch_bounds__(256) RTG_NOPK_4 k_finalize(const float* __restrict__ acc, float* __restrict__ out, int nx,
+__global__ void __launch_bounds__(256) k_finalize(const float* __restrict__ acc, float* __restrict__ out, int nx,
                                                   int ny, int row_offset, int row_stride, int row_block, int total) {
     int pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= nx * ny) return;
@@ -2344,7 +2303,7 @@ __global__ void __launch_bounds__(256) RTG_NOPK_4 k_finalize(const float* __rest
 
 // Multi-GPU gather: frame row y comes from the shard that owns it, at that shard's compact row
 // index (the rows of every shard are stacked in `recv` in rank order).
-__global__ void __launch_bounds__(256) RTG_NOPK_4 k_place_rows(const float* __restrict__ recv, float* __restrict__ frame, int nx,
+__global__ void __launch_bounds__(256) k_place_rows(const float* __restrict__ recv, float* __restrict__ frame, int nx,
                                                     int ny, int nranks, int block, const ShardPrefix pre) {
     const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // one float4 of a row
     const int row4 = (3 * nx + 3) / 4;
@@ -2357,7 +2316,7 @@ __global__ void __launch_bounds__(256) RTG_NOPK_4 k_place_rows(const float* __re
     for (int q = c; q < c + 4 && q < 3 * nx; q++) dst[q] = src[q];
 }
 
-__global__ void __launch_bounds__(256) RTG_NOPK_4 k_hit_details(const SceneView sv, const RayQ rays,
+__global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const RayQ rays,
                                                      const HitRec* __restrict__ hits, rtg_hit* __restrict__ out,
                                                      const int* __restrict__ orig_prim, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Packed-f32 bisection (DESIGN.md §4 "Compiler note"): tests/test_gpu_sah.py against librtg
-# variants built with packed-f32 ops enabled in one kernel family only (-DRTG_PK_ONLY=n; pk0 = none,
-# via the per-kernel attribute, pk = all).  A test failure (exit 1) moves on to the next variant;
+# Packed-f32 bisection (DESIGN.md §4 "Compiler note", profiles/r3_pk_bisect.txt): tests/test_gpu_sah.py
+# against librtg variants built at commit 6ae2d69 (whose rtg_device.hip has the diagnostic macros) with
+# packed-f32 ops enabled, e.g. in csrc: make OUT=../rtg/pk1.so OBJ=../../build/pk1 NOPK= EXTRA=-DRTG_PK_ONLY=1
+# (packed in one kernel family only) or EXTRA="-DRTG_PK_ONLY=1 -DRTG_PK_FENCE=3" (and not in region 3).  A test failure (exit 1) moves on to the next variant;
 # anything else (fault, abort, time limit) ends the script.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
