@@ -15,7 +15,7 @@ Prints ONE JSON line (rank 0).  Extra objects:
                issue (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, one wave64 VALU instruction per 2
                cycles at 2.4 GHz = 1228.8 G wave-instructions/s), from the committed PMC counters
                (profiles/counters_<workload>.json: SQ_INSTS_VALU per launch) divided by the live
-               HIP-event launch time; `kernels` holds the same for k_shadow, k_shade, k_resolve and
+               HIP-event launch time; `kernels` holds the same for k_shadow, k_shade, k_resolve (k_pt_gather) and
                k_accumulate plus each kernel's measured HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE)
                against 8 TB/s, and the traversal kernels' SIMD lane efficiency (node steps / lane
                slots of a collect_stats frame) with the lane-adjusted VALU fraction; `model` holds
@@ -189,8 +189,9 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
             ("k_shadow", first("rtg::k_shadow<false, false"), "shadow"),
             ("k_pt_shade" if pt else "k_shade", shade, "shade"),
             ("k_accumulate", "rtg::k_accumulate", "accumulate")]
-    if not pt:
-        rows.append(("k_resolve", "rtg::k_resolve", "resolve"))
+    # the bottom-up pass: k_resolve (Whitted), or the path tracer's per-level k_pt_gather (timed in the
+    # library's resolve slot)
+    rows.append(("k_pt_gather", "rtg::k_pt_gather", "resolve") if pt else ("k_resolve", "rtg::k_resolve", "resolve"))
     out = {}
     for key, name, slot in rows:
         n = st_roof.get(f"{slot}_launches", 0)

@@ -27,6 +27,21 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT
 #define RTG_SHADOW_CERT 0
 #endif
+// Object-level part of the certification alone: after an entry's complete walk, a winner with
+// gett() in (0, tcert] blocks whatever the remaining entries hold, so the object loop stops (no
+// per-step bookkeeping inside the walk).
+#ifndef RTG_SHADOW_CERT_OBJ
+#define RTG_SHADOW_CERT_OBJ 0
+#endif
+// Window test of an object's root box before its walk (visit_object).
+#ifndef RTG_ROOT_WINDOW
+#define RTG_ROOT_WINDOW 1
+#endif
+// Object-light shadow queries bounded where the blocking test stops being satisfiable
+// (emit_shadow_tmax) instead of just beyond the light.
+#ifndef RTG_EMIT_TMAX
+#define RTG_EMIT_TMAX 1
+#endif
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
 // 34.0 -> 29.7 ms); the simple variants already fit 4 waves (no-op for them)
@@ -168,6 +183,20 @@ DEV bool box_hit(f3 o, f3 d, f3 inv, bool fast_ok, float mnx, float mny, float m
         if (sl >= le + e) return true;
     }
     return box_test(o, d, mnx, mny, mnz, mxx, mxy, mxz);
+}
+// Window pruning of one (already padded) box, the traversal's slot test without the reachability
+// part: false when the box meets the line only outside [tlo, thi].  Reciprocal slabs with
+// the 2^-20 band of box_hit; a NaN from overflowing terms compares false (box kept).
+DEV bool window_meets(f3 o, f3 inv, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float tlo,
+                      float thi) {
+    const float ax = (mnx - o.x) * inv.x, bx = (mxx - o.x) * inv.x;
+    const float ay = (mny - o.y) * inv.y, by = (mxy - o.y) * inv.y;
+    const float az = (mnz - o.z) * inv.z, bz = (mxz - o.z) * inv.z;
+    const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+    const float lo = le - e, hi = sl + e;
+    return !(hi < lo || hi < tlo || lo > thi);
 }
 // Squared Euclidean distance from o to the box (pruning / ordering only).
 DEV float box_dist2(f3 o, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
@@ -370,6 +399,13 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         float thi = INFINITY;
         if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
         const float thi0 = thi;     // thi never exceeds the window of the best hit so far
+        // The root box, widened by the eps overhang (win_*), meets the line only outside the window:
+        // no candidate of this object can matter (behind the origin, or beyond the winner so far /
+        // the shadow query's bound), so the walk would prune every slot of its first node.
+        if (RTG_ROOT_WINDOW && !EXHAUSTIVE && fast && g.win &&
+            !window_meets(o2, inv, g.win_min[0], g.win_min[1], g.win_min[2], g.win_max[0], g.win_max[1], g.win_max[2],
+                          tlo, thi))
+            return;
         // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
         auto test_prim = [&](const TriGeom& tg, int k, int start) {
             if (STATS) st.tris++;
@@ -477,7 +513,8 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             if (!use2) {
                 // CERT: tau bounds gett()'s rounding (4u |o_a| / |d_a|, as the object-loop bound
                 // above) with a 4x margin: a candidate with t > tau has gett() > 0
-                const bool cert_on = CERT && tcert > 0.0f;
+                constexpr bool WCERT = CERT && RTG_SHADOW_CERT;   // the walk's part (else object level only)
+                const bool cert_on = WCERT && tcert > 0.0f;
                 const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : -INFINITY;
                 // > 0: the best candidate so far has gett() in (0, tcert] (a float, not a lane
                 // mask: SGPRs are the scarce register file of this loop)
@@ -499,7 +536,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
                     if (bary) { bt = c.t; bb = c.beta; bg = c.gamma; }
                     if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                    if (CERT) {
+                    if (WCERT) {
                         // gett() of a fast ray is its first quotient (d2.x finite, nonzero); a NaN
                         // compares false (not certified)
                         const float tg_ = (c.p.x - o2.x) / d2.x;
@@ -598,7 +635,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     auto push = [&](int j) {
                         if (r4[j] < 0) return;
                         int e = r4[j];
-                        if (CERT) {
+                        if (WCERT) {
                             const bool fl = !(k4[j] > tau);
                             nflag += fl;
                             e |= fl ? (int)0x80000000u : 0;
@@ -608,15 +645,15 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     };
                     push(3); push(2); push(1);
                     if (r4[0] >= 0) {
-                        if (CERT && best_cert > 0.0f && nflag == 0 && k4[0] > tau) break;
+                        if (WCERT && best_cert > 0.0f && nflag == 0 && k4[0] > tau) break;
                         cur = r4[0];
                     } else {
-                        if (CERT && best_cert > 0.0f && nflag == 0) break;
+                        if (WCERT && best_cert > 0.0f && nflag == 0) break;
                         if (sp == 0) break;
                         sp--;
                         const int e = stack[sp * sstride];
-                        if (CERT) nflag -= e < 0;
-                        cur = CERT ? (e & 0x7fffffff) : e;
+                        if (WCERT) nflag -= e < 0;
+                        cur = WCERT ? (e & 0x7fffffff) : e;
                     }
                 }
             }
@@ -1119,6 +1156,22 @@ DEV float shadow_tmax(f3 origin, f3 p, f3 lp, float eps) {
     if (!(tmax == tmax)) tmax = FLT_MAX;
     return tmax;
 }
+// Object-light (NEE) query bound: k_shadow blocks iff |p - hp| < lim = dl - (eps + 1e-4 dl)
+// (Page7.md:143-147 as the oracle states it), hp = o + d t, o = p + w (w = the normal offset).
+// With |d| = 1, |p - hp|^2 = t^2 + 2t (d.w) + |w|^2, so every hit with t >= tcut = -(d.w) +
+// sqrt((d.w)^2 - |w|^2 + lim^2) leaves the query unblocked.  The light's own surface, at
+// t ~ dl - (d.w), lies eps + 1e-4 dl beyond tcut, so the query no longer walks to it.  Margins:
+// 1e-5 relative and 1e-5 |o| absolute, far above the rounding of k_shadow's test.
+DEV float emit_shadow_tmax(f3 origin, f3 p, f3 lp, f3 d, float eps) {
+    const float dl = norm(p - lp);
+    const float lim = dl - (eps + 1e-4f * dl);
+    const f3 w = origin - p;
+    const float dw = dot(d, w);
+    const float tcut = -dw + sqrtf(fmax0(dw * dw - dot(w, w) + lim * lim));
+    const float oabs = fmaxf(fmaxf(fabsf(origin.x), fabsf(origin.y)), fabsf(origin.z));
+    const float t = (lim > 0.0f ? tcut * (1.0f + 1e-5f) : 0.0f) + 1e-5f * (oabs + dl) + 1e-30f;
+    return t == t ? t : FLT_MAX;
+}
 
 template <bool FULL = true, bool SPOT = true, bool BRDF = FULL>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
@@ -1261,6 +1314,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     if ((mode == 1.0f || mode == 2.0f) && (__float_as_uint(c.x) | __float_as_uint(c.y) | __float_as_uint(c.z)) == 0u)
         mode = 0.0f;
     if (mode == 1.0f || mode == 3.0f) tmax = shadow_tmax(origin, ret.point, lp, sv.shadow_eps);
+    if (RTG_EMIT_TMAX && mode == 3.0f) tmax = fminf(tmax, emit_shadow_tmax(origin, ret.point, lp, dir, sv.shadow_eps));
     sr.o = make_float4(origin.x, origin.y, origin.z, time);
     sr.d = make_float4(dir.x, dir.y, dir.z, tmax);
     sr.c = make_float4(c.x, c.y, c.z, mode);
@@ -1601,9 +1655,12 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                                 reinterpret_cast<float3*>(shadows.c)[k] =
                                     make_float3(nd.cr + sr.c.x, nd.cg + sr.c.y, nd.cb + sr.c.z);
                             } else {
-                                shadows.o[k] = sr.o;
+                                // the origin (+ time) is the node's, whatever the light: one record
+                                // per node, at the node's index; direction and light point only
+                                // for a traced query (k_light_sum reads every contribution)
+                                if (li == 0) shadows.o[i] = sr.o;
                                 shadows.c[k] = sr.c;
-                                if (!sv.lean_shadow) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
+                                if (!sv.lean_shadow && sr.c.w != 0.0f) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
                             }
                         }
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
@@ -1724,8 +1781,8 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
 // One shading step of oracle/rtg_oracle.c pt_sample() per ray (no reference code exists:
 // pages/Page7.md describes the integrator in prose; DESIGN.md §8 fixes it).  Writes the
 // vertex contribution v into nodes[i] (k_shadow / k_light_sum add the lights, k_pt_gather
-// adds T (x) v to the sample's radiance), the Beer-attenuated throughput into paths[i], and
-// at most one continuation ray.
+// adds T (x) v to the sample's radiance), the Beer-attenuated throughput and the sample slot into
+// the node's link plane (the only reader is k_pt_gather), and at most one continuation ray.
 struct DielSplit {
     bool entering, tir;
     float F;
@@ -1772,6 +1829,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
     RayMeta cm;
     PathRec cp;
     NodeRec nd;
+    f3 Tg = mk(0, 0, 0);            // the vertex's Beer-attenuated throughput (k_pt_gather)
     unsigned long long smask = 0;
     if (i < n) {
         f3 o, d;
@@ -1846,7 +1904,9 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
                         ShadowRec sr;
                         light_sample<FULL, SPOT, BRDF>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         const size_t k = (size_t)i * sv.num_lights + li;
-                        shadows.o[k] = sr.o; shadows.d[k] = sr.d; shadows.c[k] = sr.c; shadows.L[k] = sr.L;
+                        if (li == 0) shadows.o[i] = sr.o;       // per node (k_shade's layout)
+                        shadows.c[k] = sr.c;
+                        if (sr.c.w != 0.0f) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
                     }
@@ -1898,9 +1958,7 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
             }
         }
         nd.kind = kind;
-        PathRec pw;
-        pw.tr = T.x; pw.tg = T.y; pw.tb = T.z; pw.flags = spec | (medium << 8);
-        paths[i] = pw;
+        Tg = T;
     }
     // compaction: one continuation per lane, shadow list light-major per wave (as k_shade)
     __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64];
@@ -1927,8 +1985,8 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
     if (i < n) {
         if (has) { store_ray(next_rays, idx, cr.o, cr.d, cr.time); next_meta[idx] = cm; next_paths[idx] = cp; nd.child1 = idx; }
         nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
-        nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
-        nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, nd.slot);
+        if (smask) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);   // read by k_shadow only
+        nodes.link[i] = make_int4(__float_as_int(Tg.x), __float_as_int(Tg.y), __float_as_int(Tg.z), nd.slot);
     }
     unsigned sb = (unsigned)(s_base >> 32) + s_ws[wv];
     for (int li = 0; li < sv.num_lights; li++) {
@@ -1954,18 +2012,18 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const
     if (nL > 1 && (kind & 0x100)) {          // Scene::RecursiveShading's col = ((amb + L0) + L1) + ...
         for (int li = 0; li < nL; li++) {
             const float4 sc = shadows.c[(size_t)i * nL + li];
-            const float lit = shadows.L[(size_t)i * nL + li].w;
-            v = v + ((sc.w != 0.0f && lit == 1.0f) ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));
+            v = v + (sc.w != 0.0f ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));   // traced and not blocked
         }
     }
     if (level == 0) {
         f3 L = mk(0, 0, 0);
-        if (c) L = L + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), v);
+        if (c) { const int4 lk = nodes.link[i]; L = L + cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v); }
         level0.col[i] = make_float4(L.x, L.y, L.z, nc.w);
     } else if (c) {
-        const int slot = nodes.link[i].w;
+        const int4 lk = nodes.link[i];          // (T.xyz, slot)
+        const int slot = lk.w;
         const float4 z = level0.col[slot];
-        const f3 L = mk(z.x, z.y, z.z) + cw(mk(paths[i].tr, paths[i].tg, paths[i].tb), v);
+        const f3 L = mk(z.x, z.y, z.z) + cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v);
         level0.col[slot] = make_float4(L.x, L.y, L.z, z.w);
     }
 }
@@ -1999,7 +2057,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             const float3 q = reinterpret_cast<const float3*>(shadows.o)[idx];
             so = make_float4(q.x, q.y, q.z, 0.0f);
         } else {
-            so = shadows.o[idx];
+            so = shadows.o[i];                  // one origin record per node
         }
         const f3 o = mk(so.x, so.y, so.z);
         f3 d;
@@ -2034,7 +2092,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         // t <= tcert below, margins (1e-5 relative) far above the rounding of both sides;
         // directional / environment queries (mode 2) are blocked by any accepted hit.
         float tcert = -INFINITY;
-        if (RTG_SHADOW_CERT && !EXHAUSTIVE && !TLAS) {
+        constexpr bool KCERT = (RTG_SHADOW_CERT || RTG_SHADOW_CERT_OBJ) && !EXHAUSTIVE && !TLAS;
+        if (KCERT) {
             const float m0 = query_mode();
             if (m0 == 2.0f) {
                 tcert = INFINITY;
@@ -2055,7 +2114,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 if (tc > 0.0f) tcert = tc;
             }
         }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, RTG_SHADOW_CERT && !EXHAUSTIVE && !TLAS>(
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KCERT>(
             sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
             s_tstack + (TLAS ? threadIdx.x : 0), tcert);
         const float mode = query_mode();
@@ -2071,7 +2130,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                     const float* qo = reinterpret_cast<const float*>(shadows.o) + 3 * (size_t)idx;
                     o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
                 } else {
-                    const float* qo = reinterpret_cast<const float*>(shadows.o + idx);
+                    const float* qo = reinterpret_cast<const float*>(shadows.o + i);
                     o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
                 }
                 const float* pp = reinterpret_cast<const float*>(nodes.pnt + i);
@@ -2113,7 +2172,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             cp[1] = cp[1] + add.y;
             cp[2] = cp[2] + add.z;
         } else {
-            reinterpret_cast<float*>(shadows.L + idx)[3] = blocked ? 0.0f : 1.0f;
+            // blocked: the query's mode (c.w) becomes 0, so the light sum reads one plane only
+            if (blocked) reinterpret_cast<float*>(shadows.c + idx)[3] = 0.0f;
         }
     }
     // NaN queries are rare: one atomic per wave that has any
@@ -2156,7 +2216,7 @@ __global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const Sha
     for (int li = 0; li < sv.num_lights; li++) {
         const size_t k = (size_t)i * sv.num_lights + li;
         const float4 sc = shadows.c[k];
-        const bool lit = sc.w != 0.0f && shadows.L[k].w == 1.0f;
+        const bool lit = sc.w != 0.0f;      // a traced query k_shadow found blocked has mode 0
         col = col + (lit ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));
     }
     nodes.col[i] = make_float4(col.x, col.y, col.z, nc.w);

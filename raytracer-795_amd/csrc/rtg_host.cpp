@@ -313,6 +313,10 @@ struct SahNode2 {
 
 constexpr int kSahBins = 16;
 constexpr int kSahMaxLeaf = 4;
+#ifndef RTG_WIN_MIN_PRIMS
+#define RTG_WIN_MIN_PRIMS 64
+#endif
+constexpr int kWinMinPrims = RTG_WIN_MIN_PRIMS;   // Geometry::win threshold
 
 inline double sah_area(const float lo[3], const float hi[3]) {
     const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
@@ -784,7 +788,8 @@ struct Level {
 struct Lane {
     hipStream_t st = nullptr;
     hipEvent_t ev_count = nullptr;          // recorded after the level count copy
-    hipEvent_t ev_t[5] = {};                // trace start, trace end, shade end, shadow start, shadow end
+    hipEvent_t ev_t[6] = {};                // trace start, trace end, shade end, shadow start, shadow end,
+                                            // path-tracer gather end
     unsigned long long* h_count = nullptr;  // pinned host slot
     DBuf qcnt;                              // 128 x u64 per pass: [level] next rays | shadow entries << 32,
                                             // [64 + level] non-final nodes (k_resolve's list, RTG_RESOLVE_LIST)
@@ -1279,7 +1284,14 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         } else {
             g.node_base = dev_index[ob.root];
             g.root_leaf_start = 0; g.root_leaf_count = -1;
-            for (int z = 0; z < 3; z++) { g.root_min[z] = hn[ob.root].mn[z]; g.root_max[z] = hn[ob.root].mx[z]; }
+            for (int z = 0; z < 3; z++) {
+                g.root_min[z] = hn[ob.root].mn[z]; g.root_max[z] = hn[ob.root].mx[z];
+                g.win_min[z] = std::nextafter((float)((double)g.root_min[z] - g.prune_pad), -FLT_MAX);
+                g.win_max[z] = std::nextafter((float)((double)g.root_max[z] + g.prune_pad), FLT_MAX);
+            }
+            // the window test costs about one slot test: it pays where a skipped walk is more than a
+            // node or two (round 3: dragon -4 % k_trace, cornell's 2- to 6-triangle walls +2 %)
+            g.win = g.nprims >= kWinMinPrims;
         }
     }
 
@@ -1766,9 +1778,11 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                       Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
-        if (pt)
+        if (pt) {
             launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), Lc.shadows.as<ShadowRec>(), nL,
                              ln.levels[0].nodes.as<NodeRec>(), ln.counts[0], level, n, ln.st);
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[5], ln.st));
+        }
         HIP_TRY(hipGetLastError());
         return RTG_OK;
     };
@@ -1867,6 +1881,13 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                 HIP_TRY(hipEventElapsedTime(&b, ln.ev_t[3], ln.ev_t[4]));
                 stt.shadow_ms += b;
                 stt.shadow_launches++;
+            }
+            if (pt) {       // the path tracer's per-level gather, timed in the resolve slot
+                float g = 0.0f;
+                HIP_TRY(hipEventSynchronize(ln.ev_t[5]));
+                HIP_TRY(hipEventElapsedTime(&g, ln.ev_t[4], ln.ev_t[5]));
+                stt.resolve_ms += g;
+                stt.resolve_launches++;
             }
         }
         const int n = ln.counts[ln.level];

@@ -47,6 +47,8 @@ struct Geometry {
     int prim_base;          // absolute index of BVH position 0
     int nprims;
     float prune_pad;        // max distance a hit point can lie outside its primitive's box
+    float win_min[3];       // root box widened by prune_pad, rounded outwards: every candidate
+    float win_max[3];       // lies inside (window pruning of the whole object, visit_object)
     int num_textures;
     int textures[2];        // 1-based
     int texture_offset;
@@ -55,7 +57,7 @@ struct Geometry {
     float center[3];
     float radius;
     int center_index;       // 1-based vertex index
-    int pad1;
+    int win;                // window-test the root box before the walk (meshes of >= RTG_WIN_MIN_PRIMS)
 };
 
 // 64-byte BVH2 node holding both children's boxes (the reference tests a node's own box
@@ -334,8 +336,8 @@ struct ShadowRec {      // 64 B, nLights per shading node
 struct ShadowPlanes {
     float4* o;      // origin.xyz, time
     float4* d;      // direction.xyz, tmax
-    float4* c;      // contribution rgb, mode
-    float4* L;      // light point, lit flag (several lights)
+    float4* c;      // contribution rgb, mode (several lights: k_shadow zeroes it for a blocked query)
+    float4* L;      // light point
 };
 inline ShadowPlanes shadow_planes(ShadowRec* base, long long cap) {
     float4* b = reinterpret_cast<float4*>(base);
