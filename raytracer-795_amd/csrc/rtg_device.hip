@@ -545,6 +545,13 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                 };
                 int sp = 0;
                 int cur = g.sah_base;
+                // a one-node tree of a few triangles: test them all instead of loading the node (the
+                // winner is the minimum of a total order, so testing candidates the slot boxes would
+                // have skipped changes nothing: they lie outside the window and lose either here or
+                // at the object-level t < nearest)
+                if (g.flat_count > 0) {             // (flat_split < 0 here: sah_base >= 0)
+                    for (int q = g.flat_first; q < g.flat_first + g.flat_count; q++) test_sah(sv.stris[q]);
+                } else
                 while (true) {
                     if (STATS) { st.nodes += 4; st.steps++; }   // one node = four 32-B child records (the model's unit)
 #if RTG_QNODES
@@ -657,7 +664,14 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     }
                 }
             }
-            if (use2) walk2();
+            if (use2) {
+                if (!EXHAUSTIVE && g.flat_split >= 0) {     // root over two leaves: both, no node load
+                    for (int k = g.flat_first; k < g.flat_first + g.flat_count; k++)
+                        test_prim(sv.tris[k], k, k < g.flat_split ? g.flat_first : g.flat_split);
+                } else {
+                    walk2();
+                }
+            }
         }
     }
     if (found) {

@@ -314,9 +314,16 @@ struct SahNode2 {
 constexpr int kSahBins = 16;
 constexpr int kSahMaxLeaf = 4;
 #ifndef RTG_WIN_MIN_PRIMS
-#define RTG_WIN_MIN_PRIMS 64
+#define RTG_WIN_MIN_PRIMS 1
 #endif
 constexpr int kWinMinPrims = RTG_WIN_MIN_PRIMS;   // Geometry::win threshold
+#ifndef RTG_FLAT_MAX
+#define RTG_FLAT_MAX 8
+#endif
+constexpr int kFlatMaxPrims = RTG_FLAT_MAX;       // Geometry::flat_count: meshes tested without a node
+#ifndef RTG_FLAT_REF
+#define RTG_FLAT_REF 1                             // ... including a reference root over two leaves
+#endif
 
 inline double sah_area(const float lo[3], const float hi[3]) {
     const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
@@ -1124,6 +1131,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
 
         Geometry& g = geoms[i];
         memset(&g, 0, sizeof g);
+        g.flat_split = -1;
         g.type = o.type;
         g.prim_base = (int)tris.size();
         g.nprims = np;
@@ -1257,6 +1265,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 }
                 const size_t first = snodes.size();
                 g.sah_base = sah_collapse(bn, 0, tri_base, pad, snodes);
+                if (snodes.size() - first == 1 && np <= kFlatMaxPrims) { g.flat_first = tri_base; g.flat_count = np; }
                 if (RTG_QNODES) {
                     // the quantised copy; a node that cannot be quantised drops the mesh's tree
                     bool qok = true;
@@ -1270,6 +1279,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                         snodes.resize(first);
                         stris.resize(tri_base);
                         g.sah_base = -1;
+                        g.flat_count = 0;
                     }
                 }
             }
@@ -1289,9 +1299,19 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 g.win_min[z] = std::nextafter((float)((double)g.root_min[z] - g.prune_pad), -FLT_MAX);
                 g.win_max[z] = std::nextafter((float)((double)g.root_max[z] + g.prune_pad), FLT_MAX);
             }
-            // the window test costs about one slot test: it pays where a skipped walk is more than a
-            // node or two (round 3: dragon -4 % k_trace, cornell's 2- to 6-triangle walls +2 %)
+            // every mesh by default: on the dragon the 2-triangle floor is skipped by every ray going
+            // up (frame 35.9 -> 35.5 ms against meshes of >= 64 triangles only), cornell / cornell_pt
+            // lose about 1 % (profiles/r3_ab_flat.jsonl)
             g.win = g.nprims >= kWinMinPrims;
+            // a reference root over two leaves (the walk always visits both: leaves carry no tested box)
+            const HNode& rn = hn[ob.root];
+            auto leaf_of = [&](int c) { return c >= 0 && hn[c].left < 0 && hn[c].right < 0 && hn[c].end > hn[c].start; };
+            if (RTG_FLAT_REF && g.sah_base < 0 && np <= kFlatMaxPrims && leaf_of(rn.left) && leaf_of(rn.right) &&
+                hn[rn.right].start == hn[rn.left].end) {
+                g.flat_first = g.prim_base + hn[rn.left].start;
+                g.flat_split = g.prim_base + hn[rn.right].start;
+                g.flat_count = hn[rn.right].end - hn[rn.left].start;
+            }
         }
     }
 

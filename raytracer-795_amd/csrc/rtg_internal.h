@@ -58,6 +58,10 @@ struct Geometry {
     float radius;
     int center_index;       // 1-based vertex index
     int win;                // window-test the root box before the walk (meshes of >= RTG_WIN_MIN_PRIMS)
+    int flat_first;         // flat_count > 0: test the mesh's <= kFlatMaxPrims triangles without a node
+    int flat_count;         // (visit_object): flat_split < 0 -- a one-node traversal tree, stris[flat_first ..];
+    int flat_split;         // >= 0 -- a reference root over two leaves, tris[flat_first .. flat_split) and
+                            // [flat_split .. flat_first + flat_count) (absolute positions)
 };
 
 // 64-byte BVH2 node holding both children's boxes (the reference tests a node's own box
