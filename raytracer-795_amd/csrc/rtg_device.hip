@@ -33,6 +33,10 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT_OBJ
 #define RTG_SHADOW_CERT_OBJ 0
 #endif
+// Line test of a transformed entry's world box before its ray transform (closest_hit).
+#ifndef RTG_ENTRY_BOX
+#define RTG_ENTRY_BOX 1
+#endif
 // Window test of an object's root box before its walk (visit_object).
 #ifndef RTG_ROOT_WINDOW
 #define RTG_ROOT_WINDOW 1
@@ -705,8 +709,24 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
+    // the reference's linear loop; a transformed entry whose world box (TopObject::wbox) the ray line
+    // misses holds no candidate -- its hit points lie in the box and on the line, up to margins far
+    // above the transform's rounding (the top-level BVH's test, below) -- so a lane skips it before
+    // the ray transform (times outside [0, 1] leave the blur sweep: no skip)
+    const bool tin = time >= 0.0f && time <= 1.0f;
     if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {   // wfast is per lane: the others walk on
         for (int i = 0; i < sv.num_tops; i++) {
+            if (RTG_ENTRY_BOX && !EXHAUSTIVE && sv.tops[i].wbox && wfast && tin) {
+                const TopObject& T = sv.tops[i];
+                const f3 wi = mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+                const float ax = (T.wlo[0] - o.x) * wi.x, bx = (T.whi[0] - o.x) * wi.x;
+                const float ay = (T.wlo[1] - o.y) * wi.y, by = (T.whi[1] - o.y) * wi.y;
+                const float az = (T.wlo[2] - o.z) * wi.z, bz = (T.whi[2] - o.z) * wi.z;
+                const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                const float e = (fabsf(sl) + fabsf(le)) * 3.814697265625e-6f + 1e-30f;   // 2^-18
+                if (sl + e < le - e) continue;
+            }
             visit(i);
             if (CERT && certified) break;
         }

@@ -1351,6 +1351,25 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         T.ident = ident ? 1 : 0;
     }
 
+    // world boxes of the transformed entries: the object loop skips such an entry, before its ray
+    // transform, for a wave whose ray lines all miss the box (closest_hit, RTG_ENTRY_BOX)
+    for (int i = 0; i < d->num_objects + d->num_instances; i++) {
+        TopObject& T = tops[i];
+        T.wbox = 0;
+        const ObjBVH& ob = s->bvh[T.geom];
+        if (T.ident || ob.root < 0) continue;
+        TBox b;
+        const HNode& r = ob.nodes[ob.root];
+        if (!entry_world_box(top_model[i], r.mn, r.mx, geoms[T.geom].prune_pad, T.blur, b)) continue;
+        bool fin = true;
+        for (int z = 0; z < 3; z++) {
+            T.wlo[z] = std::nextafter((float)b.lo[z], -FLT_MAX);
+            T.whi[z] = std::nextafter((float)b.hi[z], FLT_MAX);
+            fin = fin && std::isfinite(T.wlo[z]) && std::isfinite(T.whi[z]);
+        }
+        T.wbox = fin ? 1 : 0;
+    }
+
     // top-level BVH over the entries (objects, then instances): replaces the reference's linear
     // object loop (src/Helper.cpp:32-73) for scenes with many objects
     std::vector<Node> tlas_nodes;

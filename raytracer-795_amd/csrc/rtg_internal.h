@@ -33,6 +33,8 @@ struct TopObject {
     int geom;               // index of the geometry (base mesh for instances)
     int is_instance;
     int ident;              // inv is exactly the identity (+0 off-diagonal) and blur is +0
+    int wbox;               // wlo / whi valid: a transformed entry's world box (root box + eps overhang
+    float wlo[3], whi[3];   // through the model matrix, blur sweep for times in [0, 1], margins)
 };
 
 // Per geometry (one per object; instances share their base mesh's geometry).

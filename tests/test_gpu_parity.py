@@ -78,6 +78,44 @@ def test_trace_matches_oracle(gpu, name):
             assert np.array_equal(h["normal"][m].view(np.int32), ref["normal"][m].view(np.int32))
 
 
+@pytest.mark.parametrize("name", ["cornell", "dragon"])
+def test_trace_from_surface_points_matches_oracle(gpu, name):
+    """Rays starting on (or within +-2 eps of) the scenes' triangles, as shadow and secondary rays
+    do: the t >= -eps acceptance (src/Shape.cpp:330) with the top-level t > 0 rule
+    (src/Helper.cpp:39-49) lets a candidate just behind the origin hide the rest of its object.
+    Covers the flat meshes (cornell's walls, the 2-triangle quads: triangles tested without a
+    node) and the root-box window (entries wholly behind the origin skipped) against the literal
+    oracle, pruned and exhaustive."""
+    sc = SCENES[name]()
+    rng = np.random.default_rng(23)
+    V = np.asarray(sc.vertices, np.float64)
+    faces = np.concatenate([np.asarray(ob.faces) - 1 for ob in sc.objects if ob.faces is not None])
+    n = 6000
+    f = faces[rng.integers(0, len(faces), n)]
+    a, b, c = V[f[:, 0]], V[f[:, 1]], V[f[:, 2]]
+    u, v = rng.random(n), rng.random(n)
+    flip = u + v > 1
+    u[flip], v[flip] = 1 - u[flip], 1 - v[flip]
+    nrm = np.cross(b - a, c - a)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    off = rng.uniform(-2, 2, n) * float(sc.int_eps)
+    o = (a + (b - a) * u[:, None] + (c - a) * v[:, None] + nrm * off[:, None]).astype(np.float32)
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d = d.astype(np.float32)
+    t = rng.random(n).astype(np.float32)
+    ref = pyoracle.Oracle(sc).trace(o, d, t)
+    with rtg.Renderer(sc, device=gpu) as r:
+        for trav in (0, 1):
+            h = r.trace(o, d, t, traversal=trav)
+            assert np.array_equal(h["full"], ref["full"])
+            assert np.array_equal(h["object"], ref["object"])
+            assert np.array_equal(h["prim"], ref["prim"])
+            m = ref["full"] == 1
+            assert np.array_equal(h["t"][m].view(np.int32), ref["t"][m].view(np.int32))
+            assert np.array_equal(h["point"][m].view(np.int32), ref["point"][m].view(np.int32))
+
+
 @pytest.mark.parametrize("block", [1, 2, 4, 5, 8])
 def test_row_shards_sum_to_full_frame(gpu, block):
     """Multi-GPU partition (rows (y // block) % G == rank, incl. a partial last block) +
