@@ -33,6 +33,10 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT_OBJ
 #define RTG_SHADOW_CERT_OBJ 0
 #endif
+// Shading of a flat triangle from its TriGeom record alone (hit_record).
+#ifndef RTG_FLAT_NORMAL
+#define RTG_FLAT_NORMAL 1
+#endif
 // Line test of a transformed entry's world box before its ray transform (closest_hit).
 #ifndef RTG_ENTRY_BOX
 #define RTG_ENTRY_BOX 1
@@ -1035,6 +1039,14 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h,
         f3 pc = ip - ld3(g.center);
         ret.normal = pc / norm(pc);
         if (FULL) sphere_texture(sv, g, ret);
+    } else if (RTG_FLAT_NORMAL && !FULL && !STORED && !(g.type == RTG_OBJ_TRIANGLE || g.smooth)) {
+        // flat triangle, no texturing: the normal from the record's a - b and c - b (prim_idx.w is
+        // the object's smooth flag, 1 for Triangle objects: Shape.cpp:262-276), no vertex loads
+        const TriGeom tg = sv.tris[h.prim];
+        const Cand c = tri_test(tg, o2, d2, sv.int_eps);
+        const f3 normal = cross(mk(tg.p2.y, tg.p2.z, tg.p2.w), mk(tg.p0.w, tg.p1.x, tg.p1.y));
+        ret.normal = normal / norm(normal);
+        ret.point = c.p;
     } else {
         int4 vi = sv.prim_idx[h.prim];
         Cand c;

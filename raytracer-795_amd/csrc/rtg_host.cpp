@@ -1158,12 +1158,13 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             } else {
                 int i1 = pv[3 * f], i2 = pv[3 * f + 1], i3 = pv[3 * f + 2];
                 V3 a = verts[i1 - 1], b = verts[i2 - 1], c = verts[i3 - 1];
-                V3 amb = a - b, amc = a - c;
+                V3 amb = a - b, amc = a - c, cmb = c - b;
                 tg.p0 = make_float4(a.x, a.y, a.z, amb.x);
                 tg.p1 = make_float4(amb.y, amb.z, amc.x, amc.y);
-                float fi;
-                memcpy(&fi, &f, 4);
-                tg.p2 = make_float4(amc.z, fi, 0.0f, 0.0f);
+                // c - b: with a - b the flat normal (c - b) x (a - b) of Triangle::bvhIntersect
+                // (src/Shape.cpp:327), so the shading of a flat triangle reads this record only
+                // (the traversal copy, stris, reuses p2.yzw)
+                tg.p2 = make_float4(amc.z, cmb.x, cmb.y, cmb.z);
                 int smooth = (o.type == RTG_OBJ_TRIANGLE) ? 1 : o.smooth;   // Shape.cpp:262-276 quirk
                 pi = make_int4(i1, i2, i3, smooth);
                 double e = (double)(ieps > 0 ? ieps : 0.0f);

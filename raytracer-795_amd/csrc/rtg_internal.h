@@ -114,7 +114,9 @@ constexpr float kQDirMax = 1e16f;
 struct TriGeom {
     float4 p0;  // a.xyz, (a-b).x
     float4 p1;  // (a-b).yz, (a-c).xy
-    float4 p2;  // (a-c).z, orig_index (bits), leaf length (int bits, first prim of each leaf), 0
+    float4 p2;  // (a-c).z, then (c-b).xyz in the reference-order copy (flat shading normal,
+                // hit_record); the traversal copy (stris) holds the reference position, the first
+                // position of its reference leaf and the gate flag (int bits) there
 };
 
 // Internal light types of hw7 object lights (appended after the scene's lights; only the
