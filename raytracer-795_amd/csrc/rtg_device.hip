@@ -1219,7 +1219,9 @@ DEV float emit_shadow_tmax(f3 origin, f3 p, f3 lp, f3 d, float eps) {
     return t == t ? t : FLT_MAX;
 }
 
-template <bool FULL = true, bool SPOT = true, bool BRDF = FULL>
+// EMIT: the hw7 object-light cases (the path tracer's NEE; the Whitted light loop never reaches
+// them: the render adds the object lights to the loop only for the path tracer)
+template <bool FULL = true, bool SPOT = true, bool BRDF = FULL, bool EMIT = true>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
                       uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
     const LightDev& L = sv.lights[li];
@@ -1299,7 +1301,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         break;
     }
     case kLightEmitMesh:                                        // hw7 object lights: NEE sample
-    case kLightEmitSphere: {                                    // (oracle emitter_shading)
+    case kLightEmitSphere: if constexpr (EMIT) {                // (oracle emitter_shading)
         float xi[4];
         rng4(seed, pixel, sample, path, RNG_PT_EMIT, (uint32_t)li, 0, xi);
         const f3 p = ret.point;
@@ -1689,7 +1691,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
-                        light_sample<FULL, SPOT, FULL && TEX>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
+                        light_sample<FULL, SPOT, FULL && TEX, false>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         // one light: a query that is not traced is never read (k_light_sum reads
                         // every record when there are several)
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
