@@ -33,6 +33,10 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT_OBJ
 #define RTG_SHADOW_CERT_OBJ 0
 #endif
+// Traversal-tree root node loaded ahead of the mesh's root test (visit_object); A/B switch.
+#ifndef RTG_ROOT_PREFETCH
+#define RTG_ROOT_PREFETCH 0
+#endif
 // Shading of a flat triangle from its TriGeom record alone (hit_record).
 #ifndef RTG_FLAT_NORMAL
 #define RTG_FLAT_NORMAL 1
@@ -372,6 +376,12 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
         // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
         // send every box to the exact division test instead.
+        // RTG_ROOT_PREFETCH: the traversal tree's root node does not depend on the ray, so its load
+        // is issued here and overlaps the root test and the window set-up instead of starting the walk
+#if RTG_ROOT_PREFETCH
+        Node4 rootn;
+        if (g.sah_base >= 0 && g.flat_count == 0) rootn = sv.snodes[g.sah_base];
+#endif
         const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
         const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
                           adz <= 1e30f;
@@ -580,7 +590,13 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     }
                     auto qb = [](unsigned w, int j) { return (float)((w >> (8 * j)) & 0xFFu); };
 #else
+#if RTG_ROOT_PREFETCH
+                    Node4 nd;
+                    if (cur == g.sah_base) nd = rootn;     // the first step (the root is never pushed)
+                    else nd = sv.snodes[cur];
+#else
                     const Node4 nd = sv.snodes[cur];
+#endif
                     const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
                     const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
                     const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
@@ -1230,6 +1246,12 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     f3 c = mk(0, 0, 0);
     f3 dir = mk(0, 0, 0), lp = mk(0, 0, 0);
     float mode = 0.0f, tmax = FLT_MAX;
+    // every case leaves the light colour and direction of its single BRDF call here; the call
+    // follows the switch (one inlined copy of the BRDF code instead of one per light type)
+    f3 LCs = mk(0, 0, 0), wis = mk(0, 0, 0);
+    bool lit = false;
+    float post = 1.0f;              // spot fall-off, applied after the BRDF (Light.cpp:432-434)
+    bool use_post = false;
     switch (L.type) {
     case RTG_LIGHT_POINT: {                                     // PointLight::BasicShading Light.cpp:238-250
         f3 pos = ld3(L.pos);
@@ -1237,14 +1259,17 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         lp = pos;
         mode = 1.0f;
         float dist = norm(ret.point - pos);
-        f3 LC = ld3(L.inten) / (dist * dist);
-        c = phong_or_brdf<BRDF>(LC, wo, normalized(pos - ret.point), ret, m);
+        LCs = ld3(L.inten) / (dist * dist);
+        wis = normalized(pos - ret.point);
+        lit = true;
         break;
     }
     case RTG_LIGHT_DIRECTIONAL: {                               // Light.cpp:309-321
         dir = -ld3(L.dir);
         mode = 2.0f;
-        c = phong_or_brdf<BRDF>(ld3(L.inten), wo, dir, ret, m);
+        LCs = ld3(L.inten);
+        wis = dir;
+        lit = true;
         break;
     }
     case RTG_LIGHT_SPOT: if constexpr (FULL || SPOT) {          // Light.cpp:409-436
@@ -1256,11 +1281,12 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         if (angle < L.fall || angle < L.coverage) {
             mode = 1.0f;
             float dist = norm(ret.point - pos);
-            f3 LC = ld3(L.inten) / (dist * dist);
-            c = phong_or_brdf<BRDF>(LC, wo, normalized(pos - ret.point), ret, m);
+            LCs = ld3(L.inten) / (dist * dist);
+            wis = normalized(pos - ret.point);
+            lit = true;
             if (!(angle < L.fall)) {
-                float fo = (float)pow((cos((double)angle) - (double)L.cos_cov) / (double)(L.cos_fall - L.cos_cov), 4.0);
-                c = c * fo;
+                post = (float)pow((cos((double)angle) - (double)L.cos_cov) / (double)(L.cos_fall - L.cos_cov), 4.0);
+                use_post = true;
             }
         }
         break;
@@ -1278,8 +1304,9 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         float cosTheta = fabsf(dot(normalized(pms), ld3(L.normal)));
         float dSq = norm(pms);
         dSq = dSq * dSq;
-        f3 LC = ld3(L.inten) * ((L.size * L.size) * (cosTheta / dSq));
-        c = phong_or_brdf<BRDF>(LC, wo, normalized(smp - ret.point), ret, m);
+        LCs = ld3(L.inten) * ((L.size * L.size) * (cosTheta / dSq));
+        wis = normalized(smp - ret.point);
+        lit = true;
         break;
     }
     case RTG_LIGHT_ENVIRONMENT: if constexpr (FULL) {          // Light.cpp:628-660
@@ -1297,7 +1324,9 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         }
         dir = direction;
         mode = 2.0f;
-        c = phong_or_brdf<BRDF>(env_radiance(sv, L, direction), wo, direction, ret, m);
+        LCs = env_radiance(sv, L, direction);
+        wis = direction;
+        lit = true;
         break;
     }
     case kLightEmitMesh:                                        // hw7 object lights: NEE sample
@@ -1348,13 +1377,20 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
             const float cosl = fabsf(dot(dir, nl));
             LC = ld3(L.inten) * ((cosl * L.coverage) / (dd * dd));
         }
-        c = phong_or_brdf<BRDF>(LC, wo, dir, ret, m);
-        // a sample that contributes exactly zero (light behind the surface) needs no shadow ray:
-        // blocked or not it adds 0 (oracle emitter_shading does the same)
-        mode = (c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) ? 0.0f : 3.0f;
+        LCs = LC;
+        wis = dir;
+        lit = true;
+        mode = 3.0f;            // 0 below when the contribution is exactly zero
         break;
     }
     }
+    if (lit) {
+        c = phong_or_brdf<BRDF>(LCs, wo, wis, ret, m);
+        if (use_post) c = c * post;
+    }
+    // an object-light sample that contributes exactly zero (light behind the surface) needs no
+    // shadow ray: blocked or not it adds 0 (oracle emitter_shading does the same)
+    if (mode == 3.0f && c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) mode = 0.0f;
     // A query whose unshadowed contribution is exactly +0 in every channel (a light behind
     // the surface with no specular lobe left) need not be traced: blocked, the light adds the
     // reference's Vector3f(0,0,0) (src/Light.cpp:188-204, 270-275), unblocked it adds c = +0;
