@@ -33,10 +33,6 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT_OBJ
 #define RTG_SHADOW_CERT_OBJ 0
 #endif
-// Traversal-tree root node loaded ahead of the mesh's root test (visit_object); A/B switch.
-#ifndef RTG_ROOT_PREFETCH
-#define RTG_ROOT_PREFETCH 0
-#endif
 // Shading of a flat triangle from its TriGeom record alone (hit_record).
 #ifndef RTG_FLAT_NORMAL
 #define RTG_FLAT_NORMAL 1
@@ -376,12 +372,6 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         // Reciprocal direction for the fast slab test (v_rcp_f32, 1 ulp: the 2^-20 margin of
         // child() covers it).  Components outside [1e-30, 1e30] (zero, denormal, huge, NaN)
         // send every box to the exact division test instead.
-        // RTG_ROOT_PREFETCH: the traversal tree's root node does not depend on the ray, so its load
-        // is issued here and overlaps the root test and the window set-up instead of starting the walk
-#if RTG_ROOT_PREFETCH
-        Node4 rootn;
-        if (g.sah_base >= 0 && g.flat_count == 0) rootn = sv.snodes[g.sah_base];
-#endif
         const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
         const bool fast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f &&
                           adz <= 1e30f;
@@ -590,13 +580,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     }
                     auto qb = [](unsigned w, int j) { return (float)((w >> (8 * j)) & 0xFFu); };
 #else
-#if RTG_ROOT_PREFETCH
-                    Node4 nd;
-                    if (cur == g.sah_base) nd = rootn;     // the first step (the root is never pushed)
-                    else nd = sv.snodes[cur];
-#else
                     const Node4 nd = sv.snodes[cur];
-#endif
                     const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
                     const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
                     const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
