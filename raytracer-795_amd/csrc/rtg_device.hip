@@ -58,9 +58,13 @@ namespace rtg {
 #endif
 #define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? 2 : RTG_SHADE_WAVES)))
 // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
-// spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); the full
-// variants keep the default
-#define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? 3 : 1)))
+// spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); round 3, with
+// one BRDF call site (167 VGPRs, no spill at 3 waves): 4 waves spill 140-164 B and lose, 398 -> 404
+// ms (profiles/r3_ab_ptwaves.jsonl); the full variants keep the default
+#ifndef RTG_PT_WAVES
+#define RTG_PT_WAVES 3
+#endif
+#define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? RTG_PT_WAVES : 1)))
 constexpr double PI_D = 3.14159265358979323846;
 
 // ------------------------------------------------------------------ vectors (Eigen order)
