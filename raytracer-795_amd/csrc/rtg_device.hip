@@ -1911,8 +1911,11 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
             primary_ray(cam, ps, seed, i, o, d, time);
             mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
         } else {
+            // a path's queued ray carries only its sample slot (4 bytes in the meta buffer): the
+            // path key is level + 1 and the remaining depth max_depth - level at every level
             load_ray(rays, i, o, d, time);
-            mt = meta[i];
+            mt.slot = reinterpret_cast<const int*>(meta)[i];
+            mt.path_lo = (unsigned)level + 1u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
         }
         const HitIn hin = load_hit_planes(sv, hits, n, i);
         const HitRec& h = hin.h;
@@ -2055,7 +2058,11 @@ __global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneV
     __syncthreads();
     const int idx = (int)((unsigned)s_base + s_wc[wv] + coff);
     if (i < n) {
-        if (has) { store_ray(next_rays, idx, cr.o, cr.d, cr.time); next_meta[idx] = cm; next_paths[idx] = cp; nd.child1 = idx; }
+        if (has) {
+            store_ray(next_rays, idx, cr.o, cr.d, cr.time);
+            reinterpret_cast<int*>(next_meta)[idx] = cm.slot;
+            next_paths[idx] = cp;
+        }
         nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
         if (smask) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);   // read by k_shadow only
         nodes.link[i] = make_int4(__float_as_int(Tg.x), __float_as_int(Tg.y), __float_as_int(Tg.z), nd.slot);
