@@ -52,11 +52,14 @@ namespace rtg {
 #endif
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
-// 34.0 -> 29.7 ms); the simple variants already fit 4 waves (no-op for them)
+// 34.0 -> 29.7 ms).
+// The simple variant (point / directional lights, no textures or BRDFs) at 6 waves per SIMD: 90 -> 80
+// VGPRs with an 8-byte spill, dragon k_shade 8.80 -> 7.87 ms per frame (7 waves: 8.6 ms;
+// profiles/r3_ab_shadewaves.jsonl); the spot variant (182 VGPRs) keeps the minimum of 2.
 #ifndef RTG_SHADE_WAVES
-#define RTG_SHADE_WAVES 2
+#define RTG_SHADE_WAVES 6
 #endif
-#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? 2 : RTG_SHADE_WAVES)))
+#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL || SPOT ? 2 : RTG_SHADE_WAVES)))
 // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
 // spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); round 3, with
 // one BRDF call site (167 VGPRs, no spill at 3 waves): 4 waves spill 140-164 B and lose, 398 -> 404

@@ -116,6 +116,38 @@ def test_trace_from_surface_points_matches_oracle(gpu, name):
             assert np.array_equal(h["point"][m].view(np.int32), ref["point"][m].view(np.int32))
 
 
+def test_trace_transformed_entries_any_time_matches_oracle(gpu):
+    """cornell_dynamic's transformed entries (scaled / rotated instances, the motion-blurred sphere
+    and instance) are skipped before their ray transform when the ray line misses their world box
+    (TopObject::wbox, blur swept over times in [0, 1]).  Times outside [0, 1], direction components
+    of exactly zero and rays from outside the room take the paths where that skip must not fire
+    (or the exact division tests), against the literal oracle, pruned and exhaustive."""
+    sc = scenegen.cornell(48, 36, spp=4)
+    rng = np.random.default_rng(31)
+    n = 6000
+    lo = np.asarray(sc.vertices).min(0) - 3
+    hi = np.asarray(sc.vertices).max(0) + 3
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    zero = rng.random((n, 3)) < 0.08                  # some components exactly +-0
+    d[zero] = 0.0
+    d[np.all(d == 0, axis=1), 1] = -1.0
+    d = d.astype(np.float32)
+    t = rng.uniform(-0.5, 1.5, n).astype(np.float32)
+    ref = pyoracle.Oracle(sc).trace(o, d, t)
+    with rtg.Renderer(sc, device=gpu) as r:
+        for trav in (0, 1):
+            h = r.trace(o, d, t, traversal=trav)
+            assert np.array_equal(h["full"], ref["full"])
+            assert np.array_equal(h["object"], ref["object"])
+            assert np.array_equal(h["prim"], ref["prim"])
+            m = ref["full"] == 1
+            assert np.array_equal(h["t"][m].view(np.int32), ref["t"][m].view(np.int32))
+            assert np.array_equal(h["point"][m].view(np.int32), ref["point"][m].view(np.int32))
+            assert np.array_equal(h["normal"][m].view(np.int32), ref["normal"][m].view(np.int32))
+
+
 @pytest.mark.parametrize("block", [1, 2, 4, 5, 8])
 def test_row_shards_sum_to_full_frame(gpu, block):
     """Multi-GPU partition (rows (y // block) % G == rank, incl. a partial last block) +
