@@ -59,7 +59,10 @@ namespace rtg {
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 6
 #endif
-#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL || SPOT ? 2 : RTG_SHADE_WAVES)))
+#ifndef RTG_SHADE_FULL_WAVES
+#define RTG_SHADE_FULL_WAVES 2
+#endif
+#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? RTG_SHADE_FULL_WAVES : SPOT ? 2 : RTG_SHADE_WAVES)))
 // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
 // spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); round 3, with
 // one BRDF call site (167 VGPRs, no spill at 3 waves): 4 waves spill 140-164 B and lose, 398 -> 404
