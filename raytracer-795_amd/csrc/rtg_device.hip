@@ -1244,7 +1244,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     // follows the switch (one inlined copy of the BRDF code instead of one per light type)
     f3 LCs = mk(0, 0, 0), wis = mk(0, 0, 0);
     bool lit = false;
-    float post = 1.0f;              // spot fall-off, applied after the BRDF (Light.cpp:432-434)
+    float post = 1.0f;              // spot FallOf(angle), applied after the BRDF (Light.cpp:428-431)
     bool use_post = false;
     switch (L.type) {
     case RTG_LIGHT_POINT: {                                     // PointLight::BasicShading Light.cpp:238-250
