@@ -16,7 +16,10 @@ namespace rtg {
 constexpr int kMaxLights = 64;      // per-node shadow slots are statically strided
 constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
 constexpr int kTraceBlock = 64;     // threads per traversal block (LDS stack: 128 B per lane)
-constexpr int kShadeBlock = 512;    // k_shade (simple variants): one queue atomic per block
+#ifndef RTG_SHADE_BLOCK
+#define RTG_SHADE_BLOCK 512
+#endif
+constexpr int kShadeBlock = RTG_SHADE_BLOCK;    // k_shade (simple variants): one queue atomic per block
 constexpr int kTlasMinEntries = 16; // top-level BVH over objects / instances from this many entries on
 constexpr int kTlasMaxDepth = 14;   // TLAS leaves at this depth take every remaining entry ...
 constexpr int kTlasStack = 16;      // ... so a near-first walk never pushes more than this
