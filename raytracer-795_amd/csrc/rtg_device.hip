@@ -71,6 +71,10 @@ namespace rtg {
 #define RTG_PT_WAVES 3
 #endif
 #define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? RTG_PT_WAVES : 1)))
+#ifndef RTG_PT_BLOCK
+#define RTG_PT_BLOCK 256
+#endif
+constexpr int kPtBlock = RTG_PT_BLOCK;     // k_pt_shade threads per block
 constexpr double PI_D = 3.14159265358979323846;
 
 // ------------------------------------------------------------------ vectors (Eigen order)
@@ -1893,14 +1897,14 @@ constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour 
 
 // GEN: level 0 (primary rays regenerated), else queued rays (separate instantiations, as k_shade)
 template <bool FULL, bool SPOT, bool BRDF, bool GEN = false>
-__global__ void __launch_bounds__(256) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+__global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
                                                   uint64_t seed, const RayQ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
                                                   PathRec* __restrict__ paths, const NodePlanes nodes,
                                                   const ShadowPlanes shadows, int* __restrict__ slist,
                                                   const RayQ next_rays, RayMeta* __restrict__ next_meta,
                                                   PathRec* __restrict__ next_paths, unsigned long long* qcount, int n) {
-    constexpr int BLOCK = 256;
+    constexpr int BLOCK = kPtBlock;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool has = false;
     QRay cr;
@@ -2558,7 +2562,7 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st) {
     if (n <= 0) return;
-    dim3 g(nblk(n, 256)), b(256);
+    dim3 g(nblk(n, kPtBlock)), b(kPtBlock);
 #define RTG_PT_LAUNCH1(F, S, B, G)                                                                                \
     hipLaunchKernelGGL((k_pt_shade<F, S, B, G>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, \
                        node_planes(nodes, n), \
