@@ -18,7 +18,17 @@ namespace rtg {
 
 #define DEV __device__ __forceinline__
 // k_shadow: 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
-#define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+// k_trace / k_shadow at 6 waves per SIMD (80 VGPRs, 16-96 B of spill besides the stack's scratch
+// part): possible since the LDS stack holds 16 entries (rtg_internal.h kLdsStack)
+#ifndef RTG_TRAVERSAL_WAVES
+#define RTG_TRAVERSAL_WAVES 6
+#endif
+#define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(RTG_TRAVERSAL_WAVES)))
+#if RTG_TRAVERSAL_WAVES > 4
+#define RTG_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RTG_TRAVERSAL_WAVES)))
+#else
+#define RTG_TRACE_ATTR
+#endif
 // k_shadow's certified early exit (closest_hit CERT), off by default: measured on the 1080p64
 // dragon (round 3, scripts/gpu_ab3.sh, same box) it cuts a blocked query's node steps 18.9 ->
 // 14.4 (all queries 8.81 -> 7.93) but k_shadow takes 12.9 instead of 12.4 ms per frame -- the
@@ -359,10 +369,20 @@ struct Stats { unsigned nodes, tris, steps; };
 struct HitBary { float pt, beta, gamma; };
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:32-73): the object's
 // winner (closest_hit's comments) and the top-level acceptance against `nearest` / `out`.
+// Traversal stack entry sp of a lane: LDS for the first kLdsStack entries, the lane's scratch array
+// beyond (kLdsStack < kStackDepth builds only: a smaller LDS stack for more waves per CU).
+DEV void stk_put(int* stack, int sstride, int* spill, int sp, int v) {
+    if (kLdsStack >= kStackDepth || sp < kLdsStack) stack[sp * sstride] = v;
+    else spill[sp - kLdsStack] = v;
+}
+DEV int stk_get(const int* stack, int sstride, const int* spill, int sp) {
+    return (kLdsStack >= kStackDepth || sp < kLdsStack) ? stack[sp * sstride] : spill[sp - kLdsStack];
+}
+
 template <bool EXHAUSTIVE, bool STATS, bool CERT>
 DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, const float time, const bool fin,
                       float& nearest, HitRec& out, HitBary* bary, bool& certified, int* stack, int sstride, Stats& st,
-                      const float tcert) {
+                      const float tcert, int* spill) {
     const float eps = sv.int_eps;
     const TopObject& T = sv.tops[i];
     const Geometry& g = sv.geoms[T.geom];
@@ -502,7 +522,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     if (lok && rok) {
                         int nearc = lref, farc = rref;
                         if (rk < lk) { nearc = rref; farc = lref; }
-                        stack[sp * sstride] = farc;
+                        stk_put(stack, sstride, spill, sp, farc);
                         sp++;
                         cur = nearc;
                     } else if (lok) {
@@ -512,7 +532,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     } else {
                         if (sp == 0) break;
                         sp--;
-                        cur = stack[sp * sstride];
+                        cur = stk_get(stack, sstride, spill, sp);
                     }
                 }
             };
@@ -669,7 +689,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                             nflag += fl;
                             e |= fl ? (int)0x80000000u : 0;
                         }
-                        stack[sp * sstride] = e;
+                        stk_put(stack, sstride, spill, sp, e);
                         sp++;
                     };
                     push(3); push(2); push(1);
@@ -680,7 +700,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                         if (WCERT && best_cert > 0.0f && nflag == 0) break;
                         if (sp == 0) break;
                         sp--;
-                        const int e = stack[sp * sstride];
+                        const int e = stk_get(stack, sstride, spill, sp);
                         if (WCERT) nflag -= e < 0;
                         cur = WCERT ? (e & 0x7fffffff) : e;
                     }
@@ -721,9 +741,10 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     float nearest = tmax;
     bool certified = false;
     const bool fin = ray_finite(o, d, time);
+    int spill[kStackDepth > kLdsStack ? kStackDepth - kLdsStack : 1];
     auto visit = [&](const int i) {
         visit_object<EXHAUSTIVE, STATS, CERT>(sv, i, o, d, time, fin, nearest, out, bary, certified, stack, sstride, st,
-                                              tcert);
+                                              tcert, spill);
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
@@ -1535,11 +1556,11 @@ DEV void store_ray(const RayQ& q, int k, f3 o, f3 d, float time) {
 
 // GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no ray queue).
 template <bool EXHAUSTIVE, bool STATS, bool GEN = false, bool TLAS = false>
-__global__ void __launch_bounds__(kTraceBlock) k_trace(const SceneView sv, const RayQ rays,
+__global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayQ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
                                                        const CameraDev cam, const PassDev ps, uint64_t seed,
                                                        bool compact) {
-    __shared__ int s_stack[kStackDepth * kTraceBlock];
+    __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     Stats st = {0, 0, 0};
@@ -2129,7 +2150,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount, const NodePlanes nodes,
                                                                        unsigned* nan_queries, Counters* ctr) {
-    __shared__ int s_stack[kStackDepth * kTraceBlock];
+    __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;

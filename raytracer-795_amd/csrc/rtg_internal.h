@@ -15,6 +15,14 @@ namespace rtg {
 
 constexpr int kMaxLights = 64;      // per-node shadow slots are statically strided
 constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:55,67) + root
+// The first 16 traversal-stack entries of a lane live in LDS (4 KB per 64-lane block), deeper ones
+// (up to kStackDepth: the reference-tree fallback can need 31) in the lane's scratch: with the
+// traversal kernels at 6 waves per SIMD, dragon 33.0 -> 31.6 ms, cornell_pt 392.8 -> 364.3 ms per
+// frame (round 3, profiles/r3_ab_ldsstack.jsonl; 32 entries in LDS held them at 5 waves).
+#ifndef RTG_LDS_STACK
+#define RTG_LDS_STACK 16
+#endif
+constexpr int kLdsStack = RTG_LDS_STACK;   // traversal-stack entries per lane in LDS; deeper ones in scratch
 constexpr int kTraceBlock = 64;     // threads per traversal block (LDS stack: 128 B per lane)
 #ifndef RTG_SHADE_BLOCK
 #define RTG_SHADE_BLOCK 512
