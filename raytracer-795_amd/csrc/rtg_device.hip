@@ -23,12 +23,12 @@ namespace rtg {
 #ifndef RTG_TRAVERSAL_WAVES
 #define RTG_TRAVERSAL_WAVES 6
 #endif
-#define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(RTG_TRAVERSAL_WAVES)))
-#if RTG_TRAVERSAL_WAVES > 4
-#define RTG_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RTG_TRAVERSAL_WAVES)))
-#else
-#define RTG_TRACE_ATTR
+// the top-level-BVH instantiations (many-entry scenes) keep the previous target (A/B switch)
+#ifndef RTG_TLAS_WAVES
+#define RTG_TLAS_WAVES RTG_TRAVERSAL_WAVES
 #endif
+#define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(TLAS ? RTG_TLAS_WAVES : RTG_TRAVERSAL_WAVES)))
+#define RTG_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(TLAS ? RTG_TLAS_WAVES : RTG_TRAVERSAL_WAVES)))
 // k_shadow's certified early exit (closest_hit CERT), off by default: measured on the 1080p64
 // dragon (round 3, scripts/gpu_ab3.sh, same box) it cuts a blocked query's node steps 18.9 ->
 // 14.4 (all queries 8.81 -> 7.93) but k_shadow takes 12.9 instead of 12.4 ms per frame -- the
