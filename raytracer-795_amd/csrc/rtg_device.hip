@@ -23,9 +23,11 @@ namespace rtg {
 #ifndef RTG_TRAVERSAL_WAVES
 #define RTG_TRAVERSAL_WAVES 6
 #endif
-// the top-level-BVH instantiations (many-entry scenes) keep the previous target (A/B switch)
+// the top-level-BVH instantiations (many-entry scenes, LDS also holds their 16-entry top-level
+// stack) keep the previous target: spheres 1080p64 37.3 -> 32.3 ms against 6 waves
+// (profiles/r3_ab_tlaswaves.jsonl)
 #ifndef RTG_TLAS_WAVES
-#define RTG_TLAS_WAVES RTG_TRAVERSAL_WAVES
+#define RTG_TLAS_WAVES 4
 #endif
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(TLAS ? RTG_TLAS_WAVES : RTG_TRAVERSAL_WAVES)))
 #define RTG_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(TLAS ? RTG_TLAS_WAVES : RTG_TRAVERSAL_WAVES)))
