@@ -17,9 +17,10 @@
 namespace rtg {
 
 #define DEV __device__ __forceinline__
-// k_shadow: 135 -> 128 VGPRs (3 -> 4 waves/SIMD, no spills): 32.6 -> 30.9 ms/frame on dragon1m
-// k_trace / k_shadow at 6 waves per SIMD (80 VGPRs, 16-96 B of spill besides the stack's scratch
-// part): possible since the LDS stack holds 16 entries (rtg_internal.h kLdsStack)
+// Traversal occupancy.  Round 1: k_shadow 135 -> 128 VGPRs (3 -> 4 waves/SIMD): 32.6 -> 30.9 ms per
+// dragon frame.  Round 3: k_trace / k_shadow at 6 waves per SIMD (80 VGPRs, 16-96 B of spill besides
+// the stack's scratch part), possible since the LDS stack holds 16 entries (rtg_internal.h kLdsStack):
+// dragon 33.0 -> 31.6 ms, cornell_pt 392.8 -> 364.3 ms (profiles/r3_ab_ldsstack.jsonl).
 #ifndef RTG_TRAVERSAL_WAVES
 #define RTG_TRAVERSAL_WAVES 6
 #endif
