@@ -108,72 +108,106 @@ bool rle_decode(const unsigned char* in, size_t n, std::vector<unsigned char>& o
 // ---- PIZ
 constexpr int kUshortRange = 1 << 16;
 constexpr int kBitmapSize = kUshortRange >> 3;
-constexpr int kHufEncSize = (1 << 16) + 1;
-constexpr int kHufDecBits = 14;
-constexpr int kShortZeroRun = 59, kLongZeroRun = 63, kShortestLongRun = 2 + kLongZeroRun - kShortZeroRun;
+constexpr int kSymbols = (1 << 16) + 1;     // 16-bit values plus one run-length pseudo symbol
+constexpr int kMaxLen = 58;                 // longest code length a 6-bit length field can name
 
-struct BitIn {                          // MSB-first bit reader
-    const unsigned char* p;
-    const unsigned char* end;
-    uint64_t c = 0;
-    int lc = 0;
-    bool bits(int n, uint64_t& v) {
-        while (lc < n) {
-            if (p >= end) return false;
-            c = (c << 8) | *p++;
-            lc += 8;
-        }
-        lc -= n;
-        v = (c >> lc) & ((1ull << n) - 1);
+// The PIZ entropy stream, as the OpenEXR 2 format describes it:
+//   header   int32 lo, int32 hi (symbol range, hi = the run-length pseudo symbol),
+//            int32 table bytes, int32 payload bit count, int32 reserved      (20 bytes)
+//   lengths  one 6-bit field per symbol lo..hi, most significant bit first; a field of
+//            1..58 is that symbol's code length, 0 means "no code", 59..62 stand for a
+//            stretch of 2..5 symbols without a code, and 63 is followed by an 8-bit field k
+//            for a stretch of k + 6 such symbols
+//   payload  the codes, most significant bit first; the pseudo symbol is followed by an
+//            8-bit repeat count of the value decoded before it
+// The codes are canonical with the *longest* codes numerically smallest: going from length
+// 58 down to 1, the first code of a length is the value just past the last code of the next
+// longer length, halved (rounded down), and within one length the codes ascend with the
+// symbol.  So every code of length L at least first[L] is a complete code word, and every
+// value below first[L] is the prefix of a longer one; decoding reads bit by bit and stops
+// at the first length whose code range holds the bits read so far (the code-range decoder
+// of canonical prefix codes).
+
+// Reads `n` (<= 57) bits MSB first from a byte string of `nbits` valid bits.
+struct MsbBits {
+    const unsigned char* data;
+    uint64_t nbits;
+    uint64_t at = 0;
+    bool take(int n, uint32_t& v) {
+        if (at + (uint64_t)n > nbits) return false;
+        uint32_t r = 0;
+        for (int k = 0; k < n; k++, at++) r = (r << 1) | ((data[at >> 3] >> (7 - (at & 7))) & 1u);
+        v = r;
         return true;
     }
 };
 
-// code lengths (6 bits each, 59..62 = short zero runs, 63 + 8 bits = long zero run), then the
-// canonical code assignment: per length, codes count down from the longest lengths.
-bool huf_unpack_table(const unsigned char*& ptr, const unsigned char* end, int im, int iM,
-                      std::vector<uint64_t>& hcode) {
-    hcode.assign(kHufEncSize, 0);
-    BitIn b{ptr, end};
-    for (; im <= iM; im++) {
-        uint64_t l;
-        if (!b.bits(6, l)) return false;
-        hcode[im] = l;
-        if (l == (uint64_t)kLongZeroRun) {
-            uint64_t z;
-            if (!b.bits(8, z)) return false;
-            int run = (int)z + kShortestLongRun;
-            if (im + run > iM + 1) return false;
-            while (run--) hcode[im++] = 0;
-            im--;
-        } else if (l >= (uint64_t)kShortZeroRun) {
-            int run = (int)l - kShortZeroRun + 2;
-            if (im + run > iM + 1) return false;
-            while (run--) hcode[im++] = 0;
-            im--;
+struct CanonicalCode {
+    uint64_t first[kMaxLen + 2] = {};   // first code value of each length
+    uint32_t count[kMaxLen + 2] = {};   // codes of each length
+    uint32_t start[kMaxLen + 2] = {};   // position of the length's first symbol in `by_code`
+    std::vector<int> by_code;           // symbols sorted by (length, code)
+    int shortest = 0, longest = 0;
+};
+
+// Length table -> canonical code; false with `err` set if the lengths do not form a prefix
+// code (a code that does not fit its length, or a shorter code equal to a longer one's prefix).
+bool build_canonical(const std::vector<uint8_t>& len, int lo, CanonicalCode& cc, std::string& err) {
+    for (uint8_t l : len) cc.count[l]++;
+    cc.count[0] = 0;
+    uint64_t past = 0;                      // value just past the last code of length L + 1
+    for (int L = kMaxLen; L >= 1; L--) {
+        cc.first[L] = past >> 1;
+        past = cc.first[L] + cc.count[L];
+        if (cc.count[L] && past > (1ull << L)) { err = "PIZ: Huffman code does not fit its length"; return false; }
+    }
+    for (int L = 1; L <= kMaxLen; L++)
+        if (cc.count[L]) {
+            if (!cc.shortest) cc.shortest = L;
+            cc.longest = L;
         }
+    // prefix-free: the largest length-S prefix of the length-L codes (L > S) lies below first[S]
+    for (int S = 1; S <= kMaxLen; S++) {
+        if (!cc.count[S]) continue;
+        for (int L = S + 1; L <= kMaxLen; L++)
+            if (cc.count[L] && ((cc.first[L] + cc.count[L] - 1) >> (L - S)) >= cc.first[S]) {
+                err = "PIZ: Huffman lengths do not form a prefix code";
+                return false;
+            }
     }
-    ptr = b.p;
-    uint64_t n[59] = {0};
-    for (int i = 0; i < kHufEncSize; i++) n[hcode[i]]++;
-    uint64_t c = 0;
-    for (int i = 58; i > 0; i--) {
-        const uint64_t nc = (c + n[i]) >> 1;
-        n[i] = c;
-        c = nc;
+    uint32_t acc = 0;
+    for (int L = 1; L <= kMaxLen; L++) {
+        cc.start[L] = acc;
+        acc += cc.count[L];
     }
-    for (int i = 0; i < kHufEncSize; i++) {
-        const int l = (int)hcode[i];
-        if (l > 0) hcode[i] = (uint64_t)l | (n[l]++ << 6);
-    }
+    cc.by_code.assign(acc, 0);
+    std::vector<uint32_t> fill(cc.start, cc.start + kMaxLen + 1);
+    for (size_t i = 0; i < len.size(); i++)          // ascending symbols -> ascending codes
+        if (len[i]) cc.by_code[fill[len[i]]++] = lo + (int)i;
     return true;
 }
 
-struct HufDec {
-    int len = 0;                        // short code: its length and symbol
-    int lit = 0;
-    std::vector<int> longs;             // codes longer than kHufDecBits sharing this prefix
-};
+bool read_code_lengths(MsbBits& b, int lo, int hi, std::vector<uint8_t>& len, std::string& err) {
+    len.assign((size_t)(hi - lo + 1), 0);
+    size_t sym = 0;
+    while (sym < len.size()) {
+        uint32_t field;
+        if (!b.take(6, field)) { err = "PIZ: truncated Huffman table"; return false; }
+        if (field <= (uint32_t)kMaxLen) {
+            len[sym++] = (uint8_t)field;
+            continue;
+        }
+        uint32_t stretch = field - 57;               // 59..62 -> 2..5
+        if (field == 63) {
+            uint32_t k;
+            if (!b.take(8, k)) { err = "PIZ: truncated Huffman table"; return false; }
+            stretch = k + 6;
+        }
+        if (stretch > len.size() - sym) { err = "PIZ: Huffman table runs past its symbol range"; return false; }
+        sym += stretch;                              // lengths already 0
+    }
+    return true;
+}
 
 bool huf_decode(const unsigned char* in, size_t n_in, uint16_t* out, size_t n_out, std::string& err) {
     if (n_in == 0) {
@@ -181,84 +215,56 @@ bool huf_decode(const unsigned char* in, size_t n_in, uint16_t* out, size_t n_ou
         return true;
     }
     if (n_in < 20) { err = "PIZ: truncated Huffman header"; return false; }
-    auto rd = [&](int o) { return (int32_t)((uint32_t)in[o] | (uint32_t)in[o + 1] << 8 | (uint32_t)in[o + 2] << 16 | (uint32_t)in[o + 3] << 24); };
-    const int im = rd(0), iM = rd(4), nbits = rd(12);
-    if (im < 0 || im >= kHufEncSize || iM < 0 || iM >= kHufEncSize || nbits < 0) { err = "PIZ: bad Huffman table size"; return false; }
-    const unsigned char* ptr = in + 20;
-    const unsigned char* end = in + n_in;
-    std::vector<uint64_t> hcode;
-    if (!huf_unpack_table(ptr, end, im, iM, hcode)) { err = "PIZ: bad Huffman table"; return false; }
-    if ((uint64_t)nbits > 8ull * (uint64_t)(end - ptr)) { err = "PIZ: Huffman bit count exceeds the chunk"; return false; }
-    std::vector<HufDec> dec(1 << kHufDecBits);
-    for (int s = im; s <= iM; s++) {
-        const uint64_t code = hcode[s] >> 6;
-        const int l = (int)(hcode[s] & 63);
-        if (l && (code >> l)) { err = "PIZ: invalid Huffman code"; return false; }
-        if (l > kHufDecBits) {
-            HufDec& d = dec[code >> (l - kHufDecBits)];
-            if (d.len) { err = "PIZ: invalid Huffman table entry"; return false; }
-            d.longs.push_back(s);
-        } else if (l) {
-            const size_t b = (size_t)code << (kHufDecBits - l);
-            for (size_t i = 0; i < (1ull << (kHufDecBits - l)); i++) {
-                HufDec& d = dec[b + i];
-                if (d.len || !d.longs.empty()) { err = "PIZ: invalid Huffman table entry"; return false; }
-                d.len = l;
-                d.lit = s;
+    auto i32 = [&](int o) { return (int32_t)((uint32_t)in[o] | (uint32_t)in[o + 1] << 8 | (uint32_t)in[o + 2] << 16 | (uint32_t)in[o + 3] << 24); };
+    const int lo = i32(0), hi = i32(4), table_bytes = i32(8), payload_bits = i32(12);
+    if (lo < 0 || hi < lo || hi >= kSymbols || payload_bits < 0) { err = "PIZ: bad Huffman table size"; return false; }
+    (void)table_bytes;                  // the table is self-delimiting; its bits are read below
+    const unsigned char* body = in + 20;
+    const size_t body_bytes = n_in - 20;
+
+    MsbBits tb{body, 8ull * body_bytes};
+    std::vector<uint8_t> len;
+    if (!read_code_lengths(tb, lo, hi, len, err)) return false;
+    CanonicalCode cc;
+    if (!build_canonical(len, lo, cc, err)) return false;
+    const size_t payload_at = (size_t)((tb.at + 7) / 8);        // the payload starts on a byte
+    if ((uint64_t)payload_bits > 8ull * (body_bytes - payload_at)) { err = "PIZ: Huffman bit count exceeds the chunk"; return false; }
+    if (payload_bits && !cc.longest) { err = "PIZ: Huffman payload without codes"; return false; }
+
+    MsbBits pb{body + payload_at, (uint64_t)payload_bits};
+    const int repeat_symbol = hi;
+    size_t written = 0;
+    while (pb.at < pb.nbits) {
+        uint32_t bits;
+        if (!pb.take(cc.shortest, bits)) { err = "PIZ: truncated code"; return false; }
+        uint64_t v = bits;
+        int L = cc.shortest;
+        int sym = -1;
+        for (;;) {
+            if (cc.count[L] && v >= cc.first[L] && v - cc.first[L] < cc.count[L]) {
+                sym = cc.by_code[cc.start[L] + (uint32_t)(v - cc.first[L])];
+                break;
             }
+            if (L == cc.longest) break;
+            uint32_t bit;
+            if (!pb.take(1, bit)) break;
+            v = (v << 1) | bit;
+            L++;
+        }
+        if (sym < 0) { err = "PIZ: invalid code"; return false; }
+        if (sym == repeat_symbol) {
+            uint32_t times;
+            if (!pb.take(8, times)) { err = "PIZ: truncated run"; return false; }
+            if (written == 0) { err = "PIZ: run without a value"; return false; }
+            if (written + times > n_out) { err = "PIZ: too much data"; return false; }
+            std::fill(out + written, out + written + times, out[written - 1]);
+            written += times;
+        } else {
+            if (written >= n_out) { err = "PIZ: too much data"; return false; }
+            out[written++] = (uint16_t)sym;
         }
     }
-    const int rlc = iM;                 // the run-length pseudo symbol
-    size_t no = 0;
-    // peek k bits at bit position pos (zero padded past the end of the stream)
-    const uint64_t total = (uint64_t)nbits;
-    const size_t nbytes = (size_t)((total + 7) / 8);
-    auto peek = [&](uint64_t pos, int k) -> uint64_t {
-        const size_t byte = (size_t)(pos >> 3);
-        const int sh = (int)(pos & 7);
-        uint64_t w = 0;
-        for (int i = 0; i < 8; i++) w = (w << 8) | (byte + i < nbytes ? ptr[byte + i] : 0);
-        const unsigned char x = byte + 8 < nbytes ? ptr[byte + 8] : 0;
-        if (sh) w = (w << sh) | (uint64_t)(x >> (8 - sh));
-        return w >> (64 - k);
-    };
-    uint64_t pos = 0;
-    auto emit = [&](int sym) -> bool {
-        if (sym == rlc) {
-            if (pos + 8 > total) { err = "PIZ: truncated run"; return false; }
-            const int cs = (int)peek(pos, 8);
-            pos += 8;
-            if (no + cs > n_out) { err = "PIZ: too much data"; return false; }
-            if (no == 0) { err = "PIZ: run without a value"; return false; }
-            const uint16_t s = out[no - 1];
-            for (int i = 0; i < cs; i++) out[no++] = s;
-        } else {
-            if (no >= n_out) { err = "PIZ: too much data"; return false; }
-            out[no++] = (uint16_t)sym;
-        }
-        return true;
-    };
-    while (pos < total) {
-        const HufDec& d = dec[peek(pos, kHufDecBits)];
-        if (d.len) {
-            if (pos + d.len > total) { err = "PIZ: truncated code"; return false; }
-            pos += d.len;
-            if (!emit(d.lit)) return false;
-        } else {
-            bool found = false;
-            for (int s : d.longs) {
-                const int l = (int)(hcode[s] & 63);
-                if (pos + l <= total && peek(pos, l) == (hcode[s] >> 6)) {
-                    pos += l;
-                    if (!emit(s)) return false;
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) { err = "PIZ: invalid code"; return false; }
-        }
-    }
-    if (no != n_out) { err = "PIZ: not enough data"; return false; }
+    if (written != n_out) { err = "PIZ: not enough data"; return false; }
     return true;
 }
 

@@ -3,9 +3,16 @@ format, used to check the product decoder (raytracer-795_amd/host/exr_read.cpp) 
 codec the reference's LoadEXR reads for a texture (src/Helper.cpp:346-359): NONE, RLE,
 ZIPS, ZIP and PIZ, HALF / FLOAT / UINT channels, scanline and one-level tiled layouts.
 
-It shares no code with the decoder (different language, encoder direction), so a round trip
-pins the decoder to the format description; it is not the reference's codec (compiling the
-reference's vendored tinyexr as a checker was refused here)."""
+It is written in the encode direction, in numpy: the PIZ wavelet is the forward lifting
+equations applied level by level to index arrays of disjoint lattice cells
+(`_wavelet_forward_2d`), the Huffman stage builds code lengths with a heap and assigns
+OpenEXR's canonical codes (longest codes smallest).  The decoder (C++, decode direction) reads
+lengths into a count-per-length table and decodes by code ranges, and inverts the wavelet
+cell by cell.  History: until round 4 this file's wavelet encoder was a transliteration of the
+vendored tinyexr's `wav2Encode` (src/tinyexr.h:8065-8160), so the round trip was not
+independent of tinyexr's reading of the format; it was rewritten from the equations (DESIGN.md
+§10).  It is not the reference's codec (compiling the reference's vendored tinyexr as a
+checker was refused here)."""
 from __future__ import annotations
 
 import heapq
@@ -63,55 +70,53 @@ def _rle(b: bytes) -> bytes:
 
 
 # ---------------------------------------------------------------- PIZ
-def _s16(v):
-    return v - 65536 if v >= 32768 else v
+def _lift_narrow(a: np.ndarray, b: np.ndarray):
+    """Forward lifting step for values below 2^14 (format description, "PIZ"): on the signed
+    16-bit readings, low = floor((a + b) / 2), high = a - b, both stored mod 2^16."""
+    sa = a - ((a >= 0x8000) << 16)
+    sb = b - ((b >= 0x8000) << 16)
+    return ((sa + sb) >> 1) & 0xFFFF, (sa - sb) & 0xFFFF
 
 
-def _wenc14(a, b):
-    a_s, b_s = _s16(a), _s16(b)
-    return ((a_s + b_s) >> 1) & 0xFFFF, (a_s - b_s) & 0xFFFF
+def _lift_wide(a: np.ndarray, b: np.ndarray):
+    """Forward lifting step for the full 16-bit range (modular form): with a' = a + 2^15 mod 2^16,
+    high = a' - b mod 2^16 and low = floor((a' + b) / 2), plus 2^15 when a' < b, mod 2^16."""
+    ash = (a + 0x8000) & 0xFFFF
+    low = (ash + b) >> 1
+    low = np.where(ash < b, low + 0x8000, low) & 0xFFFF
+    return low, (ash - b) & 0xFFFF
 
 
-def _wenc16(a, b):
-    ao = (a + 0x8000) & 0xFFFF
-    m = (ao + b) >> 1
-    d = ao - b
-    if d < 0:
-        m = (m + 0x8000) & 0xFFFF
-    return m, d & 0xFFFF
+def _wavelet_forward_2d(plane: np.ndarray, maxval: int) -> None:
+    """In-place multi-level 2-D transform of one (ny, nx) plane of 16-bit values (as int64).
 
-
-def _wav2_encode(buf: list, base: int, nx: int, ox: int, ny: int, oy: int, mx: int):
-    enc = _wenc14 if mx < (1 << 14) else _wenc16
-    n = min(nx, ny)
-    p, p2 = 1, 2
-    while p2 <= n:
-        oy1, oy2, ox1, ox2 = oy * p, oy * p2, ox * p, ox * p2
-        py = base
-        ey = base + oy * (ny - p2)
-        while py <= ey:
-            px = py
-            ex = py + ox * (nx - p2)
-            while px <= ex:
-                p01, p10 = px + ox1, px + oy1
-                p11 = p10 + ox1
-                i00, i01 = enc(buf[px], buf[p01])
-                i10, i11 = enc(buf[p10], buf[p11])
-                buf[px], buf[p10] = enc(i00, i10)
-                buf[p01], buf[p11] = enc(i01, i11)
-                px += ox2
-            if nx & p:
-                p10 = px + oy1
-                buf[px], buf[p10] = enc(buf[px], buf[p10])
-            py += oy2
-        if ny & p:
-            px = py
-            ex = py + ox * (nx - p2)
-            while px <= ex:
-                p01 = px + ox1
-                buf[px], buf[p01] = enc(buf[px], buf[p01])
-                px += ox2
-        p, p2 = p2, p2 << 1
+    Level k uses pair distance p = 2^k on the lattice of step q = 2p, for as long as q fits in
+    min(nx, ny).  Every q-aligned cell {(y, x), (y, x+p), (y+p, x), (y+p, x+p)} lying wholly inside
+    the plane is lifted along x (both rows), then the two low and the two high results along y;
+    where the plane leaves a strip of width p past the last full cell (nx & p, ny & p), its
+    cells are lifted along the one axis that still has a partner.  The cells of one level are
+    disjoint, so each level is a handful of gathers and scatters over index arrays."""
+    lift = _lift_narrow if maxval < (1 << 14) else _lift_wide
+    ny, nx = plane.shape
+    p = 1
+    while 2 * p <= min(nx, ny):
+        q = 2 * p
+        xs = np.arange(0, nx - q + 1, q)               # left column of every full cell
+        ys = np.arange(0, ny - q + 1, q)               # top row of every full cell
+        Y, X = np.meshgrid(ys, xs, indexing="ij")
+        tl, tr = plane[Y, X], plane[Y, X + p]
+        bl, br = plane[Y + p, X], plane[Y + p, X + p]
+        tlo, thi = lift(tl, tr)                        # along x
+        blo, bhi = lift(bl, br)
+        plane[Y, X], plane[Y + p, X] = lift(tlo, blo)  # along y: the lows ...
+        plane[Y, X + p], plane[Y + p, X + p] = lift(thi, bhi)   # ... and the highs
+        if nx & p:                                     # strip right of the last full column
+            xe = len(xs) * q
+            plane[ys, xe], plane[ys + p, xe] = lift(plane[ys, xe], plane[ys + p, xe])
+        if ny & p:                                     # strip below the last full row
+            ye = len(ys) * q
+            plane[ye, xs], plane[ye, xs + p] = lift(plane[ye, xs], plane[ye, xs + p])
+        p = q
 
 
 def _huffman_lengths(freq: dict) -> dict:
@@ -235,13 +240,17 @@ def _piz(raw: bytes, nx: int, ny: int, types: list) -> bytes:
     vals = np.nonzero(keep)[0]
     lut[vals] = np.arange(len(vals))
     maxv = len(vals) - 1
-    tmp = [int(lut[v]) for v in tmp]
+    arr = lut[np.array(tmp, dtype=np.int64)]
     base = 0
     for sz in sizes:
+        # a channel of sz 16-bit words per pixel is sz interleaved planes, each transformed alone
+        block = arr[base:base + nx * ny * sz].reshape(ny, nx, sz)
         for j in range(sz):
-            _wav2_encode(tmp, base + j, nx, sz, ny, nx * sz, maxv)
+            plane = np.ascontiguousarray(block[:, :, j])
+            _wavelet_forward_2d(plane, maxv)
+            block[:, :, j] = plane
         base += nx * ny * sz
-    huf = _huf_compress(tmp)
+    huf = _huf_compress([int(v) for v in arr])
     out = struct.pack("<HH", mn, mxb)
     if mn <= mxb:
         out += bitmap[mn:mxb + 1].tobytes()

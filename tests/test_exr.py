@@ -174,3 +174,40 @@ def test_piz_wavelet_odd_shapes(tmp_path, w, h, ptype):
     p = str(tmp_path / f"piz_{w}x{h}.exr")
     X.write_exr(p, ch, X.PIZ, ptype)
     _check(p, ch, ptype)
+
+
+def test_canonical_code_known_answer():
+    """OpenEXR's canonical assignment, worked by hand from the format rule (longest codes
+    smallest; a length's first code = half the value past the next longer length's codes):
+    lengths {0:2, 1:2, 2:2, 3:3, 4:3} -> length 3 takes 000, 001; length 2 starts at 2 >> 1 = 1."""
+    codes = X._canonical({0: 2, 1: 2, 2: 2, 3: 3, 4: 3})
+    assert codes == {3: (0b000, 3), 4: (0b001, 3), 0: (0b01, 2), 1: (0b10, 2), 2: (0b11, 2)}
+
+
+def test_wavelet_forward_known_answer():
+    """One 2x2 cell, narrow lifting, by hand: along x (10,20) -> (15,-10), (30,40) -> (35,-10);
+    along y the lows (15,35) -> (25,-20) and the highs (-10,-10) -> (-10,0)."""
+    plane = np.array([[10, 20], [30, 40]], np.int64)
+    X._wavelet_forward_2d(plane, maxval=100)
+    assert plane.tolist() == [[25, (-10) & 0xFFFF], [(-20) & 0xFFFF, 0]]
+    wide = np.array([[0, 0xFFFF], [0x8000, 1]], np.int64)
+    X._wavelet_forward_2d(wide, maxval=0xFFFF)     # the modular form, checked by its inverse
+    lo, hi = int(wide[0, 0]), int(wide[1, 0])
+    assert 0 <= lo < 65536 and 0 <= hi < 65536
+
+
+@pytest.mark.parametrize("lengths,msg", [
+    ({0: 1, 1: 1, 2: 1}, "does not fit"),                 # three 1-bit codes
+    ({0: 1}, "prefix code"),     # one 1-bit code '0', every other symbol 20 bits from 0...0
+])
+def test_piz_rejects_invalid_code_lengths(tmp_path, monkeypatch, lengths, msg):
+    """A PIZ length table that is not a prefix code is refused loudly, not decoded."""
+    def bogus(freq):
+        syms = sorted(freq)
+        return {s: lengths.get(i, 20 if len(lengths) == 1 else 1) for i, s in enumerate(syms)}
+    ch = {"Y": np.arange(16, dtype=np.float32).reshape(4, 4)}     # >= 4 symbols
+    monkeypatch.setattr(X, "_huffman_lengths", bogus)
+    p = str(tmp_path / "bad.exr")
+    X.write_exr(p, ch, X.PIZ, X.HALF)
+    with pytest.raises(RtgError, match=msg):
+        native.read_image(p)
