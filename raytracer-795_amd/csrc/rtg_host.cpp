@@ -20,6 +20,7 @@
 #include <deque>
 #include <exception>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -1163,7 +1164,13 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 tg.p1 = make_float4(amb.y, amb.z, amc.x, amc.y);
                 // c - b: with a - b the flat normal (c - b) x (a - b) of Triangle::bvhIntersect
                 // (src/Shape.cpp:327), so the shading of a flat triangle reads this record only
-                // (the traversal copy, stris, reuses p2.yzw)
+                // (the traversal copy, stris, reuses p2.yzw).  The device formed cc - b itself
+                // before; the two agree bit for bit only because this is one IEEE f32 subtraction
+                // (no contraction can apply to a lone subtraction) on f32 components, which the
+                // static_assert pins.  Covered at run time by the flat, non-Triangle floor mesh of
+                // the dragon scenes in the simple shading variant (test_gpu_fullsize.py band,
+                // test_gpu_parity.py images).
+                static_assert(std::is_same<decltype(cmb.x), float>::value, "flat-normal c - b must be f32");
                 tg.p2 = make_float4(amc.z, cmb.x, cmb.y, cmb.z);
                 int smooth = (o.type == RTG_OBJ_TRIANGLE) ? 1 : o.smooth;   // Shape.cpp:262-276 quirk
                 pi = make_int4(i1, i2, i3, smooth);

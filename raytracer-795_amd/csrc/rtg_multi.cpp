@@ -416,8 +416,9 @@ struct rtg_comm {
 
 namespace rtg {
 namespace {
-// Every rank learns whether any rank failed before the gather (an allreduce-max of a failure
-// flag), so a rank that fails early cannot leave the others blocked in ncclRecv / ncclSend.
+// Every rank learns whether any rank failed before the gather (an allreduce-sum of 0 / 1
+// failure flags: the count of failed ranks), so a rank that fails early cannot leave the others
+// blocked in ncclRecv / ncclSend.
 // Returns the number of failed ranks seen (>= 1 means: do not gather), or < 0 when the
 // agreement itself failed (the communicator is then unusable).
 int agree_failures(rtg_comm* c, bool failed, hipStream_t st, std::string& why) {
@@ -491,34 +492,49 @@ int32_t rtg_render_ranked(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
                           float* frame_device, void* stream) {
     return guarded([&]() -> int32_t {
         if (!c) return set_error(RTG_ERR_INVALID, "null communicator");
+        // The one early return that skips the failure agreement: without its device this rank
+        // cannot take part in any collective, so its peers can still block in the agreement
+        // until the job's own timeout (or the caller aborts the communicator).
         if (hipSetDevice(c->device) != hipSuccess) return set_error(RTG_ERR_NO_DEVICE, "hipSetDevice");
         hipStream_t st = (hipStream_t)stream;
-        // Local checks and the shard render record a status instead of returning: every rank
-        // reaches the failure agreement below, whatever happened to it (no rank is left waiting
-        // in the gather for a rank that gave up).
+        // Local checks and the shard render record a status instead of returning, and an
+        // exception thrown by them (bad_alloc while growing a buffer, ...) becomes a status too:
+        // every rank reaches the failure agreement below, whatever happened to it (no rank is
+        // left waiting in the gather for a rank that gave up).
         int rc = RTG_OK;
         rtg_render_opts o{};
         if (opts) o = *opts;
-        if (!s || !cam) rc = set_error(RTG_ERR_INVALID, "null argument");
-        else if (c->rank == 0 && !frame_device) rc = set_error(RTG_ERR_INVALID, "rank 0 needs the frame buffer");
-        else if (scene_device(s) != c->device) rc = set_error(RTG_ERR_INVALID, "scene and communicator on different devices");
-        else if (cam->nx < 1 || cam->ny < 1 || cam->num_samples < 1) rc = set_error(RTG_ERR_INVALID, "bad camera");
-        else if (o.num_devices > 1 || o.devices) rc = set_error(RTG_ERR_INVALID, "rtg_render_ranked: one device per rank");
         const int n = c->nranks;
         const int block = o.row_block > 1 ? o.row_block : 4;
-        const int nx = rc == RTG_OK ? cam->nx : 0, ny = rc == RTG_OK ? cam->ny : 0;
+        int nx = 0, ny = 0;
         const auto t0 = std::chrono::steady_clock::now();
-        if (rc == RTG_OK) {
-            const ShardPrefix pre = shard_prefix(ny, n, block);
-            const size_t rows = (size_t)std::max(pre.rows[c->rank + 1] - pre.rows[c->rank], 1);
-            rc = c->part.grow(c->device, rows * nx * 3 * sizeof(float));
-            if (rc == RTG_OK && c->rank == 0) rc = c->recv.grow(c->device, (size_t)ny * nx * 3 * sizeof(float));
-        }
-        if (rc == RTG_OK) {
-            const rtg_render_opts so = shard_opts(o, c->rank, n, block);
-            rc = scene_render(s, cam, &so, c->part.f(), st);
+        try {
+            if (!s || !cam) rc = set_error(RTG_ERR_INVALID, "null argument");
+            else if (c->rank == 0 && !frame_device) rc = set_error(RTG_ERR_INVALID, "rank 0 needs the frame buffer");
+            else if (scene_device(s) != c->device) rc = set_error(RTG_ERR_INVALID, "scene and communicator on different devices");
+            else if (cam->nx < 1 || cam->ny < 1 || cam->num_samples < 1) rc = set_error(RTG_ERR_INVALID, "bad camera");
+            else if (o.num_devices > 1 || o.devices) rc = set_error(RTG_ERR_INVALID, "rtg_render_ranked: one device per rank");
+            if (rc == RTG_OK) {
+                nx = cam->nx;
+                ny = cam->ny;
+                const ShardPrefix pre = shard_prefix(ny, n, block);
+                const size_t rows = (size_t)std::max(pre.rows[c->rank + 1] - pre.rows[c->rank], 1);
+                rc = c->part.grow(c->device, rows * nx * 3 * sizeof(float));
+                if (rc == RTG_OK && c->rank == 0) rc = c->recv.grow(c->device, (size_t)ny * nx * 3 * sizeof(float));
+            }
+            if (rc == RTG_OK) {
+                const rtg_render_opts so = shard_opts(o, c->rank, n, block);
+                rc = scene_render(s, cam, &so, c->part.f(), st);
+            }
+            // the shard's own completion, so the agreement + gather time below is theirs alone
+            if (rc == RTG_OK && hipStreamSynchronize(st) != hipSuccess) rc = set_error(RTG_ERR_HIP, "shard render sync");
+        } catch (const std::bad_alloc&) {
+            rc = set_error(RTG_ERR_OOM, "host allocation failed in the shard render");
+        } catch (const std::exception& e) {
+            rc = set_error(RTG_ERR_HIP, std::string("shard render: ") + e.what());
         }
         const std::string local_err = rc == RTG_OK ? std::string() : std::string(rtg_last_error());
+        const auto t1 = std::chrono::steady_clock::now();
         std::string why;
         const int failed = agree_failures(c, rc != RTG_OK, st, why);
         if (failed < 0) return set_error(RTG_ERR_HIP, "rank status agreement: " + why +
@@ -526,13 +542,12 @@ int32_t rtg_render_ranked(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
         if (rc != RTG_OK) return set_error(rc, local_err);
         if (failed > 0)
             return set_error(RTG_ERR_HIP, std::to_string(failed) + " other rank(s) failed before the gather");
-        const auto t1 = std::chrono::steady_clock::now();
         if ((rc = gather_rows(*c->R, c->comm, c->rank, n, nx, ny, block, c->part.f(), c->recv.f(), frame_device, st)))
             return rc;
         if (hipStreamSynchronize(st) != hipSuccess) return set_error(RTG_ERR_HIP, "gather sync");
         rtg_render_stats t = scene_stats(s);
         t.render_ms = ms_since(t0);
-        t.gather_ms = ms_since(t1);
+        t.gather_ms = ms_since(t1);             // failure agreement + gather, after the shard finished
         t.devices = n;
         scene_set_stats(s, t);
         return RTG_OK;

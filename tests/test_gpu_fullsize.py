@@ -8,7 +8,7 @@
   (src/BVH.cpp:137-210) inside BVHMethods::FindIntersection (src/Helper.cpp:18-80).
 * 1920x1080 row bands of the bench frames against the oracle's rows of the same frame:
   dragon1m 64 spp (16 rows through the glass and mirror spheres), cornell_dynamic 64 spp (C4)
-  and cornell_pt 256 spp (C5).  The oracle renders only the band (row_begin / row_end);
+  and cornell_pt 256 spp (C5), 64 rows each.  The oracle renders only the band (row_begin / row_end);
   the GPU renders the whole frame exactly as bench.py does.
 """
 import numpy as np
@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 
 SAH, REF_TREE = 0, 1
 BAND = (800, 816)       # rows 800..815: glass sphere, mirror sphere, dragon, floor (C3)
+WIDE_BAND = (760, 824)  # 64 rows for C4 / C5 (VERDICT r3 "weak" #1: 16 rows were too few)
 
 
 def _bits(a):
@@ -95,15 +96,15 @@ def test_dragon1m_1080p64_band_bit_exact(gpu, dragon):
 @pytest.mark.parametrize("name,spp", [("cornell", 64), ("cornell_pt", 256)])
 def test_cornell_1080p_band_matches_oracle(gpu, name, spp):
     """C4 (distribution ray tracing: DoF, motion blur, area light, rough mirror, instances) and
-    C5 (hw7 path tracer) at the bench resolution and spp, 16 rows against the oracle."""
+    C5 (hw7 path tracer) at the bench resolution and spp, 64 rows against the oracle."""
     sc = getattr(scenegen, name)(1920, 1080, spp=spp)
     orc = pyoracle.Oracle(sc)
-    ref = orc.render(0, row_begin=BAND[0], row_end=BAND[1])[0]
+    ref = orc.render(0, row_begin=WIDE_BAND[0], row_end=WIDE_BAND[1])[0]
     with rtg.Renderer(sc, device=gpu) as r:
         img = r.render(0)
-    band = slice(*BAND)
+    band = slice(*WIDE_BAND)
     linf, ndiff, nanm = _cmp(img[band], ref[band])
-    print(f"{name} 1080p{spp} rows {BAND}: Linf={linf:.3g} differing={ndiff} nan_mismatch={nanm}")
+    print(f"{name} 1080p{spp} rows {WIDE_BAND}: Linf={linf:.3g} differing={ndiff} nan_mismatch={nanm}")
     assert nanm == 0
     assert linf < 1e-3
     assert ndiff == 0
