@@ -264,6 +264,18 @@ def roofline(counters, st_roof, st_stats, workload: str, ms_per_step: float, pt:
     return roof
 
 
+def create_phases(bs: dict, create_ms: float) -> dict:
+    """rtg_build_stats' wall-time split of rtg_scene_create (ABI 7), plus the Python descriptor
+    build around it (Renderer(scene) - the library call)."""
+    keys = ("validate_ms", "prep_ms", "median_tree_ms", "records_ms", "traversal_tree_ms", "top_level_ms",
+            "upload_ms", "total_ms")
+    out = {k[:-3]: round(bs[k], 1) for k in keys if k in bs}
+    if "total_ms" in bs:
+        out["desc_python"] = round(create_ms - bs["total_ms"], 1)
+        out["upload_MB"] = round(bs["upload_bytes"] / 1e6, 1)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -466,7 +478,9 @@ def main():
                 "ms_per_frame_to_host": round(elapsed_h * 1e3 / args.steps, 2),
                 "end_to_end_ms": {"scene_create": round(create_ms, 1), "first_frame_to_host": round(first_frame_ms, 1),
                                   "total": round(create_ms + first_frame_ms, 1),
-                                  "note": "rtg_scene_create (BVH build + upload) + the first frame incl. its D2H copy"},
+                                  "scene_create_phases": create_phases(r.build_stats(), create_ms),
+                                  "note": "Renderer(scene) = the Python host's descriptor (desc_python) + "
+                                          "rtg_scene_create (library phases), then the first frame incl. its D2H copy"},
                 "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
                 "kernel_ms_rank0_streams1": {k: round(st_roof[f"{k}_ms"], 2)
                                              for k in ("trace", "shade", "shadow", "resolve", "accumulate")},

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 6
+#define RTG_ABI_VERSION 7
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -340,6 +340,19 @@ typedef struct rtg_build_stats {
     int32_t bvh_gpu_objects; /* objects whose BVH was built on the GPU */
     int32_t num_objects;
     int32_t tlas_nodes;      /* nodes of the top-level BVH (0: linear object loop) */
+    int32_t pad0;
+    /* ABI 7: wall-time split of rtg_scene_create (ms), in build order.  Together they cover the
+       whole call (total_ms); the reference does this work at the start of renderScene
+       (src/Scene.cpp:296-323, BVH.cpp:53-62). */
+    double validate_ms;      /* descriptor checks (every face index) */
+    double prep_ms;          /* vertices, per-object primitive lists, matrices, smooth normals */
+    double median_tree_ms;   /* the reference's median-split trees (= bvh_build_ms) */
+    double records_ms;       /* triangle records, reference-node flattening, reachability gates */
+    double traversal_tree_ms;/* the SAH 4-wide traversal trees (build + collapse) */
+    double top_level_ms;     /* entries, world boxes, top-level BVH, materials, textures, lights */
+    double upload_ms;        /* host -> device copies of every scene buffer */
+    double total_ms;         /* the whole rtg_scene_create call */
+    uint64_t upload_bytes;   /* bytes copied to the device */
 } rtg_build_stats;
 int32_t rtg_scene_build_stats(const rtg_scene* scene, rtg_build_stats* out);
 int32_t rtg_scene_destroy(rtg_scene* scene);

@@ -852,6 +852,7 @@ struct rtg_scene {
     int num_lanes = 8;                       // default passes in flight (env RTG_STREAMS overrides)
     int bvh_builder = RTG_BVH_AUTO;
     double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
+    rtg_build_stats bst{};                   // last scene build: per-phase wall times
     int bvh_gpu_objects = 0;                 // objects whose BVH the GPU built
     bool replica = false;                    // device copy made by scene_replicate (no host-side structures)
     rtg::MultiState* multi = nullptr;        // num_devices fan-out: replicas, RCCL communicators (rtg_multi.cpp)
@@ -992,7 +993,20 @@ int32_t rtg_scene_destroy(rtg_scene* s) {
     return RTG_OK;
 }
 
+// Wall-clock laps of the scene build (rtg_build_stats phases).
+struct PhaseClock {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    double lap() {
+        const auto n = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+        return ms;
+    }
+};
+
 static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
+    PhaseClock pc;
+    rtg_build_stats& bs = s->bst;
     const int nv = d->num_vertices;
     std::vector<V3> verts(nv);
     for (int i = 0; i < nv; i++) verts[i] = v3(d->vertices[3 * i], d->vertices[3 * i + 1], d->vertices[3 * i + 2]);
@@ -1046,6 +1060,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         V3 n = normalized(vn[i]);
         s->vnormals[3 * i] = n.x; s->vnormals[3 * i + 1] = n.y; s->vnormals[3 * i + 2] = n.z;
     }
+    bs.prep_ms += pc.lap();
 
     // BVHs and device geometry
     std::vector<Geometry> geoms(d->num_objects);
@@ -1082,6 +1097,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         ob.perm.resize(np);
         for (int k = 0; k < np; k++) ob.perm[k] = k;
         BuildCtx B{centers.data(), bmin.data(), bmax.data(), &ob.perm, &ob.nodes, {}};
+        bs.prep_ms += pc.lap();
         auto tb0 = std::chrono::steady_clock::now();
         bool use_gpu = s->device >= 0 && o.type != RTG_OBJ_SPHERE &&
                        (s->bvh_builder == RTG_BVH_GPU || (s->bvh_builder == RTG_BVH_AUTO && np >= 4096));
@@ -1127,6 +1143,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         }
         const double bms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
         s->bvh_build_ms += bms;
+        bs.median_tree_ms += pc.lap();
         if (getenv("RTG_BUILD_TIMING"))
             fprintf(stderr, "[rtg] object %d: %d prims, BVH %s %.1f ms\n", i, np, use_gpu ? "gpu" : "host", bms);
 
@@ -1247,6 +1264,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         for (int k = 0; k < np && sah_ok; k++)
             sah_ok = std::isfinite(bmin[k].x) && std::isfinite(bmin[k].y) && std::isfinite(bmin[k].z) &&
                      std::isfinite(bmax[k].x) && std::isfinite(bmax[k].y) && std::isfinite(bmax[k].z);
+        bs.records_ms += pc.lap();
         if (sah_ok && s->blas_mode != 1) {
             std::vector<SahBox> pb(np);
             std::vector<V3> pc(np);
@@ -1292,6 +1310,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 }
             }
         }
+        bs.traversal_tree_ms += pc.lap();
         if (ob.root < 0) {
             g.node_base = -1; g.root_leaf_start = g.prim_base; g.root_leaf_count = -1;
         } else if (hn[ob.root].left < 0 && hn[ob.root].right < 0) {
@@ -1513,6 +1532,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         s->num_emit++;
     }
 
+    bs.top_level_ms += pc.lap();
     if (s->device < 0) return RTG_OK;   // host-only build (introspection / CPU tests)
     std::vector<float> vflat(d->vertices, d->vertices + 3 * (size_t)nv);
     std::vector<float> tcflat;
@@ -1527,6 +1547,9 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         (rc = upload(s->d_topemit, top_emit)) || (rc = upload(s->d_etris, etris)) || (rc = upload(s->d_ecdf, ecdf)) ||
         (rc = upload(s->d_tlas, tlas_nodes)) || (rc = upload(s->d_tlasidx, tlas_idx)))
         return rc;
+    bs.upload_bytes = 0;
+    for (DBuf* b : scene_buffers(s)) bs.upload_bytes += b->used;
+    bs.upload_ms += pc.lap();
 
     SceneView& sv = s->sv;
     bind_view(s);
@@ -1589,8 +1612,10 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         if (opts && (opts->tlas < 0 || opts->tlas > 2)) return fail(RTG_ERR_INVALID, "tlas");
         if (opts && (opts->traversal_tree < 0 || opts->traversal_tree > 1)) return fail(RTG_ERR_INVALID, "traversal_tree");
         *out = nullptr;
+        PhaseClock whole;
         int rc = validate(desc);
         if (rc) return rc;
+        const double validate_ms = whole.lap();
         if (device >= 0) {
             int n = 0;
             if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RTG_ERR_NO_DEVICE, "no HIP device");
@@ -1608,12 +1633,14 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         s->blas_mode = opts ? opts->traversal_tree : 0;
         if (const char* e = getenv("RTG_SAH")) s->blas_mode = atoi(e) == 0 ? 1 : 0;
         if (const char* e = getenv("RTG_TLAS")) s->tlas_mode = atoi(e) == 0 ? 1 : 2;
+        s->bst.validate_ms = validate_ms;
         rc = build_scene(s, desc);
         if (rc) {
             scene_free(s);
             delete s;
             return rc;
         }
+        s->bst.total_ms = validate_ms + whole.lap();
         *out = s;
         return RTG_OK;
     });
@@ -2144,6 +2171,7 @@ int32_t rtg_tonemap(int32_t device, const float* hdr, int32_t nx, int32_t ny, co
 
 int32_t rtg_scene_build_stats(const rtg_scene* s, rtg_build_stats* out) {
     if (!s || !out) return fail(RTG_ERR_INVALID, "null argument");
+    *out = s->bst;
     out->bvh_build_ms = s->bvh_build_ms;
     out->bvh_gpu_objects = s->bvh_gpu_objects;
     out->num_objects = s->num_objects;

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 6
+RTG_ABI_VERSION = 7
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -136,7 +136,10 @@ class BuildOpts(C.Structure):
 
 class BuildStats(C.Structure):
     _fields_ = [("bvh_build_ms", C.c_double), ("bvh_gpu_objects", C.c_int32), ("num_objects", C.c_int32),
-                ("tlas_nodes", C.c_int32)]
+                ("tlas_nodes", C.c_int32), ("pad0", C.c_int32),
+                ("validate_ms", C.c_double), ("prep_ms", C.c_double), ("median_tree_ms", C.c_double),
+                ("records_ms", C.c_double), ("traversal_tree_ms", C.c_double), ("top_level_ms", C.c_double),
+                ("upload_ms", C.c_double), ("total_ms", C.c_double), ("upload_bytes", C.c_uint64)]
 
 
 RTG_BVH_AUTO, RTG_BVH_HOST, RTG_BVH_GPU = 0, 1, 2
