@@ -244,7 +244,16 @@ typedef struct rtg_render_opts {
                                 = the scene's device.  A device listed twice takes no RCCL
                                 communicator: its shard is copied with hipMemcpyPeer (rehearsal of
                                 the N-shard path on fewer GPUs; results are identical). */
+    /* ABI 7: ray scheduling.  RTG_SCHEDULE_AUTO: the stream schedule where built (the path
+       tracer), else passes.  RTG_SCHEDULE_PASSES: every level of every pass is one launch.
+       RTG_SCHEDULE_STREAM: steps that carry the survivors of any level together with new camera
+       samples (DESIGN.md §4 "Schedules"); max_batch_rays then caps the rays of one step.  Results
+       are bit-identical either way. */
+    int32_t schedule;
 } rtg_render_opts;
+#define RTG_SCHEDULE_AUTO 0
+#define RTG_SCHEDULE_PASSES 1
+#define RTG_SCHEDULE_STREAM 2
 
 /* Automatic pass size (rays per pass) of a render: at most 24M rays, lowered so that the level
    buffers of `lanes` passes in flight fit half of `device_bytes` (0 = no memory limit), at 2 x

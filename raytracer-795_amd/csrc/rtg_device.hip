@@ -1557,12 +1557,14 @@ DEV void store_ray(const RayQ& q, int k, f3 o, f3 d, float time) {
     if (q.t) q.t[k] = time;
 }
 
-// GEN: level-0 launch (either integrator), the ray is primary_ray(slot i) (no ray queue).
+// GEN: the launch may generate primary rays: rays [0, nq) are queued, ray i >= nq is
+// primary_ray(slot gbase + i - nq) (level 0 of a pass: nq = 0, gbase = 0; a regenerating step of
+// the path tracer's stream schedule: the survivors of the previous step, then new camera samples).
 template <bool EXHAUSTIVE, bool STATS, bool GEN = false, bool TLAS = false>
 __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const SceneView sv, const RayQ rays,
                                                        HitRec* __restrict__ hits, int n, Counters* ctr,
                                                        const CameraDev cam, const PassDev ps, uint64_t seed,
-                                                       bool compact) {
+                                                       bool compact, int nq, int gbase) {
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1570,8 +1572,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
     if (i < n) {
         f3 o, d;
         float time, tmax;
-        if (GEN) {
-            primary_ray(cam, ps, seed, i, o, d, time);
+        if (GEN && i >= nq) {
+            primary_ray(cam, ps, seed, gbase + (i - nq), o, d, time);
             tmax = FLT_MAX;
         } else {
             load_ray(rays, i, o, d, time);
@@ -1919,15 +1921,21 @@ DEV DielSplit dielectric_split(const SceneView& sv, f3 d, const Ret& ret, const 
 
 constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour to the sample
 
-// GEN: level 0 (primary rays regenerated), else queued rays (separate instantiations, as k_shade)
+// GEN: the launch may hold generated primary rays (level 0) at i >= nq, slot gbase + i - nq (a
+// pass's level 0: nq = 0; a stream step: survivors then new samples), else queued rays only
+// (separate instantiations, as k_shade).  A queued ray's level is lv_in[i] when the schedule
+// mixes levels in one launch (stream steps), else `level_in`; lv_out (when set) receives the
+// continuation's level.
 template <bool FULL, bool SPOT, bool BRDF, bool GEN = false>
-__global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+__global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level_in, const PassDev ps,
                                                   uint64_t seed, const RayQ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
                                                   PathRec* __restrict__ paths, const NodePlanes nodes,
                                                   const ShadowPlanes shadows, int* __restrict__ slist,
                                                   const RayQ next_rays, RayMeta* __restrict__ next_meta,
-                                                  PathRec* __restrict__ next_paths, unsigned long long* qcount, int n) {
+                                                  PathRec* __restrict__ next_paths, unsigned long long* qcount, int n,
+                                                  int nq, int gbase, const unsigned char* __restrict__ lv_in,
+                                                  unsigned char* __restrict__ lv_out) {
     constexpr int BLOCK = kPtBlock;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool has = false;
@@ -1937,16 +1945,21 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
     NodeRec nd;
     f3 Tg = mk(0, 0, 0);            // the vertex's Beer-attenuated throughput (k_pt_gather)
     unsigned long long smask = 0;
+    int level = 0;
     if (i < n) {
         f3 o, d;
         float time;
         RayMeta mt;
-        if (GEN) {                      // level 0 without a ray queue: generate the primary ray and its meta
-            primary_ray(cam, ps, seed, i, o, d, time);
-            mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
+        const bool gen = GEN && i >= nq;
+        if (gen) {                      // level 0 without a ray queue: generate the primary ray and its meta
+            const int slot = gbase + (i - nq);
+            primary_ray(cam, ps, seed, slot, o, d, time);
+            mt.slot = slot; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
         } else {
-            // a path's queued ray carries only its sample slot (4 bytes in the meta buffer): the
-            // path key is level + 1 and the remaining depth max_depth - level at every level
+            // a path's queued ray carries only its sample slot (4 bytes in the meta buffer) and,
+            // in a stream step, its level (1 byte): the path key is level + 1 and the remaining
+            // depth max_depth - level at every level
+            level = lv_in ? (int)lv_in[i] : level_in;
             load_ray(rays, i, o, d, time);
             mt.slot = reinterpret_cast<const int*>(meta)[i];
             mt.path_lo = (unsigned)level + 1u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
@@ -1960,7 +1973,7 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
         const int flags = sv.pt_flags;
         f3 T = mk(1, 1, 1);
         int spec = 1, medium = 0;
-        if (!GEN && level > 0) {
+        if (!gen && level > 0) {
             const PathRec pr = paths[i];
             T = mk(pr.tr, pr.tg, pr.tb);
             spec = pr.flags & 1;
@@ -2096,6 +2109,7 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
             store_ray(next_rays, idx, cr.o, cr.d, cr.time);
             reinterpret_cast<int*>(next_meta)[idx] = cm.slot;
             next_paths[idx] = cp;
+            if (lv_out) lv_out[idx] = (unsigned char)(level + 1);
         }
         nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
         if (smask) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);   // read by k_shadow only
@@ -2112,10 +2126,12 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
 
 // L[slot] += T (x) v of every contributing vertex, one level at a time (stream order keeps
 // the oracle's per-sample summation order).  Level 0 starts the sum: L = (0,0,0) [+ T (x) v].
-// With several lights the in-order light sum of k_light_sum is folded in here.
+// With several lights the in-order light sum of k_light_sum is folded in here.  Vertices
+// i >= nq are level-0 vertices (a pass's level 0: nq = 0; a stream step: its new samples);
+// `rad` is indexed by the vertex's slot (the link plane's w).
 __global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const PathRec* __restrict__ paths,
                                                    const ShadowPlanes shadows, int nL,
-                                                   const NodePlanes level0, int level, int n) {
+                                                   const NodePlanes rad, int nq, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float4 nc = nodes.col[i];
@@ -2128,16 +2144,17 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const
             v = v + (sc.w != 0.0f ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));   // traced and not blocked
         }
     }
-    if (level == 0) {
+    if (i >= nq) {
+        const int4 lk = nodes.link[i];          // (T.xyz, slot)
         f3 L = mk(0, 0, 0);
-        if (c) { const int4 lk = nodes.link[i]; L = L + cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v); }
-        level0.col[i] = make_float4(L.x, L.y, L.z, nc.w);
+        if (c) L = L + cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v);
+        rad.col[lk.w] = make_float4(L.x, L.y, L.z, nc.w);
     } else if (c) {
         const int4 lk = nodes.link[i];          // (T.xyz, slot)
         const int slot = lk.w;
-        const float4 z = level0.col[slot];
+        const float4 z = rad.col[slot];
         const f3 L = mk(z.x, z.y, z.z) + cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v);
-        level0.col[slot] = make_float4(L.x, L.y, L.z, z.w);
+        rad.col[slot] = make_float4(L.x, L.y, L.z, z.w);
     }
 }
 
@@ -2519,7 +2536,8 @@ __global__ void __launch_bounds__(256) k_hit_details(const SceneView sv, const R
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 
 void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive, Counters* ctr,
-                  hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed, bool compact) {
+                  hipStream_t st, const CameraDev* gen_cam, const PassDev* gen_ps, uint64_t seed, bool compact,
+                  int nq, int gbase) {
     if (n <= 0) return;
     dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);
     const CameraDev cam = gen_cam ? *gen_cam : CameraDev{};
@@ -2527,16 +2545,16 @@ void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int
     const bool tl = sv.tlas_root >= 0;
 #define RTG_TRACE(EX, STA, GEN)                                                                                   \
     do {                                                                                                          \
-        if (tl) hipLaunchKernelGGL((k_trace<EX, STA, GEN, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact); \
-        else hipLaunchKernelGGL((k_trace<EX, STA, GEN, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact); \
+        if (tl) hipLaunchKernelGGL((k_trace<EX, STA, GEN, true>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact, nq, gbase); \
+        else hipLaunchKernelGGL((k_trace<EX, STA, GEN, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact, nq, gbase); \
     } while (0)
     if (gen_cam) {   // primary rays generated in the kernel (rays unused)
-        if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, true, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+        if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, true, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact, nq, gbase);
         else if (ctr) RTG_TRACE(false, true, true);
         else RTG_TRACE(false, false, true);
         return;
     }
-    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, false, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact);
+    if (exhaustive) hipLaunchKernelGGL((k_trace<true, false, false, false>), g, b, 0, st, sv, rays, hits, n, ctr, cam, ps, seed, compact, nq, gbase);
     else if (ctr) RTG_TRACE(false, true, false);
     else RTG_TRACE(false, false, false);
 #undef RTG_TRACE
@@ -2584,16 +2602,18 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
-                     unsigned long long* qcount, int n, hipStream_t st) {
+                     unsigned long long* qcount, int n, hipStream_t st, bool gen, int nq, int gbase,
+                     const unsigned char* lv_in, unsigned char* lv_out) {
     if (n <= 0) return;
     dim3 g(nblk(n, kPtBlock)), b(kPtBlock);
 #define RTG_PT_LAUNCH1(F, S, B, G)                                                                                \
     hipLaunchKernelGGL((k_pt_shade<F, S, B, G>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, \
                        node_planes(nodes, n), \
-                       shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1)), slist, next_rays, next_meta, next_paths, qcount, n)
+                       shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1)), slist, next_rays, next_meta, next_paths, qcount, n, \
+                       nq, gbase, lv_in, lv_out)
 #define RTG_PT_LAUNCH(F, S, B)                                                                                    \
     do {                                                                                                          \
-        if (rays.a == nullptr) RTG_PT_LAUNCH1(F, S, B, true);                                                     \
+        if (gen) RTG_PT_LAUNCH1(F, S, B, true);                                                                   \
         else RTG_PT_LAUNCH1(F, S, B, false);                                                                      \
     } while (0)
     // textures / area / environment lights need the full variant; BRDFs alone do not
@@ -2604,12 +2624,12 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
 #undef RTG_PT_LAUNCH
 #undef RTG_PT_LAUNCH1
 }
-void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
-                      int n0, int level, int n, hipStream_t st) {
+void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* rad,
+                      long long n_rad, int nq, int n, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, node_planes(const_cast<NodeRec*>(nodes), n), paths,
                        shadow_planes(const_cast<ShadowRec*>(shadows), (long long)n * (nL > 1 ? nL : 1)), nL,
-                       node_planes(level0, n0), level, n);
+                       node_planes(rad, n_rad), nq, n);
 }
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
                     const int* rlist, const unsigned* rcount, hipStream_t st) {

@@ -783,10 +783,11 @@ int upload(DBuf& b, const std::vector<T>& v) {
 
 struct Level {
     DBuf rays, meta, hits, nodes, shadows, slist, paths, rlist;   // rlist: non-final nodes (k_resolve)
+    DBuf lv;                   // stream schedule: the queued rays' levels (1 byte each)
     long long rcap = 0;        // plane stride of `rays` (RayQ) as the previous level wrote them
     void release() {
         rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release();
-        paths.release(); rlist.release();
+        paths.release(); rlist.release(); lv.release();
     }
 };
 
@@ -796,6 +797,7 @@ struct Level {
 struct Lane {
     hipStream_t st = nullptr;
     hipEvent_t ev_count = nullptr;          // recorded after the level count copy
+    hipEvent_t ev_join = nullptr;           // stream schedule: the lane's work of a segment is done
     hipEvent_t ev_t[6] = {};                // trace start, trace end, shade end, shadow start, shadow end,
                                             // path-tracer gather end
     unsigned long long* h_count = nullptr;  // pinned host slot
@@ -808,9 +810,13 @@ struct Lane {
     bool busy = false;
     int pass = -1, level = 0;
     std::vector<int> counts;
+    // stream schedule: the current step's queued (survivor) and total ray counts, and the steps run
+    // since the lane last took new samples
+    int sq = 0, sn = 0, sdrain = 0;
     int create() {
         HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&ev_count, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
         for (hipEvent_t& e : ev_t) HIP_TRY(hipEventCreate(&e));
         HIP_TRY(hipHostMalloc((void**)&h_count, sizeof(unsigned long long), hipHostMallocDefault));
         return RTG_OK;
@@ -821,8 +827,9 @@ struct Lane {
         if (h_count) (void)hipHostFree(h_count);
         for (hipEvent_t e : ev_t) if (e) (void)hipEventDestroy(e);
         if (ev_count) (void)hipEventDestroy(ev_count);
+        if (ev_join) (void)hipEventDestroy(ev_join);
         if (st) (void)hipStreamDestroy(st);
-        h_count = nullptr; ev_count = nullptr; st = nullptr;
+        h_count = nullptr; ev_count = nullptr; ev_join = nullptr; st = nullptr;
         for (hipEvent_t& e : ev_t) e = nullptr;
     }
 };
@@ -848,8 +855,12 @@ struct rtg_scene {
     // render workspace
     std::vector<Lane> lanes;
     DBuf d_acc, d_counters, d_stats;
+    DBuf d_rad;                              // stream schedule: per-sample radiance of a segment
     rtg_render_stats stats{};
     int num_lanes = 8;                       // default passes in flight (env RTG_STREAMS overrides)
+    int stream_lanes = 4;                    // path tracer's stream schedule (env RTG_STREAM_LANES)
+    int stream_pt = 1;                       // 0: path tracer on the pass schedule (env RTG_STREAM_PT)
+    int stream_seg_pix = 0;                  // > 0: pixels per stream segment (env RTG_STREAM_SEG_PIX, tests)
     int bvh_builder = RTG_BVH_AUTO;
     double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
     rtg_build_stats bst{};                   // last scene build: per-phase wall times
@@ -980,7 +991,7 @@ static void scene_free(rtg_scene* s) {
     multi_free(s->multi);
     s->multi = nullptr;
     for (DBuf* b : scene_buffers(s)) b->release();
-    s->d_acc.release(); s->d_counters.release(); s->d_stats.release();
+    s->d_acc.release(); s->d_counters.release(); s->d_stats.release(); s->d_rad.release();
     for (Lane& l : s->lanes) l.destroy();
     s->lanes.clear();
 }
@@ -1628,6 +1639,9 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         if (!s) return fail(RTG_ERR_OOM, "host allocation");
         s->device = device;
         if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
+        if (const char* e = getenv("RTG_STREAM_LANES")) s->stream_lanes = std::max(1, std::min(8, atoi(e)));
+        if (const char* e = getenv("RTG_STREAM_PT")) s->stream_pt = atoi(e) != 0;
+        if (const char* e = getenv("RTG_STREAM_SEG_PIX")) s->stream_seg_pix = std::max(0, atoi(e));
         s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
         s->tlas_mode = opts ? opts->tlas : 0;
         s->blas_mode = opts ? opts->traversal_tree : 0;
@@ -1714,6 +1728,11 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     const int lanes_req = o.streams > 0 ? std::min(o.streams, 8) : s->num_lanes;
     const long long frame_rays = (long long)npix * total;
     int ns_chunk, np_pass;
+    size_t dev_total_b = 0;
+    {
+        size_t free_b = 0;
+        if (hipMemGetInfo(&free_b, &dev_total_b) != hipSuccess) dev_total_b = 0;
+    }
     if (o.max_batch_rays > 0) {
         const long long max_batch = o.max_batch_rays;
         // passes: all samples of a pixel range (chunks of samples only when spp exceeds the batch)
@@ -1833,7 +1852,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             launch_pt_shade(sv, cd, level, ps, o.seed, cur_q,
                             gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                             Lc.paths.as<PathRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
-                            next_q, Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st);
+                            next_q, Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st,
+                            gen, gen ? 0 : n, 0, nullptr, nullptr);
         else
             launch_shade(sv, cd, level, ps, o.seed, cur_q,
                          gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
@@ -1854,7 +1874,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt) {
             launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), Lc.shadows.as<ShadowRec>(), nL,
-                             ln.levels[0].nodes.as<NodeRec>(), ln.counts[0], level, n, ln.st);
+                             ln.levels[0].nodes.as<NodeRec>(), ln.counts[0], level == 0 ? 0 : n, n, ln.st);
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[5], ln.st));
         }
         HIP_TRY(hipGetLastError());
@@ -1927,7 +1947,160 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             std::this_thread::yield();
         }
     };
-    for (int k = 0; k < L; k++)
+    // ------------------------------------------------------------ path tracer: stream schedule
+    // (round 4).  On the pass schedule every level of every pass is its own launch
+    // (C5: ~22 passes x ~31 levels, the deep levels a few thousand rays each, each behind a host
+    // count read-back).  Here each lane runs steps of at most R rays: the survivors of its previous
+    // step -- any level; a continuation carries its slot, level and path record -- followed by new
+    // camera samples from the segment's slot cursor.  One lane runs a sample's vertices in
+    // consecutive steps of one stream, so k_pt_gather still adds them to the sample's radiance in
+    // level order: every sample, and the frame, is bit-identical to the pass schedule (and the
+    // oracle's pt_sample()).  The sample radiance of a segment of pixels lives in one buffer (16 B per
+    // slot, segments sized to an eighth of the device memory), summed per pixel in sample order
+    // (MultiSample, src/Scene.cpp:386-411) once the segment's paths have all ended.
+    if (o.schedule < RTG_SCHEDULE_AUTO || o.schedule > RTG_SCHEDULE_STREAM) return fail(RTG_ERR_INVALID, "schedule");
+    const bool want_stream = o.schedule == RTG_SCHEDULE_STREAM || (o.schedule == RTG_SCHEDULE_AUTO && s->stream_pt);
+    const bool stream_pt = pt && want_stream && npix > 0 && (long long)npix * total < (1LL << 31);
+    if (stream_pt) {
+        const int SL = o.streams > 0 ? std::min(o.streams, 8) : s->stream_lanes;
+        while ((int)s->lanes.size() < SL) {
+            s->lanes.emplace_back();
+            if ((rc = s->lanes.back().create())) { s->lanes.back().destroy(); s->lanes.pop_back(); return rc; }
+        }
+        const long long R = o.max_batch_rays > 0 ? std::max<long long>(64, o.max_batch_rays)
+                                                 : rtg_pass_rays(nL, 1, SL, (uint64_t)dev_total_b);
+        const long long rad_slots = std::max<long long>(total, (long long)(dev_total_b ? dev_total_b / 8 / 16 : 1LL << 28));
+        int seg_np = (int)std::max<long long>(1, std::min<long long>(npix, rad_slots / total));
+        if (s->stream_seg_pix > 0) seg_np = std::min(seg_np, s->stream_seg_pix);
+        if ((rc = s->d_rad.grow((size_t)16 * (size_t)seg_np * total))) return rc;
+        const int nLb = std::max(nL, 1);
+        for (int k = 0; k < SL; k++) {
+            Lane& ln = s->lanes[k];
+            if ((int)ln.levels.size() < 2) ln.levels.resize(2);
+            for (int b = 0; b < 2; b++) {
+                Level& Q = ln.levels[b];
+                if ((rc = Q.rays.grow(kRayBytes * (size_t)R)) || (rc = Q.meta.grow(sizeof(int) * (size_t)R)) ||
+                    (rc = Q.lv.grow((size_t)R)) || (rc = Q.paths.grow(sizeof(PathRec) * (size_t)R)))
+                    return rc;
+                Q.rcap = R;
+            }
+            if ((rc = ln.qcnt.grow(sizeof(unsigned long long) * 128))) return rc;
+            HIP_TRY(hipStreamWaitEvent(ln.st, e0, 0));
+        }
+        PassDev F;
+        F.s0 = 0; F.ns = total;
+        F.row_offset = off; F.row_stride = stride; F.rows_owned = rows_owned; F.row_block = block;
+        F.tile_h = stride > 1 && block < 8 ? (block >= 4 ? 4 : block >= 2 ? 2 : 1) : 8;
+        F.tile_s = tile_s;
+        long long cursor = 0, seg_slots = 0;
+        // one step of lane ln: its m survivors (queued in levels[step & 1]) + g new samples
+        auto enqueue_step = [&](Lane& ln, int m, int g) -> int {
+            const int n = m + g;
+            const int gbase = (int)cursor;
+            cursor += g;
+            if (g > 0) ln.sdrain = 0; else ln.sdrain++;
+            stt.max_level = std::max(stt.max_level, ln.sdrain);
+            stt.primary_rays += (uint64_t)g;
+            ln.sq = m; ln.sn = n;
+            Level& A = ln.levels[ln.level & 1];
+            Level& B = ln.levels[(ln.level + 1) & 1];
+            int rc2;
+            if ((rc2 = A.hits.grow(std::max(sizeof(HitRec), kHitBytes) * (size_t)n)) ||
+                (rc2 = A.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
+                (rc2 = A.shadows.grow(sizeof(ShadowRec) * (size_t)n * nLb)) ||
+                (rc2 = A.slist.grow(sizeof(int) * (size_t)n * nLb)))
+                return rc2;
+            const RayQ cur_q = ray_planes(A.rays.p, R, sv.has_blur);
+            const RayQ next_q = ray_planes(B.rays.p, R, sv.has_blur);
+            unsigned long long* qc = ln.qcnt.as<unsigned long long>() + (ln.level & 1);
+            HIP_TRY(hipMemsetAsync(qc, 0, sizeof(unsigned long long), ln.st));
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
+            launch_trace(sv, cur_q, A.hits.as<HitRec>(), n, exhaustive, sctr, ln.st, g > 0 ? &cd : nullptr, &F, o.seed,
+                         /*compact=*/true, m, gbase);
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
+            launch_pt_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), A.hits.as<HitRec>(), A.paths.as<PathRec>(),
+                            A.nodes.as<NodeRec>(), A.shadows.as<ShadowRec>(), A.slist.as<int>(), next_q,
+                            B.meta.as<RayMeta>(), B.paths.as<PathRec>(), qc, n, ln.st, g > 0, m, gbase,
+                            A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
+            HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
+            HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
+            launch_shadow(sv, A.shadows.as<ShadowRec>(), A.slist.as<int>(), reinterpret_cast<const unsigned*>(qc) + 1,
+                          A.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*whitted=*/false);
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
+            launch_pt_gather(A.nodes.as<NodeRec>(), A.paths.as<PathRec>(), A.shadows.as<ShadowRec>(), nL,
+                             s->d_rad.as<NodeRec>(), seg_slots, m, n, ln.st);
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[5], ln.st));
+            HIP_TRY(hipGetLastError());
+            ln.level++;
+            ln.busy = true;
+            return RTG_OK;
+        };
+        for (int p0 = 0; p0 < npix; p0 += seg_np) {
+            F.p0 = p0;
+            F.npass = std::min(seg_np, npix - p0);
+            seg_slots = (long long)F.npass * total;
+            cursor = 0;
+            for (int k = 0; k < SL; k++) {
+                Lane& ln = s->lanes[k];
+                ln.level = 0; ln.sdrain = 0; ln.busy = false;
+                const int g = (int)std::min<long long>(R, seg_slots - cursor);
+                if (g <= 0) continue;
+                if ((rc = enqueue_step(ln, 0, g))) return rc;
+                waiting.push_back(k);
+            }
+            while (!waiting.empty()) {
+                int pick = 0;
+                if ((rc = next_ready(pick))) return rc;
+                const int k = waiting[pick];
+                waiting.erase(waiting.begin() + pick);
+                Lane& ln = s->lanes[k];
+                HIP_TRY(hipEventSynchronize(ln.ev_count));
+                const unsigned long long q = *ln.h_count;
+                const unsigned next = (unsigned)q;
+                shadow_listed += q >> 32;
+                if (timing) {
+                    float a = 0.0f, b = 0.0f, c = 0.0f, g2 = 0.0f;
+                    HIP_TRY(hipEventElapsedTime(&a, ln.ev_t[0], ln.ev_t[1]));
+                    HIP_TRY(hipEventElapsedTime(&c, ln.ev_t[1], ln.ev_t[2]));
+                    HIP_TRY(hipEventSynchronize(ln.ev_t[5]));
+                    HIP_TRY(hipEventElapsedTime(&b, ln.ev_t[3], ln.ev_t[4]));
+                    HIP_TRY(hipEventElapsedTime(&g2, ln.ev_t[4], ln.ev_t[5]));
+                    stt.trace_ms += a; stt.trace_launches++;
+                    stt.shade_ms += c; stt.shade_launches++;
+                    if (nL > 0) { stt.shadow_ms += b; stt.shadow_launches++; }
+                    stt.resolve_ms += g2; stt.resolve_launches++;    // the gather, in the resolve slot
+                }
+                if ((long long)next > (long long)ln.sn) return fail(RTG_ERR_HIP, "path queue overflow");
+                stt.secondary_rays += next;
+                const int g = (int)std::min<long long>(R - (long long)next, seg_slots - cursor);
+                if ((long long)next + g > 0) {
+                    if ((rc = enqueue_step(ln, (int)next, g))) return rc;
+                    waiting.push_back(k);
+                } else {
+                    ln.busy = false;
+                }
+            }
+            // the segment's paths have ended: sum every pixel's samples in order, on lane 0 once
+            // every lane's last gather is done; the next segment's gathers wait for that sum
+            Lane& l0 = s->lanes[0];
+            for (int k = 1; k < SL; k++) {
+                HIP_TRY(hipEventRecord(s->lanes[k].ev_join, s->lanes[k].st));
+                HIP_TRY(hipStreamWaitEvent(l0.st, s->lanes[k].ev_join, 0));
+            }
+            const int mode = total == 1 ? 2 : 1;
+            if ((rc = timed_launch(l0, [&] {
+                     launch_accumulate(sv, s->d_rad.as<NodeRec>(), nullptr, false, s->d_acc.as<float>(), F, cam->nx, mode,
+                                       l0.st, /*whitted=*/false, (int)seg_slots, 0);
+                 }, stt.accumulate_ms, stt.accumulate_launches)))
+                return rc;
+            HIP_TRY(hipEventRecord(l0.ev_join, l0.st));
+            for (int k = 1; k < SL; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k].st, l0.ev_join, 0));
+            stt.passes++;
+        }
+    }
+    for (int k = 0; k < L && !stream_pt; k++)
         if (!s->lanes[k].passes.empty() && npix > 0) {
             if ((rc = start_pass(s->lanes[k]))) return rc;
             waiting.push_back(k);
@@ -1983,7 +2156,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             waiting.push_back(k);
         }
     }
-    for (int k = 0; k < L; k++) {
+    for (int k = 0; k < (int)s->lanes.size(); k++) {
         HIP_TRY(hipEventRecord(ejoin, s->lanes[k].st));
         HIP_TRY(hipStreamWaitEvent(st, ejoin, 0));
     }

@@ -375,9 +375,10 @@ struct Counters {
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
 struct LevelBuffers;
 // gen_cam / gen_ps non-null: level 0 (either integrator), rays are generated in the kernel
+// nq / gbase (with gen_cam): rays [0, nq) are queued, ray i >= nq is the primary ray of slot gbase + i - nq
 void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
-                  uint64_t seed = 0, bool compact = false);
+                  uint64_t seed = 0, bool compact = false, int nq = 0, int gbase = 0);
 // rlist / rcount: the level's non-final nodes (levels >= 1), appended for k_resolve
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
@@ -387,9 +388,12 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
-                     unsigned long long* qcount, int n, hipStream_t st);
-void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* level0,
-                      int n0, int level, int n, hipStream_t st);
+                     unsigned long long* qcount, int n, hipStream_t st, bool gen, int nq, int gbase,
+                     const unsigned char* lv_in, unsigned char* lv_out);
+// rad: NodePlanes over n_rad sample slots (its colour plane is the samples' radiance); vertices
+// i >= nq start their slot's sum (level 0)
+void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* rad,
+                      long long n_rad, int nq, int n, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
                     const int* rlist, const unsigned* rcount, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)

@@ -107,7 +107,11 @@ class RenderOpts(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("row_offset", C.c_int32), ("row_stride", C.c_int32),
                 ("traversal", C.c_int32), ("max_batch_rays", C.c_int32), ("collect_stats", C.c_int32),
                 ("collect_timing", C.c_int32), ("streams", C.c_int32), ("row_block", C.c_int32),
-                ("compact_rows", C.c_int32), ("num_devices", C.c_int32), ("devices", C.POINTER(C.c_int32))]
+                ("compact_rows", C.c_int32), ("num_devices", C.c_int32), ("devices", C.POINTER(C.c_int32)),
+                ("schedule", C.c_int32)]
+
+
+SCHEDULE_AUTO, SCHEDULE_PASSES, SCHEDULE_STREAM = 0, 1, 2
 
 
 class RenderStats(C.Structure):

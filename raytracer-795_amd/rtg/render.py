@@ -54,8 +54,9 @@ class Renderer:
 
     @staticmethod
     def opts(seed=DEFAULT_SEED, row_offset=0, row_stride=1, traversal=0, max_batch_rays=0, collect_stats=0,
-             collect_timing=0, streams=0, row_block=1, compact_rows=0, num_devices=0, devices=None):
+             collect_timing=0, streams=0, row_block=1, compact_rows=0, num_devices=0, devices=None, schedule=0):
         o = A.RenderOpts()
+        o.schedule = schedule
         o.seed = seed
         o.row_offset, o.row_stride, o.row_block = row_offset, row_stride, row_block
         o.traversal = traversal

@@ -140,3 +140,26 @@ def test_path_trace_full_variant_matches_oracle(gpu, name, make, flags):
     print(f"{name} flags={flags}: Linf={linf:.3g} differing={frac:.2e}")
     assert nanm == 0
     assert linf < TOL
+
+
+@pytest.mark.parametrize("flags", [I | N | R, N | R, I])
+def test_stream_schedule_equals_pass_schedule(gpu, flags, monkeypatch):
+    """The stream schedule (steps mixing the survivors of every level with new camera samples,
+    DESIGN.md §4 "Schedules") renders the pass schedule's frame bit for bit and traces the same
+    rays: small steps (many regenerating steps per lane, levels mixed in every launch), one or
+    three lanes, and segments of a few pixels (the radiance buffer reused)."""
+    sc = scenegen.cornell_pt(37, 23, spp=7, flags=flags)
+    monkeypatch.setenv("RTG_STREAM_SEG_PIX", "97")
+    with rtg.Renderer(sc, device=gpu) as r:
+        ref = r.render(0, schedule=A.SCHEDULE_PASSES)
+        st0 = r.stats()
+        for batch, streams in ((0, 0), (500, 1), (1300, 3), (64, 2)):
+            img = r.render(0, schedule=A.SCHEDULE_STREAM, max_batch_rays=batch, streams=streams)
+            st = r.stats()
+            assert np.array_equal(img.view(np.int32), ref.view(np.int32)), (batch, streams)
+            assert (st["primary_rays"], st["secondary_rays"], st["shadow_rays"]) == \
+                   (st0["primary_rays"], st0["secondary_rays"], st0["shadow_rays"]), (batch, streams)
+    o = pyoracle.Oracle(sc)
+    want, _, _, _ = o.render(0)
+    linf, _, nanm = _cmp(img, want)
+    assert nanm == 0 and linf < TOL
