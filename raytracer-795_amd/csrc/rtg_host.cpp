@@ -464,6 +464,33 @@ int sah_rec_par(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::v
     return me;
 }
 
+// Host worker threads of the scene build: up to 16 (the GPU box's CPU share per GPU), chunks of
+// at least `grain` items.  f(chunk, begin, end) runs once per chunk; chunks are numbered in order,
+// so per-chunk partial results combine deterministically.  Exceptions reach the caller.
+inline int build_threads() {
+    static const int n = [] {
+        int t = (int)std::thread::hardware_concurrency();
+        if (const char* e = getenv("RTG_BUILD_THREADS")) t = atoi(e);
+        return std::max(1, std::min(16, t));
+    }();
+    return n;
+}
+template <class F>
+int parallel_chunks(size_t n, size_t grain, F&& f) {
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)build_threads(), (n + grain - 1) / std::max<size_t>(grain, 1)));
+    if (T <= 1) { if (n) f(0, (size_t)0, n); return 1; }
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(T);
+    for (int c = 1; c < T; c++)
+        th.emplace_back([&, c] {
+            try { f(c, n * c / T, n * (c + 1) / T); } catch (...) { err[c] = std::current_exception(); }
+        });
+    try { f(0, (size_t)0, n / T); } catch (...) { err[0] = std::current_exception(); }
+    for (std::thread& t : th) t.join();
+    for (auto& e : err) if (e) std::rethrow_exception(e);
+    return T;
+}
+
 // Collapse the SAH BVH2 into 4-wide nodes: each node's slots are its children, the interior
 // slot with the largest surface area replaced by its own two children while slots are free.
 // Slot info: < 0 empty, 0 interior (ref = Node4 index), > 0 leaf of `info` triangles at ref
@@ -1090,19 +1117,65 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         const std::vector<int>& pv = op[i].v;
         int np = (int)(pv.size() / 3);
         std::vector<V3> centers(np), bmin(np), bmax(np);
-        for (int k = 0; k < np; k++) {
-            if (o.type == RTG_OBJ_SPHERE) {                            // Shape.cpp:55-67
-                V3 c = verts[o.center - 1];
-                float R = o.radius;
-                centers[k] = c;
-                bmin[k] = v3(c.x - R, c.y - R, c.z - R);
-                bmax[k] = v3(c.x + R, c.y + R, c.z + R);
-            } else {                                                  // Shape.cpp:162-190
-                V3 a = verts[pv[3 * k] - 1], b = verts[pv[3 * k + 1] - 1], c = verts[pv[3 * k + 2] - 1];
-                centers[k] = v3(((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f);
-                bmin[k] = v3(minOf3(a.x, b.x, c.x), minOf3(a.y, b.y, c.y), minOf3(a.z, b.z, c.z));
-                bmax[k] = v3(maxOf3(a.x, b.x, c.x), maxOf3(a.y, b.y, c.y), maxOf3(a.z, b.z, c.z));
+        std::vector<char> fin_chunk(std::max(build_threads(), 1), 1);
+        parallel_chunks((size_t)np, 1 << 14, [&](int ch, size_t k0, size_t k1) {
+            bool fin = true;
+            for (size_t k = k0; k < k1; k++) {
+                if (o.type == RTG_OBJ_SPHERE) {                            // Shape.cpp:55-67
+                    V3 c = verts[o.center - 1];
+                    float R = o.radius;
+                    centers[k] = c;
+                    bmin[k] = v3(c.x - R, c.y - R, c.z - R);
+                    bmax[k] = v3(c.x + R, c.y + R, c.z + R);
+                } else {                                                  // Shape.cpp:162-190
+                    V3 a = verts[pv[3 * k] - 1], b = verts[pv[3 * k + 1] - 1], c = verts[pv[3 * k + 2] - 1];
+                    centers[k] = v3(((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f);
+                    bmin[k] = v3(minOf3(a.x, b.x, c.x), minOf3(a.y, b.y, c.y), minOf3(a.z, b.z, c.z));
+                    bmax[k] = v3(maxOf3(a.x, b.x, c.x), maxOf3(a.y, b.y, c.y), maxOf3(a.z, b.z, c.z));
+                }
+                fin = fin && std::isfinite(centers[k].x) && std::isfinite(centers[k].y) && std::isfinite(centers[k].z) &&
+                      std::isfinite(bmin[k].x) && std::isfinite(bmin[k].y) && std::isfinite(bmin[k].z) &&
+                      std::isfinite(bmax[k].x) && std::isfinite(bmax[k].y) && std::isfinite(bmax[k].z);
             }
+            fin_chunk[ch] = fin;
+        });
+        bool all_finite = true;
+        for (char f : fin_chunk) all_finite = all_finite && f;
+        // traversal tree (SAH, 4-wide; below) of a triangle object with finite primitives: its
+        // binned-SAH recursion runs on its own threads, over the triangles in parse order, while the
+        // reference's median tree is built (on the GPU for large meshes); its leaves are mapped to
+        // reference positions afterwards.  Any tree shape gives the same results (the total order
+        // of candidates and the reachability gates), so it needs no reference order.
+        const bool sah_try = o.type != RTG_OBJ_SPHERE && np >= 2 && all_finite && s->blas_mode != 1;
+        std::vector<SahBox> sah_box;
+        std::vector<V3> sah_ctr;
+        std::vector<int> sah_idx;
+        std::vector<SahNode2> sah_bn;
+        std::thread sah_thread;
+        std::exception_ptr sah_err;
+        struct Joiner {                    // the SAH thread never outlives this iteration
+            std::thread& t;
+            ~Joiner() { if (t.joinable()) t.join(); }
+        } sah_join{sah_thread};
+        if (sah_try) {
+            sah_box.resize(np);
+            sah_ctr.resize(np);
+            sah_idx.resize(np);
+            parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
+                for (size_t f = k0; f < k1; f++) {
+                    for (int z = 0; z < 3; z++) { sah_box[f].lo[z] = comp(bmin[f], z); sah_box[f].hi[z] = comp(bmax[f], z); }
+                    sah_ctr[f] = v3(0.5f * (bmin[f].x + bmax[f].x), 0.5f * (bmin[f].y + bmax[f].y), 0.5f * (bmin[f].z + bmax[f].z));
+                    sah_idx[f] = (int)f;
+                }
+            });
+            sah_bn.reserve(2 * (size_t)np / kSahMaxLeaf + 16);
+            sah_thread = std::thread([&] {
+                try {
+                    sah_rec_par(sah_box, sah_ctr, sah_idx, 0, np, sah_bn, 4);
+                } catch (...) {
+                    sah_err = std::current_exception();
+                }
+            });
         }
         ObjBVH& ob = s->bvh[i];
         ob.perm.resize(np);
@@ -1110,14 +1183,9 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         BuildCtx B{centers.data(), bmin.data(), bmax.data(), &ob.perm, &ob.nodes, {}};
         bs.prep_ms += pc.lap();
         auto tb0 = std::chrono::steady_clock::now();
-        bool use_gpu = s->device >= 0 && o.type != RTG_OBJ_SPHERE &&
-                       (s->bvh_builder == RTG_BVH_GPU || (s->bvh_builder == RTG_BVH_AUTO && np >= 4096));
-        if (use_gpu) {     // non-finite centres / boxes: the GPU build does not model NaN folds
-            for (int k = 0; k < np && use_gpu; k++)
-                use_gpu = std::isfinite(centers[k].x) && std::isfinite(centers[k].y) && std::isfinite(centers[k].z) &&
-                          std::isfinite(bmin[k].x) && std::isfinite(bmin[k].y) && std::isfinite(bmin[k].z) &&
-                          std::isfinite(bmax[k].x) && std::isfinite(bmax[k].y) && std::isfinite(bmax[k].z);
-        }
+        // non-finite centres / boxes: the GPU build does not model NaN folds
+        const bool use_gpu = s->device >= 0 && o.type != RTG_OBJ_SPHERE && all_finite &&
+                             (s->bvh_builder == RTG_BVH_GPU || (s->bvh_builder == RTG_BVH_AUTO && np >= 4096));
         if (use_gpu) {
             GpuBvh gb;
             std::string err;
@@ -1175,9 +1243,15 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             g.radius = o.radius;
             g.center_index = o.center;
         }
-        // primitives in BVH order
-        float pad = 0.0f;
-        for (int k = 0; k < np; k++) {
+        // primitives in BVH order (chunks of positions in parallel; the ε-overhang pad is a max)
+        const size_t pbase = tris.size();
+        tris.resize(pbase + np);
+        primidx.resize(pbase + np);
+        s->orig_prim.resize(pbase + np);
+        std::vector<float> pad_chunk(build_threads(), 0.0f);
+        parallel_chunks((size_t)np, 1 << 14, [&](int ch, size_t k0, size_t k1) {
+          float padc = 0.0f;
+          for (size_t k = k0; k < k1; k++) {
             int f = ob.perm[k];
             TriGeom tg;
             memset(&tg, 0, sizeof tg);
@@ -1204,12 +1278,16 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 pi = make_int4(i1, i2, i3, smooth);
                 double e = (double)(ieps > 0 ? ieps : 0.0f);
                 double ext = e * ((double)vnorm(b - a) + (double)vnorm(c - a));
-                pad = std::max(pad, (float)(ext * 1.02 + 1e-7));
+                padc = std::max(padc, (float)(ext * 1.02 + 1e-7));
             }
-            tris.push_back(tg);
-            primidx.push_back(pi);
-            s->orig_prim.push_back(f);
-        }
+            tris[pbase + k] = tg;
+            primidx[pbase + k] = pi;
+            s->orig_prim[pbase + k] = f;
+          }
+          pad_chunk[ch] = padc;
+        });
+        float pad = 0.0f;
+        for (float x : pad_chunk) pad = std::max(pad, x);
         g.prune_pad = pad;
         // linearise interior nodes (pre-order) into child-box nodes
         const std::vector<HNode>& hn = ob.nodes;
@@ -1219,7 +1297,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         for (size_t k = 0; k < hn.size(); k++)
             if (hn[k].left >= 0 || hn[k].right >= 0) dev_index[k] = node_base + cnt++;
         dnodes.resize(node_base + cnt);
-        for (size_t k = 0; k < hn.size(); k++) {
+        parallel_chunks(hn.size(), 1 << 15, [&](int, size_t k0, size_t k1) {
+          for (size_t k = k0; k < k1; k++) {
             if (dev_index[k] < 0) continue;
             Node nd;
             float box[2][6];
@@ -1245,7 +1324,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             nd.c = make_float4(box[1][2], box[1][3], box[1][4], box[1][5]);
             nd.d = make_int4(ref[0], ref[1], count[0], count[1]);
             dnodes[dev_index[k]] = nd;
-        }
+          }
+        });
         // reference leaf of every position: its first position (tie order) and the box of the
         // interior node above it, which gates it (none under the root: closest_hit tests the root)
         gates.resize(6 * (size_t)(g.prim_base + np), 0.0f);
@@ -1253,7 +1333,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         std::vector<char> gated(np, 0);
         if (ob.root >= 0 && hn[ob.root].left < 0 && hn[ob.root].right < 0)
             for (int k = hn[ob.root].start; k < hn[ob.root].end; k++) leaf_start[k] = g.prim_base + hn[ob.root].start;
-        for (size_t n2 = 0; n2 < hn.size(); n2++) {
+        parallel_chunks(hn.size(), 1 << 15, [&](int, size_t n0, size_t n1) {   // a leaf has one parent
+          for (size_t n2 = n0; n2 < n1; n2++) {
             const int ch[2] = {hn[n2].left, hn[n2].right};
             for (int c : ch) {
                 if (c < 0 || hn[c].left >= 0 || hn[c].right >= 0) continue;
@@ -1266,40 +1347,35 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                     }
                 }
             }
-        }
+          }
+        });
         // traversal tree (SAH, 4-wide) of a triangle object with an interior reference root and
         // finite primitives (its boxes must bound every candidate; NaN / inf objects keep the
         // reference-tree walk)
         g.sah_base = -1;
-        bool sah_ok = o.type != RTG_OBJ_SPHERE && np >= 2 && ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0);
-        for (int k = 0; k < np && sah_ok; k++)
-            sah_ok = std::isfinite(bmin[k].x) && std::isfinite(bmin[k].y) && std::isfinite(bmin[k].z) &&
-                     std::isfinite(bmax[k].x) && std::isfinite(bmax[k].y) && std::isfinite(bmax[k].z);
+        const bool sah_ok = sah_try && ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0);
         bs.records_ms += pc.lap();
-        if (sah_ok && s->blas_mode != 1) {
-            std::vector<SahBox> pb(np);
-            std::vector<V3> pc(np);
-            std::vector<int> idx(np);
-            for (int k = 0; k < np; k++) {            // by reference position
-                const int f = ob.perm[k];
-                for (int z = 0; z < 3; z++) { pb[k].lo[z] = comp(bmin[f], z); pb[k].hi[z] = comp(bmax[f], z); }
-                pc[k] = v3(0.5f * (bmin[f].x + bmax[f].x), 0.5f * (bmin[f].y + bmax[f].y), 0.5f * (bmin[f].z + bmax[f].z));
-                idx[k] = k;
-            }
-            std::vector<SahNode2> bn;
-            bn.reserve(2 * (size_t)np / kSahMaxLeaf + 16);
-            sah_rec_par(pb, pc, idx, 0, np, bn, 4);
+        if (sah_thread.joinable()) sah_thread.join();
+        if (sah_err) std::rethrow_exception(sah_err);
+        if (sah_ok) {
+            const std::vector<SahNode2>& bn = sah_bn;
             if (bn[0].left >= 0) {
+                // SAH leaf order: face index -> reference position (inverse of the median tree's perm)
+                std::vector<int> pos_of(np);
+                for (int k = 0; k < np; k++) pos_of[ob.perm[k]] = k;
                 const int tri_base = (int)stris.size();
-                for (int k = 0; k < np; k++) {
-                    const int r = idx[k];
-                    TriGeom t = tris[g.prim_base + r];
-                    const int pos = g.prim_base + r, gt = gated[r];
-                    memcpy(&t.p2.y, &pos, 4);
-                    memcpy(&t.p2.z, &leaf_start[r], 4);
-                    memcpy(&t.p2.w, &gt, 4);
-                    stris.push_back(t);
-                }
+                stris.resize((size_t)tri_base + np);
+                parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
+                    for (size_t k = k0; k < k1; k++) {
+                        const int r = pos_of[sah_idx[k]];
+                        TriGeom t = tris[g.prim_base + r];
+                        const int pos = g.prim_base + r, gt = gated[r];
+                        memcpy(&t.p2.y, &pos, 4);
+                        memcpy(&t.p2.z, &leaf_start[r], 4);
+                        memcpy(&t.p2.w, &gt, 4);
+                        stris[tri_base + k] = t;
+                    }
+                });
                 const size_t first = snodes.size();
                 g.sah_base = sah_collapse(bn, 0, tri_base, pad, snodes);
                 if (snodes.size() - first == 1 && np <= kFlatMaxPrims) { g.flat_first = tri_base; g.flat_count = np; }
