@@ -200,11 +200,23 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
         if kr:
             out[key] = kr
     # SIMD lane efficiency of the traversal kernels (collect_stats frame): node steps / lane slots
+    # of the BVH walks (simd_eff_walk) and, entry-inclusive, (node steps + top-level entries visited)
+    # / (walk lane slots + 64 x the entries each wave's object loop went through): the reference's
+    # linear object loop (src/Helper.cpp:33-73) costs every lane its entry-start work whether or not
+    # the lane walks that entry.  The lane-adjusted VALU fraction uses the entry-inclusive figure.
     for key, pre in (("k_trace", "trace"), ("k_shadow", "shadow")):
         slots = st_stats.get(f"{pre}_lane_slots", 0)
         if key in out and slots > 0:
-            eff = st_stats[f"{pre}_steps"] / slots
+            walk = st_stats[f"{pre}_steps"] / slots
+            ev, es = st_stats.get(f"{pre}_entry_visits", 0), st_stats.get(f"{pre}_entry_slots", 0)
+            eff = (st_stats[f"{pre}_steps"] + ev) / (slots + es) if es > 0 else walk
+            out[key]["simd_eff_walk"] = round(walk, 4)
             out[key]["simd_eff"] = round(eff, 4)
+            if es > 0:
+                out[key]["entry_lane_activity"] = {
+                    "entries_visited_per_lane_slot": round(ev / es, 4),
+                    "entry_visits": ev, "entry_slots": es,
+                    "node_steps": st_stats[f"{pre}_steps"], "walk_lane_slots": slots}
             if "valu" in out[key]:
                 out[key]["valu"]["lane_adjusted_frac"] = round(out[key]["valu"]["frac"] * eff, 4)
     sq = st_stats.get("shadow_rays", 0)

@@ -294,6 +294,15 @@ typedef struct rtg_render_stats {
     double accumulate_ms;    /* collect_timing: summed device time of the sample accumulation launches */
     int32_t resolve_launches;
     int32_t accumulate_launches;
+    /* ABI 7, collect_stats: top-level entries (objects / instances) visited by the lanes -- the
+       entry-start work of BVHMethods::FindIntersection's object loop (src/Helper.cpp:33-73): ray
+       transform, root test, flat meshes' triangles -- and 64 x the entries each wave's loop went
+       through.  (steps + entry_visits) / (lane_slots + entry_slots) is the SIMD efficiency with the
+       object loop included. */
+    uint64_t trace_entry_visits;
+    uint64_t trace_entry_slots;
+    uint64_t shadow_entry_visits;
+    uint64_t shadow_entry_slots;
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */

@@ -342,7 +342,9 @@ DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d
 }
 
 // steps: node steps of this lane (the wave runs the max over its lanes)
-struct Stats { unsigned nodes, tris, steps; };
+// entries: top-level entries this lane visited (entry-start code: ray transform, root test, ...);
+// considered: entries the lane's loop went through (the wave runs each for all its lanes)
+struct Stats { unsigned nodes, tris, steps, entries, considered; };
 
 // ------------------------------------------------------------------ closest hit
 // BVHMethods::FindIntersection (src/Helper.cpp:18-80) with the per-object nearest
@@ -758,6 +760,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     const bool tin = time >= 0.0f && time <= 1.0f;
     if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {   // wfast is per lane: the others walk on
         for (int i = 0; i < sv.num_tops; i++) {
+            if (STATS) st.considered++;
             if (RTG_ENTRY_BOX && !EXHAUSTIVE && sv.tops[i].wbox && wfast && tin) {
                 const TopObject& T = sv.tops[i];
                 const f3 wi = mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
@@ -769,6 +772,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 const float e = (fabsf(sl) + fabsf(le)) * 3.814697265625e-6f + 1e-30f;   // 2^-18
                 if (sl + e < le - e) continue;
             }
+            if (STATS) st.entries++;
             visit(i);
             if (CERT && certified) break;
         }
@@ -831,6 +835,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 const int ref = take_r ? rref : lref, cnt = take_r ? rcnt : lcnt;
                 for (int k = ref; k < ref + cnt; k++) {
                     const int e = sv.tlas_idx[k];
+                    if (STATS) { st.considered++; st.entries += need ? 1u : 0u; }
                     if (need) visit(e);
                 }
             }
@@ -1568,7 +1573,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Stats st = {0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0};
     if (i < n) {
         f3 o, d;
         float time, tmax;
@@ -1595,19 +1600,23 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
         }
     }
     if (STATS) {
-        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
-        unsigned mx = st.steps;
+        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries;
+        unsigned mx = st.steps, mc = st.considered;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
             ns += __shfl_down(ns, off);
+            ne += __shfl_down(ne, off);
             mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
+            mc = max(mc, (unsigned)__shfl_xor((int)mc, off));
         }
         if ((threadIdx.x & 63) == 0) {
             atomicAdd(&ctr->node_visits, nv);
             atomicAdd(&ctr->tri_tests, nt);
             atomicAdd(&ctr->trace_lane_slots, 64ull * mx);
             atomicAdd(&ctr->trace_steps, ns);
+            atomicAdd(&ctr->trace_entry_visits, ne);
+            atomicAdd(&ctr->trace_entry_slots, 64ull * mc);
         }
     }
 }
@@ -2174,7 +2183,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
-    Stats st = {0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0};
     bool was_blocked = false;
     if (j < (int)*scount) {
         const int idx = slist[j];
@@ -2310,14 +2319,16 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     const unsigned long long nm = __ballot(nanq != 0);
     if (nm && (threadIdx.x & 63) == 0) atomicAdd(nan_queries, (unsigned)__popcll(nm));
     if (STATS) {
-        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps;
+        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries;
         unsigned long long bq = was_blocked ? 1ull : 0ull, bs = was_blocked ? st.steps : 0ull,
                            bt = was_blocked ? st.tris : 0ull;
-        unsigned mx = st.steps;
+        unsigned mx = st.steps, mc = st.considered;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
             ns += __shfl_down(ns, off);
+            ne += __shfl_down(ne, off);
+            mc = max(mc, (unsigned)__shfl_xor((int)mc, off));
             bq += __shfl_down(bq, off);
             bs += __shfl_down(bs, off);
             bt += __shfl_down(bt, off);
@@ -2331,6 +2342,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             atomicAdd(&ctr->shadow_blocked, bq);
             atomicAdd(&ctr->shadow_blocked_steps, bs);
             atomicAdd(&ctr->shadow_blocked_tris, bt);
+            atomicAdd(&ctr->shadow_entry_visits, ne);
+            atomicAdd(&ctr->shadow_entry_slots, 64ull * mc);
         }
     }
 }

@@ -2263,6 +2263,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     stt.shadow_blocked = ctr.shadow_blocked;
     stt.shadow_blocked_steps = ctr.shadow_blocked_steps;
     stt.shadow_blocked_tris = ctr.shadow_blocked_tris;
+    stt.trace_entry_visits = ctr.trace_entry_visits;
+    stt.trace_entry_slots = ctr.trace_entry_slots;
+    stt.shadow_entry_visits = ctr.shadow_entry_visits;
+    stt.shadow_entry_slots = ctr.shadow_entry_slots;
     stt.devices = 1;
     s->stats = stt;
     return RTG_OK;

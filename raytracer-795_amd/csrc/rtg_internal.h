@@ -370,6 +370,8 @@ struct Counters {
     // shadow queries found blocked, and the node steps / triangle tests they took (the rest of
     // shadow_steps / shadow_tri_tests went to unblocked queries)
     unsigned long long shadow_blocked, shadow_blocked_steps, shadow_blocked_tris;
+    // top-level entries visited by the lanes, and 64 x the entries each wave's loop went through
+    unsigned long long trace_entry_visits, trace_entry_slots, shadow_entry_visits, shadow_entry_slots;
 };
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------

@@ -195,6 +195,10 @@ void add_stats(rtg_render_stats& a, const rtg_render_stats& b) {
     a.shadow_blocked += b.shadow_blocked;
     a.shadow_blocked_steps += b.shadow_blocked_steps;
     a.shadow_blocked_tris += b.shadow_blocked_tris;
+    a.trace_entry_visits += b.trace_entry_visits;
+    a.trace_entry_slots += b.trace_entry_slots;
+    a.shadow_entry_visits += b.shadow_entry_visits;
+    a.shadow_entry_slots += b.shadow_entry_slots;
     a.resolve_ms += b.resolve_ms;
     a.accumulate_ms += b.accumulate_ms;
     a.resolve_launches += b.resolve_launches;

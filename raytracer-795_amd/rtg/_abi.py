@@ -125,7 +125,9 @@ class RenderStats(C.Structure):
                 ("shade_ms", C.c_double), ("shade_launches", C.c_int32), ("devices", C.c_int32),
                 ("gather_ms", C.c_double), ("shadow_blocked", C.c_uint64), ("shadow_blocked_steps", C.c_uint64),
                 ("shadow_blocked_tris", C.c_uint64), ("resolve_ms", C.c_double), ("accumulate_ms", C.c_double),
-                ("resolve_launches", C.c_int32), ("accumulate_launches", C.c_int32)]
+                ("resolve_launches", C.c_int32), ("accumulate_launches", C.c_int32),
+                ("trace_entry_visits", C.c_uint64), ("trace_entry_slots", C.c_uint64),
+                ("shadow_entry_visits", C.c_uint64), ("shadow_entry_slots", C.c_uint64)]
 
 RTG_COMM_ID_BYTES = 128
 
