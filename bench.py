@@ -229,6 +229,14 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
             "steps_per_unblocked": round((st_stats["shadow_steps"] - st_stats["shadow_blocked_steps"]) / ub, 3),
             "tris_per_blocked": round(st_stats["shadow_blocked_tris"] / max(b, 1), 3),
             "tris_per_unblocked": round((st_stats["shadow_tri_tests"] - st_stats["shadow_blocked_tris"]) / ub, 3)}
+        if "shadow_hist_before" in st_stats and b > 0:
+            # finding the blocker vs proving it nearest (Light::IsShadow, src/Light.cpp:188-204)
+            out["k_shadow"]["queries"]["blocked_steps_split"] = {
+                "steps_before_blocker_per_blocked": round(st_stats["shadow_blocked_steps_before"] / b, 3),
+                "steps_after_blocker_per_blocked": round(
+                    (st_stats["shadow_blocked_steps"] - st_stats["shadow_blocked_steps_before"]) / b, 3),
+                "bins": ["0", "1", "2", "3-4", "5-8", "9-16", "17-32", ">32"],
+                "hist_before": st_stats["shadow_hist_before"], "hist_after": st_stats["shadow_hist_after"]}
     return out, shade
 
 

@@ -303,6 +303,13 @@ typedef struct rtg_render_stats {
     uint64_t trace_entry_slots;
     uint64_t shadow_entry_visits;
     uint64_t shadow_entry_slots;
+    /* ABI 7, collect_stats: blocked shadow queries (Light::IsShadow needs the nearest blocker,
+       src/Light.cpp:188-204): histograms of the node steps taken before the eventual blocker was
+       accepted (finding it) and after (proving it nearest), bins 0, 1, 2, 3-4, 5-8, 9-16, 17-32,
+       > 32; and the steps before, summed */
+    uint64_t shadow_hist_before[8];
+    uint64_t shadow_hist_after[8];
+    uint64_t shadow_blocked_steps_before;
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */

@@ -344,7 +344,9 @@ DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d
 // steps: node steps of this lane (the wave runs the max over its lanes)
 // entries: top-level entries this lane visited (entry-start code: ray transform, root test, ...);
 // considered: entries the lane's loop went through (the wave runs each for all its lanes)
-struct Stats { unsigned nodes, tris, steps, entries, considered; };
+// cand_step: node steps taken when the current object's best candidate was accepted; win_step: the
+// same for the query's final winner (the steps after it only prove that it is the nearest)
+struct Stats { unsigned nodes, tris, steps, entries, considered, cand_step, win_step; };
 
 // ------------------------------------------------------------------ closest hit
 // BVHMethods::FindIntersection (src/Helper.cpp:18-80) with the per-object nearest
@@ -404,7 +406,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             f3 ip;
             if (sphere_test(o2, d2, ld3(g.center), g.radius, eps, ip)) {
                 float dist = norm(ip - o2);
-                if (dist < FLT_MAX) { found = true; bprim = g.prim_base; bp = ip; }
+                if (dist < FLT_MAX) { found = true; bprim = g.prim_base; bp = ip; if (STATS) st.cand_step = st.steps; }
             }
         }
     } else {
@@ -462,6 +464,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                 if (dist < FLT_MAX &&
                     (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
                     best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
+                    if (STATS) st.cand_step = st.steps;
                     if (bary) { bt = c.t; bb = c.beta; bg = c.gamma; }
                     if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                 }
@@ -581,6 +584,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                         if (!box_hit(o2, d2, inv, fast, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) return;
                     }
                     best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
+                    if (STATS) st.cand_step = st.steps;
                     if (bary) { bt = c.t; bb = c.beta; bg = c.gamma; }
                     if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                     if (WCERT) {
@@ -726,6 +730,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         if (t > 0 && (t < nearest || (t == nearest && i < out.obj))) {   // src/Helper.cpp:43, 64
             nearest = t;
             out.obj = i; out.prim = bprim; out.t = t;
+            if (STATS) st.win_step = st.cand_step;
             if (bary) { bary->pt = bt; bary->beta = bb; bary->gamma = bg; }
         }
         // the object's winner is this candidate (a complete walk, a sphere) or, after the walk's
@@ -1573,7 +1578,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Stats st = {0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, 0};
     if (i < n) {
         f3 o, d;
         float time, tmax;
@@ -2183,7 +2188,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
-    Stats st = {0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, 0};
     bool was_blocked = false;
     if (j < (int)*scount) {
         const int idx = slist[j];
@@ -2319,6 +2324,13 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     const unsigned long long nm = __ballot(nanq != 0);
     if (nm && (threadIdx.x & 63) == 0) atomicAdd(nan_queries, (unsigned)__popcll(nm));
     if (STATS) {
+        if (was_blocked) {        // node steps until the blocker was accepted / after it (proof of nearest)
+            const unsigned before = st.win_step, after = st.steps - st.win_step;
+            auto bin = [](unsigned x) { return x == 0 ? 0 : x == 1 ? 1 : x == 2 ? 2 : x <= 4 ? 3 : x <= 8 ? 4 : x <= 16 ? 5 : x <= 32 ? 6 : 7; };
+            atomicAdd(&ctr->shadow_hist_before[bin(before)], 1ull);
+            atomicAdd(&ctr->shadow_hist_after[bin(after)], 1ull);
+            atomicAdd(&ctr->shadow_blocked_steps_before, (unsigned long long)before);
+        }
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries;
         unsigned long long bq = was_blocked ? 1ull : 0ull, bs = was_blocked ? st.steps : 0ull,
                            bt = was_blocked ? st.tris : 0ull;

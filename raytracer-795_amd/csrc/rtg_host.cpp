@@ -2267,6 +2267,11 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     stt.trace_entry_slots = ctr.trace_entry_slots;
     stt.shadow_entry_visits = ctr.shadow_entry_visits;
     stt.shadow_entry_slots = ctr.shadow_entry_slots;
+    for (int b = 0; b < 8; b++) {
+        stt.shadow_hist_before[b] = ctr.shadow_hist_before[b];
+        stt.shadow_hist_after[b] = ctr.shadow_hist_after[b];
+    }
+    stt.shadow_blocked_steps_before = ctr.shadow_blocked_steps_before;
     stt.devices = 1;
     s->stats = stt;
     return RTG_OK;

@@ -372,6 +372,9 @@ struct Counters {
     unsigned long long shadow_blocked, shadow_blocked_steps, shadow_blocked_tris;
     // top-level entries visited by the lanes, and 64 x the entries each wave's loop went through
     unsigned long long trace_entry_visits, trace_entry_slots, shadow_entry_visits, shadow_entry_slots;
+    // blocked shadow queries: histograms (bins 0, 1, 2, 3-4, 5-8, 9-16, 17-32, >32) of the node steps
+    // taken before the blocker was accepted and after it, and the summed steps before
+    unsigned long long shadow_hist_before[8], shadow_hist_after[8], shadow_blocked_steps_before;
 };
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------

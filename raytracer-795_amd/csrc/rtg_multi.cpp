@@ -199,6 +199,11 @@ void add_stats(rtg_render_stats& a, const rtg_render_stats& b) {
     a.trace_entry_slots += b.trace_entry_slots;
     a.shadow_entry_visits += b.shadow_entry_visits;
     a.shadow_entry_slots += b.shadow_entry_slots;
+    for (int k = 0; k < 8; k++) {
+        a.shadow_hist_before[k] += b.shadow_hist_before[k];
+        a.shadow_hist_after[k] += b.shadow_hist_after[k];
+    }
+    a.shadow_blocked_steps_before += b.shadow_blocked_steps_before;
     a.resolve_ms += b.resolve_ms;
     a.accumulate_ms += b.accumulate_ms;
     a.resolve_launches += b.resolve_launches;

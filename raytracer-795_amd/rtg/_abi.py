@@ -127,7 +127,9 @@ class RenderStats(C.Structure):
                 ("shadow_blocked_tris", C.c_uint64), ("resolve_ms", C.c_double), ("accumulate_ms", C.c_double),
                 ("resolve_launches", C.c_int32), ("accumulate_launches", C.c_int32),
                 ("trace_entry_visits", C.c_uint64), ("trace_entry_slots", C.c_uint64),
-                ("shadow_entry_visits", C.c_uint64), ("shadow_entry_slots", C.c_uint64)]
+                ("shadow_entry_visits", C.c_uint64), ("shadow_entry_slots", C.c_uint64),
+                ("shadow_hist_before", C.c_uint64 * 8), ("shadow_hist_after", C.c_uint64 * 8),
+                ("shadow_blocked_steps_before", C.c_uint64)]
 
 RTG_COMM_ID_BYTES = 128
 

@@ -102,7 +102,8 @@ class Renderer:
     def stats(self) -> dict:
         s = A.RenderStats()
         A.check(self.lib.rtg_last_render_stats(self.handle, C.byref(s)), self.lib)
-        return {k: getattr(s, k) for k, _ in A.RenderStats._fields_}
+        return {k: (list(v) if isinstance(v, C.Array) else v)
+                for k, v in ((k, getattr(s, k)) for k, _ in A.RenderStats._fields_)}
 
     def trace(self, origins: np.ndarray, directions: np.ndarray, times=None, traversal=0) -> dict:
         n = len(origins)
