@@ -1663,7 +1663,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                    int n, const HitIn& hin, const f3 o, const f3 d, const float time, const RayMeta& mt,
                    const NodePlanes& nodes, const ShadowPlanes& shadows, int* __restrict__ slist,
                    const RayQ& next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount,
-                   int* __restrict__ rlist, unsigned* rcount) {
+                   int* __restrict__ rlist, unsigned* rcount, unsigned char* __restrict__ lv_out) {
     const HitRec& h = hin.h;
     int nchild = 0;
     QRay c0r, c1r;
@@ -1829,6 +1829,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
         auto put_ray = [&](int k, const QRay& rr, const RayMeta& mm) {
             store_ray(next_rays, k, rr.o, rr.d, rr.time);
             if (!sv.meta_free) next_meta[k] = mm;
+            if (lv_out) lv_out[k] = (unsigned char)(level + 1);
         };
         if (has0) { put_ray(idx, c0r, c0m); nd.child0 = idx; idx++; }
         if (has1) { put_ray(idx, c1r, c1m); nd.child1 = idx; }
@@ -1860,6 +1861,7 @@ DEV RayMeta level_meta(const SceneView& sv, int level, const RayQ& rays, const R
     if (rays.a == nullptr) {          // level 0: the primary ray's meta
         mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
     } else if (sv.meta_free && level > 0) {   // nothing below level 0 draws random numbers
+        // (depth from the level: the launch's, or the ray's own in a stream step)
         mt.slot = 0; mt.path_lo = 0u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
     } else {
         mt = meta[i];
@@ -1867,17 +1869,21 @@ DEV RayMeta level_meta(const SceneView& sv, int level, const RayQ& rays, const R
     return mt;
 }
 
-// GEN: level 0 (the primary ray of slot i, regenerated), else a queued ray -- separate
-// instantiations, so neither carries the other's live ranges.
+// GEN: the launch holds generated primary rays at i >= nq (slot gbase + i - nq; a pass's level 0:
+// nq = 0), else queued rays only -- separate instantiations, so a queued-only launch carries no
+// ray-generation live ranges.  A queued ray's level is lv_in[i] in a stream step (levels mixed in
+// one launch), else `level_in`; lv_out (when set) receives the children's levels.
 template <bool FULL, bool SPOT, int BLOCK = FULL ? 256 : kShadeBlock, bool TEX = FULL, bool GEN = false>
-__global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level, const PassDev ps,
+__global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView sv, const CameraDev cam, int level_in, const PassDev ps,
                                                uint64_t seed,
                                                const RayQ rays, const RayMeta* __restrict__ meta,
                                                const HitRec* __restrict__ hits, const NodePlanes nodes,
                                                const ShadowPlanes shadows, int* __restrict__ slist,
                                                const RayQ next_rays, RayMeta* __restrict__ next_meta,
                                                unsigned long long* qcount, int* __restrict__ rlist,
-                                               unsigned* rcount, int n) {
+                                               unsigned* rcount, int n, int nq, int gbase,
+                                               const unsigned char* __restrict__ lv_in,
+                                               unsigned char* __restrict__ lv_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     HitIn h;
     h.h.obj = -1; h.h.prim = -1; h.h.t = 0.0f; h.h.pad = 0;
@@ -1885,18 +1891,22 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
     f3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     float time = 0.0f;
     RayMeta mt = {};
+    int level = level_in;
     if (i < n) {
         h = load_hit_planes(sv, hits, n, i);
-        if (GEN) {
-            primary_ray(cam, ps, seed, i, o, d, time);
-            mt.slot = i; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
+        if (GEN && i >= nq) {
+            const int slot = gbase + (i - nq);
+            primary_ray(cam, ps, seed, slot, o, d, time);
+            mt.slot = slot; mt.path_lo = 1u; mt.path_hi = 0u; mt.depth = sv.max_depth;
+            level = 0;
         } else {
+            if (lv_in) level = lv_in[i];
             load_ray(rays, i, o, d, time);
             mt = level_meta(sv, level, rays, meta, i);
         }
     }
     shade_ray<FULL, SPOT, BLOCK, TEX>(sv, cam, level, ps, seed, i, n, h, o, d, time, mt, nodes, shadows, slist,
-                                      next_rays, next_meta, qcount, rlist, rcount);
+                                      next_rays, next_meta, qcount, rlist, rcount, lv_out);
 }
 
 // ------------------------------------------------------------------ hw7 path tracer
@@ -2587,19 +2597,21 @@ void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
-                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st) {
+                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st,
+                  int gen, int nq, int gbase, const unsigned char* lv_in, unsigned char* lv_out) {
     if (n <= 0) return;
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
     const NodePlanes np = node_planes(nodes, n);
     const ShadowPlanes sp = shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1));
+    const bool G = gen < 0 ? rays.a == nullptr : gen != 0;   // gen < 0: a pass's level (level 0 has no queue)
 #define RTG_SHADE(F, S, B, T, gr, bl)                                                                             \
     do {                                                                                                          \
-        if (rays.a == nullptr)                                                                                    \
+        if (G)                                                                                                    \
             hipLaunchKernelGGL((k_shade<F, S, B, T, true>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
-                               slist, next_rays, next_meta, qcount, rlist, rcount, n);                            \
+                               slist, next_rays, next_meta, qcount, rlist, rcount, n, nq, gbase, lv_in, lv_out); \
         else                                                                                                      \
             hipLaunchKernelGGL((k_shade<F, S, B, T, false>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
-                               slist, next_rays, next_meta, qcount, rlist, rcount, n);                            \
+                               slist, next_rays, next_meta, qcount, rlist, rcount, n, nq, gbase, lv_in, lv_out); \
     } while (0)
     if (sv.full && sv.tex) RTG_SHADE(true, true, 256, true, dim3(nblk(n, 256)), dim3(256));
     else if (sv.full) RTG_SHADE(true, true, 256, false, dim3(nblk(n, 256)), dim3(256));
@@ -2661,6 +2673,18 @@ void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_no
     if (n <= 0) return;
     hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, node_planes(nodes, n),
                        node_planes(const_cast<NodeRec*>(child_nodes), n_child), rlist, rcount, n);
+}
+void launch_resolve_planes(const SceneView& sv, const NodePlanes& self, const NodePlanes& child, int count,
+                           hipStream_t st) {
+    if (count <= 0) return;
+    hipLaunchKernelGGL(k_resolve, dim3(nblk(count, 256)), dim3(256), 0, st, sv, self, child, (const int*)nullptr,
+                       (const unsigned*)nullptr, count);
+}
+void launch_accumulate_planes(const SceneView& sv, const NodePlanes& level0, const NodePlanes& level1, bool resolve,
+                              float* acc, const PassDev& ps, int nx, int mode, hipStream_t st) {
+    if (ps.npass <= 0) return;
+    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, level0, level1, resolve, acc,
+                       ps, nx, mode);
 }
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
                        const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1) {

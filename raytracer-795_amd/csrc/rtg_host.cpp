@@ -840,6 +840,8 @@ struct Lane {
     // stream schedule: the current step's queued (survivor) and total ray counts, and the steps run
     // since the lane last took new samples
     int sq = 0, sn = 0, sdrain = 0;
+    std::vector<DBuf> snodes;                // reference integrator: node records of each step of a segment
+    std::vector<int> step_m, step_g, step_gb;   // ... and each step's survivors, new samples, first new slot
     int create() {
         HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&ev_count, hipEventDisableTiming));
@@ -850,6 +852,8 @@ struct Lane {
     }
     void destroy() {
         for (Level& l : levels) l.release();
+        for (DBuf& b : snodes) b.release();
+        snodes.clear();
         qcnt.release();
         if (h_count) (void)hipHostFree(h_count);
         for (hipEvent_t e : ev_t) if (e) (void)hipEventDestroy(e);
@@ -888,6 +892,9 @@ struct rtg_scene {
     int stream_lanes = 4;                    // path tracer's stream schedule (env RTG_STREAM_LANES)
     int stream_pt = 1;                       // 0: path tracer on the pass schedule (env RTG_STREAM_PT)
     int stream_seg_pix = 0;                  // > 0: pixels per stream segment (env RTG_STREAM_SEG_PIX, tests)
+    int stream_whitted = 1;                  // 0: reference integrator on the pass schedule (env RTG_STREAM_WHITTED)
+    int stream_div = 3;                      // about this many new-sample steps per lane (env RTG_STREAM_DIV)
+    long long stream_node_budget = 0;        // > 0: node-record bytes per segment (env RTG_STREAM_NODE_BUDGET, tests)
     int bvh_builder = RTG_BVH_AUTO;
     double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
     rtg_build_stats bst{};                   // last scene build: per-phase wall times
@@ -1718,6 +1725,9 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         if (const char* e = getenv("RTG_STREAM_LANES")) s->stream_lanes = std::max(1, std::min(8, atoi(e)));
         if (const char* e = getenv("RTG_STREAM_PT")) s->stream_pt = atoi(e) != 0;
         if (const char* e = getenv("RTG_STREAM_SEG_PIX")) s->stream_seg_pix = std::max(0, atoi(e));
+        if (const char* e = getenv("RTG_STREAM_WHITTED")) s->stream_whitted = atoi(e) != 0;
+        if (const char* e = getenv("RTG_STREAM_DIV")) s->stream_div = std::max(1, atoi(e));
+        if (const char* e = getenv("RTG_STREAM_NODE_BUDGET")) s->stream_node_budget = std::max(0LL, atoll(e));
         s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
         s->tlas_mode = opts ? opts->tlas : 0;
         s->blas_mode = opts ? opts->traversal_tree : 0;
@@ -2023,53 +2033,74 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             std::this_thread::yield();
         }
     };
-    // ------------------------------------------------------------ path tracer: stream schedule
+    // ------------------------------------------------------------ stream schedule
     // (round 4).  On the pass schedule every level of every pass is its own launch
     // (C5: ~22 passes x ~31 levels, the deep levels a few thousand rays each, each behind a host
-    // count read-back).  Here each lane runs steps of at most R rays: the survivors of its previous
-    // step -- any level; a continuation carries its slot, level and path record -- followed by new
-    // camera samples from the segment's slot cursor.  One lane runs a sample's vertices in
-    // consecutive steps of one stream, so k_pt_gather still adds them to the sample's radiance in
-    // level order: every sample, and the frame, is bit-identical to the pass schedule (and the
-    // oracle's pt_sample()).  The sample radiance of a segment of pixels lives in one buffer (16 B per
-    // slot, segments sized to an eighth of the device memory), summed per pixel in sample order
-    // (MultiSample, src/Scene.cpp:386-411) once the segment's paths have all ended.
+    // count read-back; an N=8 dragon shard: the passes holding the glass sphere run their seven
+    // levels alone at the end).  Here each lane runs steps of at most R rays: the survivors of its
+    // previous step -- children of any level, each carrying its slot and level (the path tracer: its
+    // path record too) -- followed by new camera samples from the frame's slot cursor.  A lane runs
+    // a sample's ray tree in consecutive steps of one stream, so every per-sample sum keeps its
+    // order and the frame is bit-identical to the pass schedule (and to the oracle):
+    //  * path tracer: k_pt_gather adds each vertex to the sample's radiance in level order; the
+    //    radiance of a segment of pixels lives in one buffer (16 B per slot, segments sized to an
+    //    eighth of the device memory) and is summed per pixel in sample order (MultiSample,
+    //    src/Scene.cpp:386-411) once the segment's paths have ended;
+    //  * reference integrator: a step's node records [survivors | new samples] stay in HBM; a node's
+    //    children are survivors of the lane's next step (their queue index is their node index
+    //    there).  When a segment's trees have all ended, each lane evaluates RecursiveShading
+    //    bottom-up (src/Scene.cpp:148-219), last step first, and sums the new samples of each step
+    //    per pixel (their level-0 nodes resolved inside the sum).  New samples come in whole pixels;
+    //    a segment closes (no new samples until its trees end) when its node records reach a quarter
+    //    of the device memory.
     if (o.schedule < RTG_SCHEDULE_AUTO || o.schedule > RTG_SCHEDULE_STREAM) return fail(RTG_ERR_INVALID, "schedule");
-    const bool want_stream = o.schedule == RTG_SCHEDULE_STREAM || (o.schedule == RTG_SCHEDULE_AUTO && s->stream_pt);
-    const bool stream_pt = pt && want_stream && npix > 0 && (long long)npix * total < (1LL << 31);
-    if (stream_pt) {
+    const bool want_stream = o.schedule == RTG_SCHEDULE_STREAM ||
+                             (o.schedule == RTG_SCHEDULE_AUTO && (pt ? s->stream_pt : s->stream_whitted));
+    const bool stream = want_stream && npix > 0 && (long long)npix * total < (1LL << 31) &&
+                        (pt || (s->stream_whitted && !RTG_RESOLVE_LIST));
+    if (stream) {
         const int SL = o.streams > 0 ? std::min(o.streams, 8) : s->stream_lanes;
         while ((int)s->lanes.size() < SL) {
             s->lanes.emplace_back();
             if ((rc = s->lanes.back().create())) { s->lanes.back().destroy(); s->lanes.pop_back(); return rc; }
         }
+        // rays per step: an even share of the frame, about s->stream_div new-sample steps per lane,
+        // within the memory cap of a pass
+        const long long kR = rtg_pass_rays(nL, pt ? 1 : 0, SL, (uint64_t)dev_total_b);
+        const long long share = (frame_rays + (long long)SL * s->stream_div - 1) / ((long long)SL * s->stream_div);
         const long long R = o.max_batch_rays > 0 ? std::max<long long>(64, o.max_batch_rays)
-                                                 : rtg_pass_rays(nL, 1, SL, (uint64_t)dev_total_b);
+                                                 : std::max<long long>(std::min<long long>(kR, 1LL << 16),
+                                                                       std::min(kR, share));
         const long long rad_slots = std::max<long long>(total, (long long)(dev_total_b ? dev_total_b / 8 / 16 : 1LL << 28));
-        int seg_np = (int)std::max<long long>(1, std::min<long long>(npix, rad_slots / total));
-        if (s->stream_seg_pix > 0) seg_np = std::min(seg_np, s->stream_seg_pix);
-        if ((rc = s->d_rad.grow((size_t)16 * (size_t)seg_np * total))) return rc;
+        int seg_np = pt ? (int)std::max<long long>(1, std::min<long long>(npix, rad_slots / total)) : npix;
+        if (pt && s->stream_seg_pix > 0) seg_np = std::min(seg_np, s->stream_seg_pix);
+        if (pt && (rc = s->d_rad.grow((size_t)16 * (size_t)seg_np * total))) return rc;
+        const double node_budget = s->stream_node_budget > 0 ? (double)s->stream_node_budget
+                                                             : (dev_total_b ? 0.25 * (double)dev_total_b : 16e9);
         const int nLb = std::max(nL, 1);
         for (int k = 0; k < SL; k++) {
             Lane& ln = s->lanes[k];
-            if ((int)ln.levels.size() < 2) ln.levels.resize(2);
-            for (int b = 0; b < 2; b++) {
-                Level& Q = ln.levels[b];
-                if ((rc = Q.rays.grow(kRayBytes * (size_t)R)) || (rc = Q.meta.grow(sizeof(int) * (size_t)R)) ||
-                    (rc = Q.lv.grow((size_t)R)) || (rc = Q.paths.grow(sizeof(PathRec) * (size_t)R)))
-                    return rc;
-                Q.rcap = R;
-            }
+            if ((int)ln.levels.size() < 3) ln.levels.resize(3);
+            if (pt)
+                for (int b2 = 0; b2 < 2; b2++) {
+                    Level& Q = ln.levels[b2];
+                    if ((rc = Q.rays.grow(kRayBytes * (size_t)R)) || (rc = Q.meta.grow(sizeof(int) * (size_t)R)) ||
+                        (rc = Q.lv.grow((size_t)R)) || (rc = Q.paths.grow(sizeof(PathRec) * (size_t)R)))
+                        return rc;
+                    Q.rcap = R;
+                }
             if ((rc = ln.qcnt.grow(sizeof(unsigned long long) * 128))) return rc;
             HIP_TRY(hipStreamWaitEvent(ln.st, e0, 0));
         }
         PassDev F;
-        F.s0 = 0; F.ns = total;
+        F.s0 = 0; F.ns = total; F.p0 = 0; F.npass = npix;
         F.row_offset = off; F.row_stride = stride; F.rows_owned = rows_owned; F.row_block = block;
         F.tile_h = stride > 1 && block < 8 ? (block >= 4 ? 4 : block >= 2 ? 2 : 1) : 8;
         F.tile_s = tile_s;
-        long long cursor = 0, seg_slots = 0;
-        // one step of lane ln: its m survivors (queued in levels[step & 1]) + g new samples
+        long long cursor = 0, seg_end = 0, seg_slots = 0;
+        double seg_node_bytes = 0.0;
+        bool seg_closed = false;
+        // one step of lane ln: its m survivors (queued by its previous step) + g new samples
         auto enqueue_step = [&](Lane& ln, int m, int g) -> int {
             const int n = m + g;
             const int gbase = (int)cursor;
@@ -2078,50 +2109,99 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             stt.max_level = std::max(stt.max_level, ln.sdrain);
             stt.primary_rays += (uint64_t)g;
             ln.sq = m; ln.sn = n;
-            Level& A = ln.levels[ln.level & 1];
-            Level& B = ln.levels[(ln.level + 1) & 1];
+            const int step = ln.level;
+            Level& A = ln.levels[step & 1];          // this step's queue (survivors)
+            Level& B = ln.levels[(step + 1) & 1];    // the next step's
+            Level& W = pt ? A : ln.levels[2];        // hits / shadow records / lists of the step
             int rc2;
-            if ((rc2 = A.hits.grow(std::max(sizeof(HitRec), kHitBytes) * (size_t)n)) ||
-                (rc2 = A.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
-                (rc2 = A.shadows.grow(sizeof(ShadowRec) * (size_t)n * nLb)) ||
-                (rc2 = A.slist.grow(sizeof(int) * (size_t)n * nLb)))
+            if ((rc2 = W.hits.grow(std::max(sizeof(HitRec), kHitBytes) * (size_t)n)) ||
+                (rc2 = W.shadows.grow(sizeof(ShadowRec) * (size_t)n * nLb)) ||
+                (rc2 = W.slist.grow(sizeof(int) * (size_t)n * nLb)))
                 return rc2;
-            const RayQ cur_q = ray_planes(A.rays.p, R, sv.has_blur);
-            const RayQ next_q = ray_planes(B.rays.p, R, sv.has_blur);
-            unsigned long long* qc = ln.qcnt.as<unsigned long long>() + (ln.level & 1);
+            DBuf* nodes = &A.nodes;
+            if (!pt) {                               // the step's node records stay until the resolve
+                if ((int)ln.snodes.size() <= step) ln.snodes.resize(step + 1);
+                if ((int)ln.step_m.size() <= step) { ln.step_m.resize(step + 1); ln.step_g.resize(step + 1); ln.step_gb.resize(step + 1); }
+                nodes = &ln.snodes[step];
+                ln.step_m[step] = m; ln.step_g[step] = g; ln.step_gb[step] = gbase;
+                // children: at most two per ray (DielectricRefraction, src/Scene.cpp:166-209)
+                // (B is free: its rays were the previous step's queue, consumed earlier on this stream)
+                const long long cap = 2LL * std::max(n, 1);
+                if (B.rcap < cap) B.rcap = cap + cap / 4;        // the planes' stride
+                if ((rc2 = B.rays.grow(kRayBytes * (size_t)B.rcap)) || (rc2 = B.lv.grow((size_t)B.rcap)) ||
+                    (!sv.meta_free && (rc2 = B.meta.grow(sizeof(RayMeta) * (size_t)B.rcap))))
+                    return rc2;
+                seg_node_bytes += (double)sizeof(NodeRec) * n;
+                if (seg_node_bytes > node_budget) seg_closed = true;
+            } else {
+                if ((rc2 = A.nodes.grow(sizeof(NodeRec) * (size_t)n))) return rc2;
+            }
+            if ((rc2 = nodes->grow(sizeof(NodeRec) * (size_t)n))) return rc2;
+            const RayQ cur_q = ray_planes(A.rays.p, A.rcap, sv.has_blur);
+            const RayQ next_q = ray_planes(B.rays.p, B.rcap, sv.has_blur);
+            unsigned long long* qc = ln.qcnt.as<unsigned long long>() + (step & 1);
             HIP_TRY(hipMemsetAsync(qc, 0, sizeof(unsigned long long), ln.st));
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
-            launch_trace(sv, cur_q, A.hits.as<HitRec>(), n, exhaustive, sctr, ln.st, g > 0 ? &cd : nullptr, &F, o.seed,
+            launch_trace(sv, cur_q, W.hits.as<HitRec>(), n, exhaustive, sctr, ln.st, g > 0 ? &cd : nullptr, &F, o.seed,
                          /*compact=*/true, m, gbase);
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[1], ln.st));
-            launch_pt_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), A.hits.as<HitRec>(), A.paths.as<PathRec>(),
-                            A.nodes.as<NodeRec>(), A.shadows.as<ShadowRec>(), A.slist.as<int>(), next_q,
-                            B.meta.as<RayMeta>(), B.paths.as<PathRec>(), qc, n, ln.st, g > 0, m, gbase,
-                            A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
+            if (pt)
+                launch_pt_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), W.hits.as<HitRec>(), A.paths.as<PathRec>(),
+                                nodes->as<NodeRec>(), W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q,
+                                B.meta.as<RayMeta>(), B.paths.as<PathRec>(), qc, n, ln.st, g > 0, m, gbase,
+                                A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
+            else
+                launch_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), W.hits.as<HitRec>(), nodes->as<NodeRec>(),
+                             W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q, B.meta.as<RayMeta>(), qc, nullptr,
+                             nullptr, n, ln.st, g > 0 ? 1 : 0, m, gbase, A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
             HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
             HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
-            launch_shadow(sv, A.shadows.as<ShadowRec>(), A.slist.as<int>(), reinterpret_cast<const unsigned*>(qc) + 1,
-                          A.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*whitted=*/false);
+            launch_shadow(sv, W.shadows.as<ShadowRec>(), W.slist.as<int>(), reinterpret_cast<const unsigned*>(qc) + 1,
+                          nodes->as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*whitted=*/!pt);
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
-            launch_pt_gather(A.nodes.as<NodeRec>(), A.paths.as<PathRec>(), A.shadows.as<ShadowRec>(), nL,
-                             s->d_rad.as<NodeRec>(), seg_slots, m, n, ln.st);
+            if (pt)
+                launch_pt_gather(nodes->as<NodeRec>(), A.paths.as<PathRec>(), W.shadows.as<ShadowRec>(), nL,
+                                 s->d_rad.as<NodeRec>(), seg_slots, m, n, ln.st);
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[5], ln.st));
             HIP_TRY(hipGetLastError());
             ln.level++;
             ln.busy = true;
             return RTG_OK;
         };
-        for (int p0 = 0; p0 < npix; p0 += seg_np) {
-            F.p0 = p0;
-            F.npass = std::min(seg_np, npix - p0);
-            seg_slots = (long long)F.npass * total;
-            cursor = 0;
+        // new samples for a lane's next step: up to R rays with its survivors, whole pixels on the
+        // reference integrator (a pixel's samples are summed from one step's nodes)
+        auto new_samples = [&](long long m) -> int {
+            const long long left = seg_end - cursor;
+            if (left <= 0 || seg_closed) return 0;
+            long long g = std::min(left, std::max(0LL, R - m));
+            if (!pt) {
+                g = (g / total) * total;
+                if (g == 0 && m == 0) g = std::min<long long>(left, total);
+            }
+            return (int)g;
+        };
+        const long long all_slots = (long long)npix * total;
+        while (cursor < all_slots) {
+            // one segment: [cursor, seg_end) of the slots (the path tracer: a radiance buffer's worth)
+            const long long seg_begin = cursor;
+            if (pt) {
+                F.p0 = (int)(cursor / total);
+                F.npass = std::min(seg_np, npix - F.p0);
+                seg_slots = (long long)F.npass * total;
+                seg_end = cursor + seg_slots;
+                cursor = 0;                          // path tracer slots are segment-relative
+                seg_end = seg_slots;
+            } else {
+                seg_end = all_slots;
+            }
+            seg_node_bytes = 0.0;
+            seg_closed = false;
             for (int k = 0; k < SL; k++) {
                 Lane& ln = s->lanes[k];
                 ln.level = 0; ln.sdrain = 0; ln.busy = false;
-                const int g = (int)std::min<long long>(R, seg_slots - cursor);
+                const int g = new_samples(0);
                 if (g <= 0) continue;
                 if ((rc = enqueue_step(ln, 0, g))) return rc;
                 waiting.push_back(k);
@@ -2146,11 +2226,12 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                     stt.trace_ms += a; stt.trace_launches++;
                     stt.shade_ms += c; stt.shade_launches++;
                     if (nL > 0) { stt.shadow_ms += b; stt.shadow_launches++; }
-                    stt.resolve_ms += g2; stt.resolve_launches++;    // the gather, in the resolve slot
+                    if (pt) { stt.resolve_ms += g2; stt.resolve_launches++; }   // the gather, in the resolve slot
                 }
-                if ((long long)next > (long long)ln.sn) return fail(RTG_ERR_HIP, "path queue overflow");
+                if ((long long)next > (pt ? 1LL : 2LL) * ln.sn) return fail(RTG_ERR_HIP, "stream queue overflow");
+                if (!pt && next > 0 && ln.level >= (1 << 20)) return fail(RTG_ERR_UNSUPPORTED, "stream: too many steps");
                 stt.secondary_rays += next;
-                const int g = (int)std::min<long long>(R - (long long)next, seg_slots - cursor);
+                const int g = new_samples(next);
                 if ((long long)next + g > 0) {
                     if ((rc = enqueue_step(ln, (int)next, g))) return rc;
                     waiting.push_back(k);
@@ -2158,25 +2239,59 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                     ln.busy = false;
                 }
             }
-            // the segment's paths have ended: sum every pixel's samples in order, on lane 0 once
-            // every lane's last gather is done; the next segment's gathers wait for that sum
-            Lane& l0 = s->lanes[0];
-            for (int k = 1; k < SL; k++) {
-                HIP_TRY(hipEventRecord(s->lanes[k].ev_join, s->lanes[k].st));
-                HIP_TRY(hipStreamWaitEvent(l0.st, s->lanes[k].ev_join, 0));
-            }
             const int mode = total == 1 ? 2 : 1;
-            if ((rc = timed_launch(l0, [&] {
-                     launch_accumulate(sv, s->d_rad.as<NodeRec>(), nullptr, false, s->d_acc.as<float>(), F, cam->nx, mode,
-                                       l0.st, /*whitted=*/false, (int)seg_slots, 0);
-                 }, stt.accumulate_ms, stt.accumulate_launches)))
-                return rc;
-            HIP_TRY(hipEventRecord(l0.ev_join, l0.st));
-            for (int k = 1; k < SL; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k].st, l0.ev_join, 0));
+            if (pt) {
+                // the segment's paths have ended: sum every pixel's samples in order, on lane 0 once
+                // every lane's last gather is done; the next segment's gathers wait for that sum
+                Lane& l0 = s->lanes[0];
+                for (int k = 1; k < SL; k++) {
+                    HIP_TRY(hipEventRecord(s->lanes[k].ev_join, s->lanes[k].st));
+                    HIP_TRY(hipStreamWaitEvent(l0.st, s->lanes[k].ev_join, 0));
+                }
+                if ((rc = timed_launch(l0, [&] {
+                         launch_accumulate(sv, s->d_rad.as<NodeRec>(), nullptr, false, s->d_acc.as<float>(), F, cam->nx,
+                                           mode, l0.st, /*whitted=*/false, (int)seg_slots, 0);
+                     }, stt.accumulate_ms, stt.accumulate_launches)))
+                    return rc;
+                HIP_TRY(hipEventRecord(l0.ev_join, l0.st));
+                for (int k = 1; k < SL; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k].st, l0.ev_join, 0));
+                cursor = (long long)(F.p0 + F.npass) * total;       // back to frame slots
+            } else {
+                // every tree of the segment has ended: bottom-up, last step first, per lane
+                for (int k = 0; k < SL; k++) {
+                    Lane& ln = s->lanes[k];
+                    const int K = ln.level;
+                    for (int j = K - 1; j >= 0; j--) {
+                        const int n = ln.step_m[j] + ln.step_g[j];
+                        const NodePlanes self = node_planes(ln.snodes[j].as<NodeRec>(), n);
+                        const NodePlanes child = j + 1 < K ? node_planes(ln.snodes[j + 1].as<NodeRec>(),
+                                                                         ln.step_m[j + 1] + ln.step_g[j + 1])
+                                                           : self;     // no children: every link is -1
+                        if (ln.step_m[j] > 0 &&
+                            (rc = timed_launch(ln, [&] { launch_resolve_planes(sv, self, child, ln.step_m[j], ln.st); },
+                                               stt.resolve_ms, stt.resolve_launches)))
+                            return rc;
+                        if (ln.step_g[j] > 0) {
+                            const int mj = ln.step_m[j];
+                            const NodePlanes l0 = {self.col + mj, self.pnt + mj, self.link + mj};
+                            PassDev P = F;
+                            P.p0 = ln.step_gb[j] / total;
+                            P.npass = ln.step_g[j] / total;
+                            if ((rc = timed_launch(ln, [&] {
+                                     launch_accumulate_planes(sv, l0, child, true, s->d_acc.as<float>(), P, cam->nx, mode,
+                                                              ln.st);
+                                 }, stt.accumulate_ms, stt.accumulate_launches)))
+                                return rc;
+                        }
+                    }
+                    HIP_TRY(hipGetLastError());
+                }
+                if (cursor == seg_begin) return fail(RTG_ERR_OOM, "stream: a segment made no progress");
+            }
             stt.passes++;
         }
     }
-    for (int k = 0; k < L && !stream_pt; k++)
+    for (int k = 0; k < L && !stream; k++)
         if (!s->lanes[k].passes.empty() && npix > 0) {
             if ((rc = start_pass(s->lanes[k]))) return rc;
             waiting.push_back(k);

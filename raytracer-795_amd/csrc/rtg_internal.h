@@ -385,9 +385,19 @@ void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
                   uint64_t seed = 0, bool compact = false, int nq = 0, int gbase = 0);
 // rlist / rcount: the level's non-final nodes (levels >= 1), appended for k_resolve
+// gen: 1 = rays i >= nq are primary rays of slots gbase + i - nq, 0 = queued only, -1 = a pass's level
+// (primaries iff rays.a is null); lv_in / lv_out: per-ray levels of a stream step (or null)
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
-                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st);
+                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st,
+                  int gen = -1, int nq = 0, int gbase = 0, const unsigned char* lv_in = nullptr,
+                  unsigned char* lv_out = nullptr);
+// the bottom-up step and the accumulation on explicit node planes (stream schedule: a step's nodes
+// [0, count) against the next step's; the primaries of a pixel range at an offset of a step's planes)
+void launch_resolve_planes(const SceneView& sv, const NodePlanes& self, const NodePlanes& child, int count,
+                           hipStream_t st);
+void launch_accumulate_planes(const SceneView& sv, const NodePlanes& level0, const NodePlanes& level1, bool resolve,
+                              float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
                    int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted = true);
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
