@@ -75,7 +75,14 @@ namespace rtg {
 #ifndef RTG_SHADE_FULL_WAVES
 #define RTG_SHADE_FULL_WAVES 2
 #endif
-#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? RTG_SHADE_FULL_WAVES : SPOT ? 2 : RTG_SHADE_WAVES)))
+// Round 4: the full variant without textures / BRDFs and without spot / environment lights
+// (SPOT = false, light_sample) needs 105 VGPRs instead of 255; capped at 5 waves per SIMD it fits
+// 94 with no spill (cornell_dynamic 1080p64: 16.4 ms/frame at 5 waves, 16.8 at 4 or 3)
+#ifndef RTG_SHADE_LIGHT_WAVES
+#define RTG_SHADE_LIGHT_WAVES 5
+#endif
+#define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? (!SPOT && !TEX ? RTG_SHADE_LIGHT_WAVES : RTG_SHADE_FULL_WAVES) \
+                                                            : SPOT ? 2 : RTG_SHADE_WAVES)))
 // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
 // spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); round 3, with
 // one BRDF call site (167 VGPRs, no spill at 3 waves): 4 waves spill 140-164 B and lose, 398 -> 404
@@ -1269,6 +1276,11 @@ DEV float emit_shadow_tmax(f3 origin, f3 p, f3 lp, f3 d, float eps) {
 
 // EMIT: the hw7 object-light cases (the path tracer's NEE; the Whitted light loop never reaches
 // them: the render adds the object lights to the loop only for the path tracer)
+// SPOT: the scene has a spot or (full variants) an environment light (SceneView::heavy).  Their
+// double-precision libm code (spot fall-off: acos, cos, pow; environment: acos, atan2 and the
+// rejection loop) sets the register peak of the shading kernels: inlined into the full k_shade it
+// takes the light loop from 79 to 244 VGPRs (cross-compiled resource usage, round 4), so scenes
+// without such lights get variants without that code.
 template <bool FULL = true, bool SPOT = true, bool BRDF = FULL, bool EMIT = true>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
                       uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
@@ -1304,7 +1316,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         lit = true;
         break;
     }
-    case RTG_LIGHT_SPOT: if constexpr (FULL || SPOT) {          // Light.cpp:409-436
+    case RTG_LIGHT_SPOT: if constexpr (SPOT) {                  // Light.cpp:409-436
         f3 pos = ld3(L.pos);
         dir = toward(pos, ret.point);
         lp = pos;
@@ -1341,7 +1353,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
         lit = true;
         break;
     }
-    case RTG_LIGHT_ENVIRONMENT: if constexpr (FULL) {          // Light.cpp:628-660
+    case RTG_LIGHT_ENVIRONMENT: if constexpr (FULL && SPOT) {  // Light.cpp:628-660
         f3 n = ret.normal;
         f3 u = ortho_u(n);
         f3 w = cross(n, u);
@@ -2613,8 +2625,11 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
             hipLaunchKernelGGL((k_shade<F, S, B, T, false>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
                                slist, next_rays, next_meta, qcount, rlist, rcount, n, nq, gbase, lv_in, lv_out); \
     } while (0)
-    if (sv.full && sv.tex) RTG_SHADE(true, true, 256, true, dim3(nblk(n, 256)), dim3(256));
-    else if (sv.full) RTG_SHADE(true, true, 256, false, dim3(nblk(n, 256)), dim3(256));
+    // full variants: SPOT = a spot or environment light (their libm code compiled in)
+    if (sv.full && sv.tex && sv.heavy) RTG_SHADE(true, true, 256, true, dim3(nblk(n, 256)), dim3(256));
+    else if (sv.full && sv.tex) RTG_SHADE(true, false, 256, true, dim3(nblk(n, 256)), dim3(256));
+    else if (sv.full && sv.heavy) RTG_SHADE(true, true, 256, false, dim3(nblk(n, 256)), dim3(256));
+    else if (sv.full) RTG_SHADE(true, false, 256, false, dim3(nblk(n, 256)), dim3(256));
     else if (sv.spot) RTG_SHADE(false, true, kShadeBlock, false, g, b);
     else RTG_SHADE(false, false, kShadeBlock, false, g, b);
 #undef RTG_SHADE
@@ -2654,7 +2669,9 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
         else RTG_PT_LAUNCH1(F, S, B, false);                                                                      \
     } while (0)
     // textures / area / environment lights need the full variant; BRDFs alone do not
-    if (sv.full && !sv.brdf_only) RTG_PT_LAUNCH(true, true, true);
+    if (sv.full && !sv.brdf_only) {
+        if (sv.heavy) RTG_PT_LAUNCH(true, true, true); else RTG_PT_LAUNCH(true, false, true);
+    }
     else if (sv.full) { if (sv.spot) RTG_PT_LAUNCH(false, true, true); else RTG_PT_LAUNCH(false, false, true); }
     else if (sv.spot) RTG_PT_LAUNCH(false, true, false);
     else RTG_PT_LAUNCH(false, false, false);

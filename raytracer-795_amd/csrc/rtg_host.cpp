@@ -892,7 +892,7 @@ struct rtg_scene {
     int stream_lanes = 4;                    // path tracer's stream schedule (env RTG_STREAM_LANES)
     int stream_pt = 1;                       // 0: path tracer on the pass schedule (env RTG_STREAM_PT)
     int stream_seg_pix = 0;                  // > 0: pixels per stream segment (env RTG_STREAM_SEG_PIX, tests)
-    int stream_whitted = 1;                  // 0: reference integrator on the pass schedule (env RTG_STREAM_WHITTED)
+    int stream_whitted = 0;                  // 1: reference integrator on the stream schedule by default (env RTG_STREAM_WHITTED)
     int stream_div = 3;                      // about this many new-sample steps per lane (env RTG_STREAM_DIV)
     long long stream_node_budget = 0;        // > 0: node-record bytes per segment (env RTG_STREAM_NODE_BUDGET, tests)
     int bvh_builder = RTG_BVH_AUTO;
@@ -1675,6 +1675,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.full |= any_brdf;
     sv.spot = 0;
     for (int i = 0; i < d->num_lights; i++) sv.spot |= d->lights[i].type == RTG_LIGHT_SPOT;
+    sv.heavy = sv.spot || d->environment_light != -1;
+    for (int i = 0; i < d->num_lights; i++) sv.heavy |= d->lights[i].type == RTG_LIGHT_ENVIRONMENT;
     int any_rough = 0;
     for (int i = 0; i < d->num_materials; i++) any_rough |= d->materials[i].is_rough != 0;
     sv.meta_free = !sv.full && !any_rough;
@@ -2057,7 +2059,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     const bool want_stream = o.schedule == RTG_SCHEDULE_STREAM ||
                              (o.schedule == RTG_SCHEDULE_AUTO && (pt ? s->stream_pt : s->stream_whitted));
     const bool stream = want_stream && npix > 0 && (long long)npix * total < (1LL << 31) &&
-                        (pt || (s->stream_whitted && !RTG_RESOLVE_LIST));
+                        (pt || !RTG_RESOLVE_LIST);
     if (stream) {
         const int SL = o.streams > 0 ? std::min(o.streams, 8) : s->stream_lanes;
         while ((int)s->lanes.size() < SL) {

@@ -187,6 +187,8 @@ struct SceneView {
     int bg_texture, env_light;
     int full;                      // 0: no textures / BRDFs / area or environment lights
     int spot;                      // any spot light (its double-precision cone math is compiled in)
+    int heavy;                     // a spot or environment light: the full shading variants compile in
+                                   // their double-precision libm code only then (light_sample)
     int brdf_only;                 // full only because of BRDFs (no textures / area / environment)
     int tex;                       // any textured object or BRDF material (k_shade's TEX variant)
     int meta_free;                 // Whitted: no RNG below level 0 (no textures / area / environment

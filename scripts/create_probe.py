@@ -1,0 +1,24 @@
+"""Scene-creation phases of the dragon1m scene, created several times in one process (the first
+includes one-time HIP / code-object set-up).  usage: python scripts/create_probe.py [times]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytracer-795_amd"))
+import torch  # noqa: E402,F401
+import rtg  # noqa: E402
+from rtg import scenegen  # noqa: E402
+
+times = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+sc = scenegen.dragon1m(1920, 1080, spp=64)
+torch.cuda.init()
+for k in range(times):
+    t0 = time.perf_counter()
+    r = rtg.Renderer(sc, 0)
+    ms = (time.perf_counter() - t0) * 1e3
+    bs = r.build_stats()
+    print(json.dumps({"create": k, "wall_ms": round(ms, 1),
+                      **{q: round(v, 1) if isinstance(v, float) else v for q, v in bs.items()}}), flush=True)
+    r.close()

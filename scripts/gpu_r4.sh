@@ -27,9 +27,12 @@ for step in "$@"; do
     bench) run bench 300 python3 bench.py ;;
     bench_*) run $step 400 python3 bench.py --workload ${step#bench_} ;;
     nocpu_*) run $step 300 python3 bench.py --no-cpu --workload ${step#nocpu_} ;;
+    create) run create 300 env RTG_BUILD_TIMING=1 python3 scripts/create_probe.py 3 ;;
     shard) run shard 300 python3 scripts/shard_probe.py 1 8 ;;
     eb:*) IFS=: read -r _ kv wl <<< "$step"; name="eb_${kv//=/_}_$wl"
           run $name 300 env $kv python3 bench.py --no-cpu --workload $wl ;;
+    lib:*) IFS=: read -r _ lib wl <<< "$step"; run lib_${lib}_$wl 300 env RTG_LIBRARY=raytracer-795_amd/rtg/$lib.so python3 bench.py --no-cpu --workload $wl ;;
+    shardenv:*) IFS=: read -r _ kv <<< "$step"; run shard_${kv//=/_} 300 env $kv python3 scripts/shard_probe.py 1 8 ;;
     kt_*) wl=${step#kt_}; run $step 300 rocprofv3 --kernel-trace --stats -d $D/$step -o kt --output-format csv -- python3 scripts/tl_probe.py $wl 2
           python3 scripts/tl_util.py $(ls $D/$step/*kernel_trace.csv | head -1) > $D/${step}_util.txt; cat $D/${step}_util.txt ;;
     ktshard_*) wl=${step#ktshard_}; run $step 300 rocprofv3 --kernel-trace --stats -d $D/$step -o kt --output-format csv -- python3 scripts/tl_probe.py $wl 3 0 8

@@ -2,7 +2,7 @@
 # Per-kernel VGPR / scratch summary of the device code (cross-compiled, no GPU needed).
 cd "$(dirname "$0")/../raytracer-795_amd/csrc"
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt \
-  -fno-gpu-flush-denormals-to-zero -Xclang -target-feature -Xclang -packed-fp32-ops --cuda-device-only -c rtg_device.hip -o /tmp/rtg_dev_regs.o \
+  -fno-gpu-flush-denormals-to-zero $EXTRA -Xclang -target-feature -Xclang -packed-fp32-ops --cuda-device-only -c rtg_device.hip -o /tmp/rtg_dev_regs.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c '
 import re, sys
 name = None

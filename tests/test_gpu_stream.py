@@ -45,15 +45,15 @@ def test_stream_equals_passes_reference_integrator(gpu, name, monkeypatch):
         assert st["passes"] >= 1
 
 
-def test_stream_default_matches_oracle_and_shards(gpu):
-    """The default schedule of the reference integrator is the stream: against the oracle, and row
-    shards gathered bit-exactly."""
+def test_stream_matches_oracle_and_shards(gpu):
+    """The reference integrator on the stream schedule (the pass schedule is its default since
+    round 4: DESIGN.md §4 "Schedules"): against the oracle, and row shards gathered bit-exactly."""
     sc = scenegen.glass_nest(30, 20, spp=3, max_depth=6)
     with rtg.Renderer(sc, device=gpu) as r:
-        img = r.render(0)
+        img = r.render(0, schedule=A.SCHEDULE_STREAM)
         acc = np.zeros_like(img)
         for rank in range(3):
-            acc += r.render(0, row_offset=rank, row_stride=3, row_block=4)
+            acc += r.render(0, row_offset=rank, row_stride=3, row_block=4, schedule=A.SCHEDULE_STREAM)
     ref, _, _, _ = pyoracle.Oracle(sc).render(0)
     assert _same(np.nan_to_num(img), np.nan_to_num(ref))
     assert _same(acc, img)
