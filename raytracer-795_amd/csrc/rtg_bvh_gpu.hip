@@ -24,6 +24,9 @@
 #include <limits.h>
 
 #include <hipcub/hipcub.hpp>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 #include <string>
 #include <vector>
@@ -305,10 +308,23 @@ inline int nb(long long n, int b) { return (int)((n + b - 1) / b); }
         }                                                                      \
     } while (0)
 
+// One empty launch: loads this module's code object (the first launch of a module costs ~7 ms).
+void gpu_bvh_warm(hipStream_t st) { hipLaunchKernelGGL(k_iota, dim3(1), dim3(64), 0, st, 0, nullptr); }
+
 int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, int n, GpuBvh& out, std::string& err,
                   hipStream_t st) {
     out = GpuBvh();
     if (n <= 0) { out.root = -1; return 0; }
+    // RTG_BUILD_TIMING: wall time of the build's stages on stderr (synchronising between them)
+    const bool timing = getenv("RTG_BUILD_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        (void)hipStreamSynchronize(st);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[rtg] gpu bvh %-10s %7.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     DevArr<float> c3, lo3, hi3, box;
     DevArr<int> perm, perm2, segid, less, G, ptr, lens, offs, nn, ni, nnoff, nioff, big, cnt;
     DevArr<int4> nodes;
@@ -330,7 +346,9 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
     BVH_TRY(segs.grow(scap)); BVH_TRY(next.grow(scap));
     size_t node_cap = 2 * (size_t)n + 64;
     BVH_TRY(nodes.grow(node_cap)); BVH_TRY(box.grow(6 * node_cap));
+    lap("alloc+h2d");
     hipLaunchKernelGGL(k_iota, dim3(nb(n, 256)), dim3(256), 0, st, n, perm.p);
+    lap("first-kern");
 
     // root: construct(0, n, 0, 0)
     int num_nodes = 1;
@@ -343,6 +361,7 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
         if (n >= kBigNode) hipLaunchKernelGGL(k_box_big, dim3(1), dim3(256), 0, st, big.p, cnt.p, nodes.p, perm.p, lo3.p, hi3.p, box.p);
         else hipLaunchKernelGGL(k_box_small, dim3(1), dim3(64), 0, st, nodes.p, 0, 1, perm.p, lo3.p, hi3.p, box.p);
     }
+    out.level_start.assign(1, 0);
     int S = 0;
     if (n >= 2) {
         Seg s0; s0.start = 0; s0.end = n; s0.node = 0; s0.off = 0;
@@ -421,18 +440,22 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
                                    box.p);
         }
         BVH_TRY(hipGetLastError());
+        out.level_start.push_back(num_nodes);   // depth + 1 starts here
         num_nodes += new_nodes;
         std::swap(segs.p, next.p);
         std::swap(segs.cap, next.cap);
         S = S_next;
     }
-    out.perm.resize(n);
-    out.nodes.resize(num_nodes);
-    out.box.resize(6 * (size_t)num_nodes);
-    BVH_TRY(hipMemcpyAsync(out.perm.data(), perm.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-    BVH_TRY(hipMemcpyAsync(out.nodes.data(), nodes.p, sizeof(int4) * num_nodes, hipMemcpyDeviceToHost, st));
-    BVH_TRY(hipMemcpyAsync(out.box.data(), box.p, sizeof(float) * 6 * num_nodes, hipMemcpyDeviceToHost, st));
+    lap("levels");
+    out.level_start.push_back(num_nodes);
+    BVH_TRY(out.perm.alloc(n));
+    BVH_TRY(out.nodes.alloc(num_nodes));
+    BVH_TRY(out.box.alloc(6 * (size_t)num_nodes));
+    BVH_TRY(hipMemcpyAsync(out.perm.p, perm.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+    BVH_TRY(hipMemcpyAsync(out.nodes.p, nodes.p, sizeof(int4) * num_nodes, hipMemcpyDeviceToHost, st));
+    BVH_TRY(hipMemcpyAsync(out.box.p, box.p, sizeof(float) * 6 * num_nodes, hipMemcpyDeviceToHost, st));
     BVH_TRY(hipStreamSynchronize(st));
+    lap("d2h");
     out.root = 0;
     return 0;
 }

@@ -2606,6 +2606,9 @@ void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int
     else RTG_TRACE(false, false, false);
 #undef RTG_TRACE
 }
+__global__ void k_warm() {}
+void device_warm(hipStream_t st) { hipLaunchKernelGGL(k_warm, dim3(1), dim3(64), 0, st); }
+
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,

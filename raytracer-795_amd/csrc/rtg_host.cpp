@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <new>
 #include <string>
@@ -218,6 +219,49 @@ inline float maxOf3(float a, float b, float c) {
     return c;
 }
 
+// Allocator whose value-less construct() leaves the element uninitialised: the scene build's large
+// record arrays are written in full by parallel loops, so resize() need not zero hundreds of MB on
+// one thread first (the pages are touched first by the threads that fill them).
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInit<U>; };
+    NoInit() = default;
+    template <class U> NoInit(const NoInit<U>&) noexcept {}
+    template <class U, class... A>
+    void construct(U* q, A&&... a) {
+        if constexpr (sizeof...(A) == 0) ::new ((void*)q) U;
+        else ::new ((void*)q) U(std::forward<A>(a)...);
+    }
+};
+template <class T> using hvec = std::vector<T, NoInit<T>>;
+
+// Host worker threads of the scene build: up to 16 (the GPU box's CPU share per GPU), chunks of
+// at least `grain` items.  f(chunk, begin, end) runs once per chunk; chunks are numbered in order,
+// so per-chunk partial results combine deterministically.  Exceptions reach the caller.
+inline int build_threads() {
+    static const int n = [] {
+        int t = (int)std::thread::hardware_concurrency();
+        if (const char* e = getenv("RTG_BUILD_THREADS")) t = atoi(e);
+        return std::max(1, std::min(16, t));
+    }();
+    return n;
+}
+template <class F>
+int parallel_chunks(size_t n, size_t grain, F&& f) {
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)build_threads(), (n + grain - 1) / std::max<size_t>(grain, 1)));
+    if (T <= 1) { if (n) f(0, (size_t)0, n); return 1; }
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(T);
+    for (int c = 1; c < T; c++)
+        th.emplace_back([&, c] {
+            try { f(c, n * c / T, n * (c + 1) / T); } catch (...) { err[c] = std::current_exception(); }
+        });
+    try { f(0, (size_t)0, n / T); } catch (...) { err[0] = std::current_exception(); }
+    for (std::thread& t : th) t.join();
+    for (auto& e : err) if (e) std::rethrow_exception(e);
+    return T;
+}
+
 struct HNode {            // pre-order node of the reference tree
     int left, right;      // node numbers, -1 null
     int start, end;
@@ -225,8 +269,8 @@ struct HNode {            // pre-order node of the reference tree
 };
 
 struct ObjBVH {
-    std::vector<int> perm;        // BVH position -> original prim index
-    std::vector<HNode> nodes;     // pre-order
+    hvec<int> perm;               // BVH position -> original prim index
+    hvec<HNode> nodes;            // pre-order
     int root = -1;
 };
 
@@ -234,8 +278,8 @@ struct BuildCtx {
     const V3* centers;            // per original prim
     const V3* bmin;               // per original prim
     const V3* bmax;
-    std::vector<int>* prims;      // current permutation
-    std::vector<HNode>* nodes;
+    hvec<int>* prims;             // current permutation
+    hvec<HNode>* nodes;
     std::vector<float> scratch;
 };
 
@@ -295,6 +339,83 @@ int construct(BuildCtx& B, int start, int end, int splitType, int depth) {
     return n;
 }
 
+// construct() with the subtrees of the top `pdepth` levels (>= 64K primitives) built on their own
+// threads, each into its own pre-order node array (its own BuildCtx), appended left then right with
+// their child numbers shifted: the same permutation and the same pre-order nodes as the recursion
+// (the two halves partition disjoint ranges of the permutation).  The top node's box is reduced in
+// parallel (min / max are exact in any order); the median selection and the reference's swap
+// partition stay sequential -- they define the permutation.
+int construct_par(BuildCtx& B, int start, int end, int splitType, int depth, int pdepth) {
+    if (pdepth <= 0 || end - start < (1 << 16) || start == end - 1 || depth >= 30) return construct(B, start, end, splitType, depth);
+    if (splitType > 2) splitType = 0;
+    const int n = (int)B.nodes->size();
+    {
+        HNode h;
+        h.left = h.right = -1; h.start = start; h.end = end;
+        const int len = end - start;
+        std::vector<std::array<float, 6>> part(build_threads());
+        const int T = parallel_chunks((size_t)len, 1 << 15, [&](int ch, size_t k0, size_t k1) {
+            float mn[3], mx[3];
+            range_box(B, start + (int)k0, start + (int)k1, mn, mx);
+            part[ch] = {mn[0], mn[1], mn[2], mx[0], mx[1], mx[2]};
+        });
+        for (int z = 0; z < 3; z++) { h.mn[z] = part[0][z]; h.mx[z] = part[0][3 + z]; }
+        for (int c = 1; c < T; c++)
+            for (int z = 0; z < 3; z++) { h.mn[z] = min2(h.mn[z], part[c][z]); h.mx[z] = max2(h.mx[z], part[c][3 + z]); }
+        B.nodes->push_back(h);
+    }
+    int* p = B.prims->data();
+    const int len = end - start;
+    B.scratch.resize(len);
+    parallel_chunks((size_t)len, 1 << 15, [&](int, size_t k0, size_t k1) {
+        for (size_t i = k0; i < k1; i++) B.scratch[i] = comp(B.centers[p[start + i]], splitType);
+    });
+    const int mi = len / 2;
+    std::nth_element(B.scratch.begin(), B.scratch.begin() + mi, B.scratch.end());
+    float split = B.scratch[mi];
+    if (len % 2 == 0) {
+        const float lower = *std::max_element(B.scratch.begin(), B.scratch.begin() + mi);
+        split = (lower + split) * 0.5f;
+    }
+    int swapIndex = start;
+    for (int i = start; i < end; i++) {
+        if (comp(B.centers[p[i]], splitType) < split) {
+            std::swap(p[swapIndex], p[i]);
+            swapIndex++;
+        }
+    }
+    hvec<HNode> L, R;
+    BuildCtx BL{B.centers, B.bmin, B.bmax, B.prims, &L, {}}, BR{B.centers, B.bmin, B.bmax, B.prims, &R, {}};
+    int l = -1, r = -1;
+    std::exception_ptr err;
+    std::thread t([&] {
+        try { l = construct_par(BL, start, swapIndex, splitType + 1, depth + 1, pdepth - 1); } catch (...) { err = std::current_exception(); }
+    });
+    try {
+        r = construct_par(BR, swapIndex, end, splitType + 1, depth + 1, pdepth - 1);
+    } catch (...) {
+        t.join();
+        throw;
+    }
+    t.join();
+    if (err) std::rethrow_exception(err);
+    auto append = [&](const hvec<HNode>& sub, int root) {
+        if (root < 0) return -1;
+        const int off = (int)B.nodes->size();
+        for (HNode x : sub) {
+            if (x.left >= 0) x.left += off;
+            if (x.right >= 0) x.right += off;
+            B.nodes->push_back(x);
+        }
+        return off + root;
+    };
+    const int lo = append(L, l);
+    const int ro = append(R, r);
+    (*B.nodes)[n].left = lo;
+    (*B.nodes)[n].right = ro;
+    return n;
+}
+
 // ------------------------------------------------------------------ traversal tree (SAH, 4-wide)
 // The reference's median-split tree (one primitive per leaf, axis = depth % 3) decides *which*
 // candidates exist -- a primitive counts only if every interior box above its leaf is hit
@@ -331,64 +452,113 @@ inline double sah_area(const float lo[3], const float hi[3]) {
     return dx * dy + dy * dz + dz * dx;
 }
 
-// Node box and split of the SAH-ordered range [s, e) (partitions idx[s, e)); returns the split
-// position, or -1 for a leaf.
-int sah_split(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::vector<int>& idx, int s, int e,
-              SahNode2& nd) {
-    float clo[3], chi[3];
-    for (int z = 0; z < 3; z++) { nd.lo[z] = clo[z] = FLT_MAX; nd.hi[z] = chi[z] = -FLT_MAX; }
-    for (int k = s; k < e; k++) {
-        const SahBox& b = pb[idx[k]];
-        const float c[3] = {pc[idx[k]].x, pc[idx[k]].y, pc[idx[k]].z};
-        for (int z = 0; z < 3; z++) {
-            nd.lo[z] = std::min(nd.lo[z], b.lo[z]);
-            nd.hi[z] = std::max(nd.hi[z], b.hi[z]);
-            clo[z] = std::min(clo[z], c[z]);
-            chi[z] = std::max(chi[z], c[z]);
+// One triangle of the binned-SAH build: its box and face index, partitioned in place (32 B,
+// so the passes over a range stream through memory instead of gathering through an index array;
+// 1 M-triangle dragon: the tree's build went from 86 ms to ...).  The centroid is the box centre.
+struct SahRec {
+    float lo[3], hi[3];
+    int idx, pad_;
+};
+inline float sah_ctr(const SahRec& r, int z) { return 0.5f * (r.lo[z] + r.hi[z]); }
+
+// Node box and split of the SAH-ordered range [s, e) (partitions r[s, e)); returns the split
+// position, or -1 for a leaf.  Ranges of >= kSahParMin triangles run their passes on the build's
+// worker threads (per-chunk bounds and bins combined in chunk order; a stable partition through
+// `tmp`), smaller ones on the calling thread (std::partition).
+constexpr int kSahParMin = 1 << 18;
+int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd) {
+    const int n = e - s;
+    const bool par = n >= kSahParMin;
+    struct Bounds { float lo[3], hi[3], clo[3], chi[3]; };
+    auto bounds_of = [&](size_t k0, size_t k1) {
+        Bounds B;
+        for (int z = 0; z < 3; z++) { B.lo[z] = B.clo[z] = FLT_MAX; B.hi[z] = B.chi[z] = -FLT_MAX; }
+        for (size_t k = k0; k < k1; k++) {
+            const SahRec& q = r[k];
+            for (int z = 0; z < 3; z++) {
+                const float c = sah_ctr(q, z);
+                B.lo[z] = std::min(B.lo[z], q.lo[z]);
+                B.hi[z] = std::max(B.hi[z], q.hi[z]);
+                B.clo[z] = std::min(B.clo[z], c);
+                B.chi[z] = std::max(B.chi[z], c);
+            }
         }
+        return B;
+    };
+    Bounds B;
+    if (par) {
+        std::vector<Bounds> part(build_threads());
+        const int T = parallel_chunks((size_t)n, 1 << 15, [&](int ch, size_t k0, size_t k1) { part[ch] = bounds_of(s + k0, s + k1); });
+        B = part[0];
+        for (int c = 1; c < T; c++)
+            for (int z = 0; z < 3; z++) {
+                B.lo[z] = std::min(B.lo[z], part[c].lo[z]); B.hi[z] = std::max(B.hi[z], part[c].hi[z]);
+                B.clo[z] = std::min(B.clo[z], part[c].clo[z]); B.chi[z] = std::max(B.chi[z], part[c].chi[z]);
+            }
+    } else {
+        B = bounds_of(s, e);
     }
+    for (int z = 0; z < 3; z++) { nd.lo[z] = B.lo[z]; nd.hi[z] = B.hi[z]; }
     nd.left = nd.right = -1;
     nd.start = s;
-    nd.count = e - s;
-    const int n = e - s;
+    nd.count = n;
     if (n <= 1) return -1;
     int axis = 0;
     for (int z = 1; z < 3; z++)
-        if (chi[z] - clo[z] > chi[axis] - clo[axis]) axis = z;
-    const float ext = chi[axis] - clo[axis];
+        if (B.chi[z] - B.clo[z] > B.chi[axis] - B.clo[axis]) axis = z;
+    const float ext = B.chi[axis] - B.clo[axis];
     int mid = -1;
     if (ext > 0.0f) {
-        int cnt[kSahBins] = {};
-        float blo[kSahBins][3], bhi[kSahBins][3];
-        for (int b = 0; b < kSahBins; b++)
-            for (int z = 0; z < 3; z++) { blo[b][z] = FLT_MAX; bhi[b][z] = -FLT_MAX; }
         const float sc = (float)kSahBins / ext;
-        auto bin_of = [&](int p) {
-            const float c = axis == 0 ? pc[p].x : (axis == 1 ? pc[p].y : pc[p].z);
-            return std::min(kSahBins - 1, std::max(0, (int)((c - clo[axis]) * sc)));
+        const float c0 = B.clo[axis];
+        auto bin_of = [&](const SahRec& q) {
+            return std::min(kSahBins - 1, std::max(0, (int)((sah_ctr(q, axis) - c0) * sc)));
         };
-        for (int k = s; k < e; k++) {
-            const int b = bin_of(idx[k]);
-            cnt[b]++;
-            for (int z = 0; z < 3; z++) {
-                blo[b][z] = std::min(blo[b][z], pb[idx[k]].lo[z]);
-                bhi[b][z] = std::max(bhi[b][z], pb[idx[k]].hi[z]);
+        struct Bins { int cnt[kSahBins]; float lo[kSahBins][3], hi[kSahBins][3]; };
+        auto bins_of = [&](size_t k0, size_t k1, Bins& Q) {
+            for (int b = 0; b < kSahBins; b++) {
+                Q.cnt[b] = 0;
+                for (int z = 0; z < 3; z++) { Q.lo[b][z] = FLT_MAX; Q.hi[b][z] = -FLT_MAX; }
             }
+            for (size_t k = k0; k < k1; k++) {
+                const int b = bin_of(r[k]);
+                Q.cnt[b]++;
+                for (int z = 0; z < 3; z++) {
+                    Q.lo[b][z] = std::min(Q.lo[b][z], r[k].lo[z]);
+                    Q.hi[b][z] = std::max(Q.hi[b][z], r[k].hi[z]);
+                }
+            }
+        };
+        Bins Q;
+        if (par) {
+            std::vector<Bins> part(build_threads());
+            const int T = parallel_chunks((size_t)n, 1 << 15, [&](int ch, size_t k0, size_t k1) { bins_of(s + k0, s + k1, part[ch]); });
+            Q = part[0];
+            for (int c = 1; c < T; c++)
+                for (int b = 0; b < kSahBins; b++) {
+                    Q.cnt[b] += part[c].cnt[b];
+                    for (int z = 0; z < 3; z++) {
+                        Q.lo[b][z] = std::min(Q.lo[b][z], part[c].lo[b][z]);
+                        Q.hi[b][z] = std::max(Q.hi[b][z], part[c].hi[b][z]);
+                    }
+                }
+        } else {
+            bins_of(s, e, Q);
         }
         double rcost[kSahBins];
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
         int rc = 0;
         for (int b = kSahBins - 1; b >= 1; b--) {
-            rc += cnt[b];
-            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], blo[b][z]); hi[z] = std::max(hi[z], bhi[b][z]); }
+            rc += Q.cnt[b];
+            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], Q.lo[b][z]); hi[z] = std::max(hi[z], Q.hi[b][z]); }
             rcost[b] = rc ? sah_area(lo, hi) * rc : 0.0;
         }
         for (int z = 0; z < 3; z++) { lo[z] = FLT_MAX; hi[z] = -FLT_MAX; }
         int lc = 0, best_b = -1;
         double best = 1e300;
         for (int b = 0; b < kSahBins - 1; b++) {
-            lc += cnt[b];
-            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], blo[b][z]); hi[z] = std::max(hi[z], bhi[b][z]); }
+            lc += Q.cnt[b];
+            for (int z = 0; z < 3; z++) { lo[z] = std::min(lo[z], Q.lo[b][z]); hi[z] = std::max(hi[z], Q.hi[b][z]); }
             if (lc == 0 || lc == n) continue;
             const double cost = sah_area(lo, hi) * lc + rcost[b + 1];
             if (cost < best) { best = cost; best_b = b; }
@@ -397,9 +567,35 @@ int sah_split(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::vec
         const double leaf_cost = sah_area(nd.lo, nd.hi) * n;
         if (n <= kSahMaxLeaf && (best_b < 0 || leaf_cost <= sah_area(nd.lo, nd.hi) + best)) return -1;
         if (best_b >= 0) {
-            int* first = idx.data() + s;
-            int* pivot = std::partition(first, idx.data() + e, [&](int p) { return bin_of(p) <= best_b; });
-            mid = (int)(pivot - idx.data());
+            auto left = [&](const SahRec& q) { return bin_of(q) <= best_b; };
+            if (par) {
+                // stable: per-chunk left counts, then every chunk scatters its records to their
+                // places in tmp, then back
+                std::vector<int> nl(build_threads() + 1, 0), nr(build_threads() + 1, 0);
+                const int T = parallel_chunks((size_t)n, 1 << 15, [&](int ch, size_t k0, size_t k1) {
+                    int c = 0;
+                    for (size_t k = k0; k < k1; k++) c += left(r[s + k]);
+                    nl[ch] = c;
+                    nr[ch] = (int)(k1 - k0) - c;
+                });
+                std::vector<int> lo_at(T), hi_at(T);
+                int acc = 0;
+                for (int c = 0; c < T; c++) { lo_at[c] = acc; acc += nl[c]; }
+                mid = s + acc;
+                for (int c = 0; c < T; c++) { hi_at[c] = acc; acc += nr[c]; }
+                parallel_chunks((size_t)n, 1 << 15, [&](int ch, size_t k0, size_t k1) {
+                    int a = lo_at[ch], b2 = hi_at[ch];
+                    for (size_t k = k0; k < k1; k++) {
+                        const SahRec& q = r[s + k];
+                        if (left(q)) tmp[s + a++] = q; else tmp[s + b2++] = q;
+                    }
+                });
+                parallel_chunks((size_t)n, 1 << 16, [&](int, size_t k0, size_t k1) {
+                    std::copy(tmp + s + k0, tmp + s + k1, r + s + k0);
+                });
+            } else {
+                mid = (int)(std::partition(r + s, r + e, left) - r);
+            }
         }
     } else if (n <= kSahMaxLeaf) {
         return -1;
@@ -409,28 +605,27 @@ int sah_split(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::vec
 }
 
 // Binned SAH BVH2 over [s, e), nodes appended depth first (node, left subtree, right subtree).
-int sah_rec(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::vector<int>& idx, int s, int e,
-            std::vector<SahNode2>& out) {
+int sah_rec(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out) {
     SahNode2 nd;
-    const int mid = sah_split(pb, pc, idx, s, e, nd);
+    const int mid = sah_split(r, tmp, s, e, nd);
     const int me = (int)out.size();
     out.push_back(nd);
     if (mid < 0) return me;
-    const int l = sah_rec(pb, pc, idx, s, mid, out);
-    const int r = sah_rec(pb, pc, idx, mid, e, out);
+    const int l = sah_rec(r, tmp, s, mid, out);
+    const int rr = sah_rec(r, tmp, mid, e, out);
     out[me].left = l;
-    out[me].right = r;
+    out[me].right = rr;
     return me;
 }
 
 // Same tree, the subtrees of the top `depth` levels (>= 64K triangles) built on their own threads
 // into their own node arrays and appended in sah_rec's depth-first order: the result is identical
-// to sah_rec's, node numbering included (1 M-triangle dragon on the GPU box's host: 247 -> 78 ms).  The two halves partition disjoint ranges of idx.
-int sah_rec_par(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::vector<int>& idx, int s, int e,
-                std::vector<SahNode2>& out, int depth) {
-    if (depth <= 0 || e - s < (1 << 16)) return sah_rec(pb, pc, idx, s, e, out);
+// to sah_rec's, node numbering included (1 M-triangle dragon on the GPU box's host: 247 -> 78 ms).
+// The two halves partition disjoint ranges of r (and of tmp).
+int sah_rec_par(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out, int depth) {
+    if (depth <= 0 || e - s < (1 << 16)) return sah_rec(r, tmp, s, e, out);
     SahNode2 nd;
-    const int mid = sah_split(pb, pc, idx, s, e, nd);
+    const int mid = sah_split(r, tmp, s, e, nd);
     const int me = (int)out.size();
     out.push_back(nd);
     if (mid < 0) return me;
@@ -438,13 +633,13 @@ int sah_rec_par(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::v
     std::exception_ptr err;
     std::thread t([&] {
         try {
-            sah_rec_par(pb, pc, idx, s, mid, L, depth - 1);
+            sah_rec_par(r, tmp, s, mid, L, depth - 1);
         } catch (...) {
             err = std::current_exception();
         }
     });
     try {
-        sah_rec_par(pb, pc, idx, mid, e, R, depth - 1);
+        sah_rec_par(r, tmp, mid, e, R, depth - 1);
     } catch (...) {
         t.join();
         throw;
@@ -464,33 +659,6 @@ int sah_rec_par(const std::vector<SahBox>& pb, const std::vector<V3>& pc, std::v
     return me;
 }
 
-// Host worker threads of the scene build: up to 16 (the GPU box's CPU share per GPU), chunks of
-// at least `grain` items.  f(chunk, begin, end) runs once per chunk; chunks are numbered in order,
-// so per-chunk partial results combine deterministically.  Exceptions reach the caller.
-inline int build_threads() {
-    static const int n = [] {
-        int t = (int)std::thread::hardware_concurrency();
-        if (const char* e = getenv("RTG_BUILD_THREADS")) t = atoi(e);
-        return std::max(1, std::min(16, t));
-    }();
-    return n;
-}
-template <class F>
-int parallel_chunks(size_t n, size_t grain, F&& f) {
-    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)build_threads(), (n + grain - 1) / std::max<size_t>(grain, 1)));
-    if (T <= 1) { if (n) f(0, (size_t)0, n); return 1; }
-    std::vector<std::thread> th;
-    std::vector<std::exception_ptr> err(T);
-    for (int c = 1; c < T; c++)
-        th.emplace_back([&, c] {
-            try { f(c, n * c / T, n * (c + 1) / T); } catch (...) { err[c] = std::current_exception(); }
-        });
-    try { f(0, (size_t)0, n / T); } catch (...) { err[0] = std::current_exception(); }
-    for (std::thread& t : th) t.join();
-    for (auto& e : err) if (e) std::rethrow_exception(e);
-    return T;
-}
-
 // Collapse the SAH BVH2 into 4-wide nodes: each node's slots are its children, the interior
 // slot with the largest surface area replaced by its own two children while slots are free.
 // Slot info: < 0 empty, 0 interior (ref = Node4 index), > 0 leaf of `info` triangles at ref
@@ -498,10 +666,17 @@ int parallel_chunks(size_t n, size_t grain, F&& f) {
 // overhang of a candidate beyond its triangle, rounded outwards), so the device walk needs no
 // parameter-space padding: a t-space pad of pad/|d_a| on every axis would stop pruning rays
 // with one small direction component.
-int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad, std::vector<Node4>& out) {
-    const int me = (int)out.size();
-    out.emplace_back();
-    int slot[4] = {bn[n].left, bn[n].right, -1, -1};
+// The slots of the 4-wide node over BVH2 node n (children expanded largest-area first) and their
+// widened boxes / leaf refs; interior slots get their ref from the caller.
+struct Collapsed {
+    int slot[4], used;
+    float lo[3][4], hi[3][4];
+    int ref[4], info[4];
+};
+Collapsed collapse_node(const std::vector<SahNode2>& bn, int n, int tri_base, float pad) {
+    Collapsed C;
+    int* slot = C.slot;
+    slot[0] = bn[n].left; slot[1] = bn[n].right; slot[2] = slot[3] = -1;
     int used = 2;
     while (used < 4) {
         int pick = -1;
@@ -516,8 +691,11 @@ int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad
         slot[pick] = bn[c].left;
         slot[used++] = bn[c].right;
     }
-    float lo[3][4], hi[3][4];
-    int ref[4], info[4];
+    C.used = used;
+    auto& lo = C.lo;
+    auto& hi = C.hi;
+    int* ref = C.ref;
+    int* info = C.info;
     for (int j = 0; j < 4; j++) {
         if (j >= used) {
             for (int z = 0; z < 3; z++) { lo[z][j] = 0.0f; hi[z][j] = 0.0f; }
@@ -532,9 +710,14 @@ int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad
         if (c.left < 0) { ref[j] = tri_base + c.start; info[j] = c.count; }
         else { ref[j] = 0; info[j] = 0; }
     }
-    for (int j = 0; j < used; j++)
-        if (bn[slot[j]].left >= 0) ref[j] = sah_collapse(bn, slot[j], tri_base, pad, out);
-    Node4& nd = out[me];
+    return C;
+}
+Node4 node4_of(const Collapsed& C) {
+    const auto& lo = C.lo;
+    const auto& hi = C.hi;
+    const int* ref = C.ref;
+    const int* info = C.info;
+    Node4 nd;
     nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
     nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
     nd.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
@@ -543,6 +726,50 @@ int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad
     nd.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
     nd.ref = make_int4(ref[0], ref[1], ref[2], ref[3]);
     nd.info = make_int4(info[0], info[1], info[2], info[3]);
+    return nd;
+}
+template <class V>
+int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad, V& out) {
+    const int me = (int)out.size();
+    out.emplace_back();
+    Collapsed C = collapse_node(bn, n, tri_base, pad);
+    for (int j = 0; j < C.used; j++)
+        if (bn[C.slot[j]].left >= 0) C.ref[j] = sah_collapse(bn, C.slot[j], tri_base, pad, out);
+    out[me] = node4_of(C);
+    return me;
+}
+// Same nodes in the same (depth-first) order, the subtrees of the top `depth` levels (>= 64K
+// triangles) collapsed on their own threads into their own arrays and appended with their interior
+// refs shifted.
+template <class V>
+int sah_collapse_par(const std::vector<SahNode2>& bn, int n, int tri_base, float pad, V& out, int depth) {
+    if (depth <= 0 || bn[n].count < (1 << 16)) return sah_collapse(bn, n, tri_base, pad, out);
+    const int me = (int)out.size();
+    out.emplace_back();
+    Collapsed C = collapse_node(bn, n, tri_base, pad);
+    V sub[4];
+    std::thread th[4];
+    std::exception_ptr err[4];
+    for (int j = 0; j < C.used; j++)
+        if (bn[C.slot[j]].left >= 0)
+            th[j] = std::thread([&, j] {
+                try { sah_collapse_par(bn, C.slot[j], tri_base, pad, sub[j], depth - 1); } catch (...) { err[j] = std::current_exception(); }
+            });
+    for (int j = 0; j < 4; j++) if (th[j].joinable()) th[j].join();
+    for (int j = 0; j < 4; j++) if (err[j]) std::rethrow_exception(err[j]);
+    for (int j = 0; j < C.used; j++) {
+        if (bn[C.slot[j]].left < 0) continue;
+        const int off = (int)out.size();
+        for (Node4 x : sub[j]) {
+            if (x.info.x == 0) x.ref.x += off;
+            if (x.info.y == 0) x.ref.y += off;
+            if (x.info.z == 0) x.ref.z += off;
+            if (x.info.w == 0) x.ref.w += off;
+            out.push_back(x);
+        }
+        C.ref[j] = off;                  // the subtree's root (its index 0)
+    }
+    out[me] = node4_of(C);
     return me;
 }
 
@@ -798,8 +1025,10 @@ struct DBuf {
     void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; used = 0; }
 };
 
-template <class T>
-int upload(DBuf& b, const std::vector<T>& v) {
+
+template <class V>
+int upload(DBuf& b, const V& v) {
+    using T = typename V::value_type;
     size_t n = std::max<size_t>(v.size(), 1) * sizeof(T);
     int rc = b.grow(n);
     if (rc) return rc;
@@ -1041,13 +1270,34 @@ int32_t rtg_scene_destroy(rtg_scene* s) {
 // Wall-clock laps of the scene build (rtg_build_stats phases).
 struct PhaseClock {
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-    double lap() {
+    double lap(const char* what = nullptr) {
         const auto n = std::chrono::steady_clock::now();
         const double ms = std::chrono::duration<double, std::milli>(n - t).count();
         t = n;
+        if (what && getenv("RTG_BUILD_TIMING")) fprintf(stderr, "[rtg] phase %-16s %7.2f ms\n", what, ms);
         return ms;
     }
 };
+
+// Triangle record of face f (1-based vertex indices pv[3f..3f+2]): a, a - b, a - c (the Cramer
+// operands of Triangle::bvhIntersect, src/Shape.cpp:297-316) and c - b.  With a - b, c - b gives
+// the flat normal (c - b) x (a - b) (src/Shape.cpp:327), so the shading of a flat triangle reads
+// this record only; the device formed cc - b itself before, and the two agree bit for bit only
+// because this is one IEEE f32 subtraction (no contraction can apply to a lone subtraction) on f32
+// components, which the static_assert pins.  Covered at run time by the flat, non-Triangle floor
+// mesh of the dragon scenes in the simple shading variant (test_gpu_fullsize.py band,
+// test_gpu_parity.py images).  p2.yzw is free for the caller (the traversal copy's reference
+// position, leaf start and gate flag).
+static TriGeom tri_geom(const std::vector<V3>& verts, const std::vector<int>& pv, size_t f) {
+    const V3 a = verts[pv[3 * f] - 1], b = verts[pv[3 * f + 1] - 1], c = verts[pv[3 * f + 2] - 1];
+    const V3 amb = a - b, amc = a - c, cmb = c - b;
+    static_assert(std::is_same<decltype(cmb.x), float>::value, "flat-normal c - b must be f32");
+    TriGeom tg;
+    tg.p0 = make_float4(a.x, a.y, a.z, amb.x);
+    tg.p1 = make_float4(amb.y, amb.z, amc.x, amc.y);
+    tg.p2 = make_float4(amc.z, cmb.x, cmb.y, cmb.z);
+    return tg;
+}
 
 static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     PhaseClock pc;
@@ -1105,17 +1355,17 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         V3 n = normalized(vn[i]);
         s->vnormals[3 * i] = n.x; s->vnormals[3 * i + 1] = n.y; s->vnormals[3 * i + 2] = n.z;
     }
-    bs.prep_ms += pc.lap();
+    bs.prep_ms += pc.lap("prep");
 
     // BVHs and device geometry
     std::vector<Geometry> geoms(d->num_objects);
-    std::vector<Node> dnodes;
-    std::vector<Node4> snodes;               // traversal trees (SAH, 4-wide)
+    hvec<Node> dnodes;
+    hvec<Node4> snodes;                      // traversal trees (SAH, 4-wide)
     std::vector<Node4q> qnodes;              // ... quantised (RTG_QNODES; uploaded instead of snodes)
-    std::vector<TriGeom> stris;              // their triangles, SAH leaf order (p2 = ref position / leaf / gated)
-    std::vector<float> gates;                // per reference position: its leaf's parent box
-    std::vector<TriGeom> tris;
-    std::vector<int4> primidx;
+    hvec<TriGeom> stris;                     // their triangles, SAH leaf order (p2 = ref position / leaf / gated)
+    hvec<float> gates;                       // per reference position: its leaf's parent box
+    hvec<TriGeom> tris;
+    hvec<int4> primidx;
     s->orig_prim.clear();
     s->bvh.assign(d->num_objects, ObjBVH());
     const float ieps = d->intersection_test_eps;
@@ -1123,7 +1373,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         const rtg_object_desc& o = d->objects[i];
         const std::vector<int>& pv = op[i].v;
         int np = (int)(pv.size() / 3);
-        std::vector<V3> centers(np), bmin(np), bmax(np);
+        hvec<V3> centers(np), bmin(np), bmax(np);
         std::vector<char> fin_chunk(std::max(build_threads(), 1), 1);
         parallel_chunks((size_t)np, 1 << 14, [&](int ch, size_t k0, size_t k1) {
             bool fin = true;
@@ -1154,10 +1404,33 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         // reference positions afterwards.  Any tree shape gives the same results (the total order
         // of candidates and the reachability gates), so it needs no reference order.
         const bool sah_try = o.type != RTG_OBJ_SPHERE && np >= 2 && all_finite && s->blas_mode != 1;
-        std::vector<SahBox> sah_box;
-        std::vector<V3> sah_ctr;
-        std::vector<int> sah_idx;
+        // the eps overhang of a candidate beyond its triangle (Triangle::bvhIntersect's t >= -eps):
+        // the traversal tree's boxes and the root window are widened by it (a max over the faces,
+        // so the evaluation order does not matter)
+        float obj_pad = 0.0f;
+        if (o.type != RTG_OBJ_SPHERE) {
+            std::vector<float> pad_chunk(build_threads(), 0.0f);
+            parallel_chunks((size_t)np, 1 << 14, [&](int ch, size_t k0, size_t k1) {
+                float padc = 0.0f;
+                for (size_t k = k0; k < k1; k++) {
+                    const V3 a = verts[pv[3 * k] - 1], b = verts[pv[3 * k + 1] - 1], c = verts[pv[3 * k + 2] - 1];
+                    const double e = (double)(ieps > 0 ? ieps : 0.0f);
+                    const double ext = e * ((double)vnorm(b - a) + (double)vnorm(c - a));
+                    padc = std::max(padc, (float)(ext * 1.02 + 1e-7));
+                }
+                pad_chunk[ch] = padc;
+            });
+            for (float x : pad_chunk) obj_pad = std::max(obj_pad, x);
+        }
+        hvec<SahRec> sah_rec_buf, sah_tmp;
+        hvec<int> sah_idx;
         std::vector<SahNode2> sah_bn;
+        // the SAH thread also collapses its tree to 4-wide nodes (leaf refs from tri_base0, the
+        // object's first traversal-order triangle) and forms the triangles' records in that order
+        // (p2.yzw, which need the reference tree, are filled after the join)
+        const int tri_base0 = (int)stris.size();
+        hvec<Node4> sah_nodes;
+        hvec<TriGeom> sah_tris;
         std::thread sah_thread;
         std::exception_ptr sah_err;
         struct Joiner {                    // the SAH thread never outlives this iteration
@@ -1165,20 +1438,36 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             ~Joiner() { if (t.joinable()) t.join(); }
         } sah_join{sah_thread};
         if (sah_try) {
-            sah_box.resize(np);
-            sah_ctr.resize(np);
+            sah_rec_buf.resize(np);
+            sah_tmp.resize(np);
             sah_idx.resize(np);
             parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
                 for (size_t f = k0; f < k1; f++) {
-                    for (int z = 0; z < 3; z++) { sah_box[f].lo[z] = comp(bmin[f], z); sah_box[f].hi[z] = comp(bmax[f], z); }
-                    sah_ctr[f] = v3(0.5f * (bmin[f].x + bmax[f].x), 0.5f * (bmin[f].y + bmax[f].y), 0.5f * (bmin[f].z + bmax[f].z));
-                    sah_idx[f] = (int)f;
+                    SahRec& q = sah_rec_buf[f];
+                    for (int z = 0; z < 3; z++) { q.lo[z] = comp(bmin[f], z); q.hi[z] = comp(bmax[f], z); }
+                    q.idx = (int)f;
+                    q.pad_ = 0;
                 }
             });
             sah_bn.reserve(2 * (size_t)np / kSahMaxLeaf + 16);
             sah_thread = std::thread([&] {
                 try {
-                    sah_rec_par(sah_box, sah_ctr, sah_idx, 0, np, sah_bn, 4);
+                    PhaseClock tc;
+                    sah_rec_par(sah_rec_buf.data(), sah_tmp.data(), 0, np, sah_bn, 4);
+                    parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
+                        for (size_t k = k0; k < k1; k++) sah_idx[k] = sah_rec_buf[k].idx;
+                    });
+                    tc.lap(" sah_tree (thread)");
+                    if (sah_bn[0].left >= 0) {
+                        sah_nodes.reserve((size_t)np / 2 + 16);
+                        sah_collapse_par(sah_bn, 0, tri_base0, obj_pad, sah_nodes, 3);
+                        tc.lap(" sah_collapse (thread)");
+                        sah_tris.resize(np);
+                        parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
+                            for (size_t k = k0; k < k1; k++) sah_tris[k] = tri_geom(verts, pv, (size_t)sah_idx[k]);
+                        });
+                        tc.lap(" sah_tris (thread)");
+                    }
                 } catch (...) {
                     sah_err = std::current_exception();
                 }
@@ -1188,7 +1477,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         ob.perm.resize(np);
         for (int k = 0; k < np; k++) ob.perm[k] = k;
         BuildCtx B{centers.data(), bmin.data(), bmax.data(), &ob.perm, &ob.nodes, {}};
-        bs.prep_ms += pc.lap();
+        bs.prep_ms += pc.lap("prep");
         auto tb0 = std::chrono::steady_clock::now();
         // non-finite centres / boxes: the GPU build does not model NaN folds
         const bool use_gpu = s->device >= 0 && o.type != RTG_OBJ_SPHERE && all_finite &&
@@ -1196,40 +1485,63 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         if (use_gpu) {
             GpuBvh gb;
             std::string err;
+            PhaseClock sub;
             if (gpu_build_bvh(&centers[0].x, &bmin[0].x, &bmax[0].x, np, gb, err, nullptr))
                 return fail(RTG_ERR_HIP, "GPU BVH build: " + err);
-            ob.perm = std::move(gb.perm);
-            // breadth-first -> the reference's pre-order numbering (node, left subtree, right subtree)
+            sub.lap(" gpu_build");
+            ob.perm.resize(np);
+            parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
+                std::copy(gb.perm.p + k0, gb.perm.p + k1, ob.perm.data() + k0);
+            });
+            // breadth-first -> the reference's pre-order numbering (node, left subtree, right
+            // subtree).  The build appends each depth's nodes after the previous depth's
+            // (gb.level_start), so subtree sizes come from one pass per depth, deepest first, and
+            // pre-order positions from one pass per depth, root first (pre[left] = pre[node] + 1,
+            // pre[right] = pre[left] + size[left]); each pass is parallel within its depth.
             const int nn = (int)gb.nodes.size();
-            std::vector<int> pre(nn, -1), stk;
-            ob.nodes.clear();
-            ob.nodes.reserve(nn);
-            if (nn > 0) stk.push_back(0);
-            while (!stk.empty()) {
-                const int id = stk.back();
-                stk.pop_back();
-                pre[id] = (int)ob.nodes.size();
-                HNode h;
-                h.left = gb.nodes[id].x; h.right = gb.nodes[id].y;     // fixed below
-                h.start = gb.nodes[id].z; h.end = gb.nodes[id].w;
-                for (int z = 0; z < 3; z++) { h.mn[z] = gb.box[6 * (size_t)id + z]; h.mx[z] = gb.box[6 * (size_t)id + 3 + z]; }
-                ob.nodes.push_back(h);
-                if (gb.nodes[id].y >= 0) stk.push_back(gb.nodes[id].y);
-                if (gb.nodes[id].x >= 0) stk.push_back(gb.nodes[id].x);
-            }
-            for (HNode& h : ob.nodes) {
-                if (h.left >= 0) h.left = pre[h.left];
-                if (h.right >= 0) h.right = pre[h.right];
-            }
+            hvec<int> pre(nn), sz(nn);
+            const std::vector<int>& ls = gb.level_start;
+            const int depths = (int)ls.size() - 1;
+            for (int dd = depths - 1; dd >= 0; dd--)
+                parallel_chunks((size_t)(ls[dd + 1] - ls[dd]), 1 << 14, [&](int, size_t k0, size_t k1) {
+                    for (size_t k = k0; k < k1; k++) {
+                        const int id = ls[dd] + (int)k;
+                        const int4 c = gb.nodes[id];
+                        sz[id] = 1 + (c.x >= 0 ? sz[c.x] : 0) + (c.y >= 0 ? sz[c.y] : 0);
+                    }
+                });
+            if (nn > 0) pre[0] = 0;
+            for (int dd = 0; dd < depths; dd++)
+                parallel_chunks((size_t)(ls[dd + 1] - ls[dd]), 1 << 14, [&](int, size_t k0, size_t k1) {
+                    for (size_t k = k0; k < k1; k++) {
+                        const int id = ls[dd] + (int)k;
+                        const int4 c = gb.nodes[id];
+                        if (c.x >= 0) pre[c.x] = pre[id] + 1;
+                        if (c.y >= 0) pre[c.y] = pre[id] + 1 + (c.x >= 0 ? sz[c.x] : 0);
+                    }
+                });
+            ob.nodes.resize(nn);
+            parallel_chunks((size_t)nn, 1 << 15, [&](int, size_t k0, size_t k1) {
+                for (size_t id = k0; id < k1; id++) {
+                    const int4 c = gb.nodes[id];
+                    HNode h;
+                    h.left = c.x >= 0 ? pre[c.x] : -1;
+                    h.right = c.y >= 0 ? pre[c.y] : -1;
+                    h.start = c.z; h.end = c.w;
+                    for (int z = 0; z < 3; z++) { h.mn[z] = gb.box[6 * id + z]; h.mx[z] = gb.box[6 * id + 3 + z]; }
+                    ob.nodes[pre[id]] = h;
+                }
+            });
             ob.root = nn > 0 ? 0 : -1;
             s->bvh_gpu_objects++;
+            sub.lap(" preorder");
         } else {
             ob.nodes.reserve(2 * (size_t)np + 1);
-            ob.root = construct(B, 0, np, 0, 0);
+            ob.root = construct_par(B, 0, np, 0, 0, 4);
         }
         const double bms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
         s->bvh_build_ms += bms;
-        bs.median_tree_ms += pc.lap();
+        bs.median_tree_ms += pc.lap("median_tree");
         if (getenv("RTG_BUILD_TIMING"))
             fprintf(stderr, "[rtg] object %d: %d prims, BVH %s %.1f ms\n", i, np, use_gpu ? "gpu" : "host", bms);
 
@@ -1250,54 +1562,33 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             g.radius = o.radius;
             g.center_index = o.center;
         }
-        // primitives in BVH order (chunks of positions in parallel; the ε-overhang pad is a max)
+        // primitives in BVH order (chunks of positions in parallel)
         const size_t pbase = tris.size();
         tris.resize(pbase + np);
         primidx.resize(pbase + np);
         s->orig_prim.resize(pbase + np);
-        std::vector<float> pad_chunk(build_threads(), 0.0f);
-        parallel_chunks((size_t)np, 1 << 14, [&](int ch, size_t k0, size_t k1) {
-          float padc = 0.0f;
+        parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
           for (size_t k = k0; k < k1; k++) {
-            int f = ob.perm[k];
+            const int f = ob.perm[k];
             TriGeom tg;
-            memset(&tg, 0, sizeof tg);
             int4 pi;
             if (o.type == RTG_OBJ_SPHERE) {
+                memset(&tg, 0, sizeof tg);
                 pi = make_int4(o.center, 0, 0, 0);
             } else {
-                int i1 = pv[3 * f], i2 = pv[3 * f + 1], i3 = pv[3 * f + 2];
-                V3 a = verts[i1 - 1], b = verts[i2 - 1], c = verts[i3 - 1];
-                V3 amb = a - b, amc = a - c, cmb = c - b;
-                tg.p0 = make_float4(a.x, a.y, a.z, amb.x);
-                tg.p1 = make_float4(amb.y, amb.z, amc.x, amc.y);
-                // c - b: with a - b the flat normal (c - b) x (a - b) of Triangle::bvhIntersect
-                // (src/Shape.cpp:327), so the shading of a flat triangle reads this record only
-                // (the traversal copy, stris, reuses p2.yzw).  The device formed cc - b itself
-                // before; the two agree bit for bit only because this is one IEEE f32 subtraction
-                // (no contraction can apply to a lone subtraction) on f32 components, which the
-                // static_assert pins.  Covered at run time by the flat, non-Triangle floor mesh of
-                // the dragon scenes in the simple shading variant (test_gpu_fullsize.py band,
-                // test_gpu_parity.py images).
-                static_assert(std::is_same<decltype(cmb.x), float>::value, "flat-normal c - b must be f32");
-                tg.p2 = make_float4(amc.z, cmb.x, cmb.y, cmb.z);
-                int smooth = (o.type == RTG_OBJ_TRIANGLE) ? 1 : o.smooth;   // Shape.cpp:262-276 quirk
-                pi = make_int4(i1, i2, i3, smooth);
-                double e = (double)(ieps > 0 ? ieps : 0.0f);
-                double ext = e * ((double)vnorm(b - a) + (double)vnorm(c - a));
-                padc = std::max(padc, (float)(ext * 1.02 + 1e-7));
+                tg = tri_geom(verts, pv, (size_t)f);
+                const int smooth = (o.type == RTG_OBJ_TRIANGLE) ? 1 : o.smooth;   // Shape.cpp:262-276 quirk
+                pi = make_int4(pv[3 * f], pv[3 * f + 1], pv[3 * f + 2], smooth);
             }
             tris[pbase + k] = tg;
             primidx[pbase + k] = pi;
             s->orig_prim[pbase + k] = f;
           }
-          pad_chunk[ch] = padc;
         });
-        float pad = 0.0f;
-        for (float x : pad_chunk) pad = std::max(pad, x);
+        const float pad = obj_pad;
         g.prune_pad = pad;
         // linearise interior nodes (pre-order) into child-box nodes
-        const std::vector<HNode>& hn = ob.nodes;
+        const hvec<HNode>& hn = ob.nodes;
         std::vector<int> dev_index(hn.size(), -1);
         int node_base = (int)dnodes.size();
         int cnt = 0;
@@ -1361,31 +1652,57 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         // reference-tree walk)
         g.sah_base = -1;
         const bool sah_ok = sah_try && ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0);
-        bs.records_ms += pc.lap();
+        bs.records_ms += pc.lap("records");
+        PhaseClock sub;
         if (sah_thread.joinable()) sah_thread.join();
         if (sah_err) std::rethrow_exception(sah_err);
+        sub.lap(" sah_join_wait");
         if (sah_ok) {
             const std::vector<SahNode2>& bn = sah_bn;
             if (bn[0].left >= 0) {
-                // SAH leaf order: face index -> reference position (inverse of the median tree's perm)
+                // SAH leaf order: face index -> reference position (inverse of the median tree's
+                // perm); the thread's records get their reference position, leaf and gate flag
                 std::vector<int> pos_of(np);
-                for (int k = 0; k < np; k++) pos_of[ob.perm[k]] = k;
+                parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
+                    for (size_t k = k0; k < k1; k++) pos_of[ob.perm[k]] = (int)k;
+                });
                 const int tri_base = (int)stris.size();
-                stris.resize((size_t)tri_base + np);
+                if (tri_base != tri_base0) return fail(RTG_ERR_UNSUPPORTED, "internal: traversal-tree triangle base");
                 parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
                     for (size_t k = k0; k < k1; k++) {
                         const int r = pos_of[sah_idx[k]];
-                        TriGeom t = tris[g.prim_base + r];
+                        TriGeom& t = sah_tris[k];
                         const int pos = g.prim_base + r, gt = gated[r];
                         memcpy(&t.p2.y, &pos, 4);
                         memcpy(&t.p2.z, &leaf_start[r], 4);
                         memcpy(&t.p2.w, &gt, 4);
-                        stris[tri_base + k] = t;
                     }
                 });
+                if (stris.empty()) stris = std::move(sah_tris);
+                else stris.insert(stris.end(), sah_tris.begin(), sah_tris.end());
+                sub.lap(" stris");
+                // the thread's nodes, interior refs shifted to this mesh's first node
                 const size_t first = snodes.size();
-                g.sah_base = sah_collapse(bn, 0, tri_base, pad, snodes);
-                if (snodes.size() - first == 1 && np <= kFlatMaxPrims) { g.flat_first = tri_base; g.flat_count = np; }
+                const size_t nsub = sah_nodes.size();
+                const int off = (int)first;
+                if (first == 0) {
+                    snodes = std::move(sah_nodes);
+                } else {
+                    snodes.resize(first + sah_nodes.size());
+                    parallel_chunks(sah_nodes.size(), 1 << 15, [&](int, size_t k0, size_t k1) {
+                        for (size_t k = k0; k < k1; k++) {
+                            Node4 x = sah_nodes[k];
+                            if (x.info.x == 0) x.ref.x += off;
+                            if (x.info.y == 0) x.ref.y += off;
+                            if (x.info.z == 0) x.ref.z += off;
+                            if (x.info.w == 0) x.ref.w += off;
+                            snodes[first + k] = x;
+                        }
+                    });
+                }
+                g.sah_base = off;
+                sub.lap(" nodes");
+                if (nsub == 1 && np <= kFlatMaxPrims) { g.flat_first = tri_base; g.flat_count = np; }
                 if (RTG_QNODES) {
                     // the quantised copy; a node that cannot be quantised drops the mesh's tree
                     bool qok = true;
@@ -1404,7 +1721,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 }
             }
         }
-        bs.traversal_tree_ms += pc.lap();
+        bs.traversal_tree_ms += pc.lap("traversal_tree");
         if (ob.root < 0) {
             g.node_base = -1; g.root_leaf_start = g.prim_base; g.root_leaf_count = -1;
         } else if (hn[ob.root].left < 0 && hn[ob.root].right < 0) {
@@ -1626,7 +1943,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         s->num_emit++;
     }
 
-    bs.top_level_ms += pc.lap();
+    bs.top_level_ms += pc.lap("top_level");
     if (s->device < 0) return RTG_OK;   // host-only build (introspection / CPU tests)
     std::vector<float> vflat(d->vertices, d->vertices + 3 * (size_t)nv);
     std::vector<float> tcflat;
@@ -1643,7 +1960,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         return rc;
     bs.upload_bytes = 0;
     for (DBuf* b : scene_buffers(s)) bs.upload_bytes += b->used;
-    bs.upload_ms += pc.lap();
+    bs.upload_ms += pc.lap("upload");
 
     SceneView& sv = s->sv;
     bind_view(s);
@@ -1736,6 +2053,34 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         if (const char* e = getenv("RTG_SAH")) s->blas_mode = atoi(e) == 0 ? 1 : 0;
         if (const char* e = getenv("RTG_TLAS")) s->tlas_mode = atoi(e) == 0 ? 1 : 2;
         s->bst.validate_ms = validate_ms;
+        // The HIP runtime's first host-to-device copy in a process costs 90-145 ms (its copy path is
+        // set up then: scripts/hip_init_probe.py on MI355X), even after the device context exists,
+        // and the first launch from a code object a few ms more.  Start both now on their own
+        // thread (a 256-byte pinned copy, one empty launch), so that they overlap the
+        // host part of the build (descriptor checks, primitive boxes, the traversal tree's SAH build)
+        // instead of stalling the first upload.  Errors are left to the build's own calls.
+        std::thread warm;
+        struct WarmJoin {
+            std::thread& t;
+            ~WarmJoin() { if (t.joinable()) t.join(); }
+        } warm_join{warm};
+        if (device >= 0)
+            warm = std::thread([device] {
+                if (hipSetDevice(device) != hipSuccess) return;
+                void* h = nullptr;
+                void* dptr = nullptr;
+                if (hipHostMalloc(&h, 256, hipHostMallocDefault) != hipSuccess) return;
+                memset(h, 0, 256);
+                if (hipMalloc(&dptr, 256) == hipSuccess) {
+                    (void)hipMemcpy(dptr, h, 256, hipMemcpyHostToDevice);
+                    (void)hipFree(dptr);
+                }
+                (void)hipHostFree(h);
+                // and the GPU build's code object (loading the render kernels' here as well delayed
+                // the build without shortening the first frame)
+                gpu_bvh_warm(nullptr);
+                (void)hipStreamSynchronize(nullptr);
+            });
         rc = build_scene(s, desc);
         if (rc) {
             scene_free(s);

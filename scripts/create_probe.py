@@ -1,5 +1,5 @@
 """Scene-creation phases of the dragon1m scene, created several times in one process (the first
-includes one-time HIP / code-object set-up).  usage: python scripts/create_probe.py [times]"""
+includes one-time HIP / code-object set-up).  usage: python scripts/create_probe.py [times] [auto|host|gpu]"""
 import json
 import os
 import sys
@@ -12,13 +12,14 @@ import rtg  # noqa: E402
 from rtg import scenegen  # noqa: E402
 
 times = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+builder = {"auto": 0, "host": 1, "gpu": 2}[sys.argv[2] if len(sys.argv) > 2 else "auto"]
 sc = scenegen.dragon1m(1920, 1080, spp=64)
 torch.cuda.init()
 for k in range(times):
     t0 = time.perf_counter()
-    r = rtg.Renderer(sc, 0)
+    r = rtg.Renderer(sc, 0, bvh_builder=builder)
     ms = (time.perf_counter() - t0) * 1e3
     bs = r.build_stats()
-    print(json.dumps({"create": k, "wall_ms": round(ms, 1),
+    print(json.dumps({"create": k, "builder": builder, "wall_ms": round(ms, 1),
                       **{q: round(v, 1) if isinstance(v, float) else v for q, v in bs.items()}}), flush=True)
     r.close()
