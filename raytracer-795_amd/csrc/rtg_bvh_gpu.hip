@@ -361,7 +361,6 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
         if (n >= kBigNode) hipLaunchKernelGGL(k_box_big, dim3(1), dim3(256), 0, st, big.p, cnt.p, nodes.p, perm.p, lo3.p, hi3.p, box.p);
         else hipLaunchKernelGGL(k_box_small, dim3(1), dim3(64), 0, st, nodes.p, 0, 1, perm.p, lo3.p, hi3.p, box.p);
     }
-    out.level_start.assign(1, 0);
     int S = 0;
     if (n >= 2) {
         Seg s0; s0.start = 0; s0.end = n; s0.node = 0; s0.off = 0;
@@ -440,14 +439,12 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
                                    box.p);
         }
         BVH_TRY(hipGetLastError());
-        out.level_start.push_back(num_nodes);   // depth + 1 starts here
         num_nodes += new_nodes;
         std::swap(segs.p, next.p);
         std::swap(segs.cap, next.cap);
         S = S_next;
     }
     lap("levels");
-    out.level_start.push_back(num_nodes);
     BVH_TRY(out.perm.alloc(n));
     BVH_TRY(out.nodes.alloc(num_nodes));
     BVH_TRY(out.box.alloc(6 * (size_t)num_nodes));

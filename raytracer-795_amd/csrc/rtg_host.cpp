@@ -270,8 +270,10 @@ struct HNode {            // pre-order node of the reference tree
 
 struct ObjBVH {
     hvec<int> perm;               // BVH position -> original prim index
-    hvec<HNode> nodes;            // pre-order
+    hvec<HNode> nodes;            // pre-order (host build) or breadth-first (GPU build, bfs)
     int root = -1;
+    bool bfs = false;             // nodes in the GPU build's breadth-first order (root 0, children after
+                                  // their parent); rtg_scene_object_bvh reports the pre-order
 };
 
 struct BuildCtx {
@@ -1493,48 +1495,24 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
                 std::copy(gb.perm.p + k0, gb.perm.p + k1, ob.perm.data() + k0);
             });
-            // breadth-first -> the reference's pre-order numbering (node, left subtree, right
-            // subtree).  The build appends each depth's nodes after the previous depth's
-            // (gb.level_start), so subtree sizes come from one pass per depth, deepest first, and
-            // pre-order positions from one pass per depth, root first (pre[left] = pre[node] + 1,
-            // pre[right] = pre[left] + size[left]); each pass is parallel within its depth.
+            // the nodes stay in the build's breadth-first order: the device records below number
+            // the interior nodes in any order (they follow child links), and only the introspection
+            // call needs the reference's pre-order (rtg_scene_object_bvh converts)
             const int nn = (int)gb.nodes.size();
-            hvec<int> pre(nn), sz(nn);
-            const std::vector<int>& ls = gb.level_start;
-            const int depths = (int)ls.size() - 1;
-            for (int dd = depths - 1; dd >= 0; dd--)
-                parallel_chunks((size_t)(ls[dd + 1] - ls[dd]), 1 << 14, [&](int, size_t k0, size_t k1) {
-                    for (size_t k = k0; k < k1; k++) {
-                        const int id = ls[dd] + (int)k;
-                        const int4 c = gb.nodes[id];
-                        sz[id] = 1 + (c.x >= 0 ? sz[c.x] : 0) + (c.y >= 0 ? sz[c.y] : 0);
-                    }
-                });
-            if (nn > 0) pre[0] = 0;
-            for (int dd = 0; dd < depths; dd++)
-                parallel_chunks((size_t)(ls[dd + 1] - ls[dd]), 1 << 14, [&](int, size_t k0, size_t k1) {
-                    for (size_t k = k0; k < k1; k++) {
-                        const int id = ls[dd] + (int)k;
-                        const int4 c = gb.nodes[id];
-                        if (c.x >= 0) pre[c.x] = pre[id] + 1;
-                        if (c.y >= 0) pre[c.y] = pre[id] + 1 + (c.x >= 0 ? sz[c.x] : 0);
-                    }
-                });
             ob.nodes.resize(nn);
             parallel_chunks((size_t)nn, 1 << 15, [&](int, size_t k0, size_t k1) {
                 for (size_t id = k0; id < k1; id++) {
                     const int4 c = gb.nodes[id];
                     HNode h;
-                    h.left = c.x >= 0 ? pre[c.x] : -1;
-                    h.right = c.y >= 0 ? pre[c.y] : -1;
-                    h.start = c.z; h.end = c.w;
+                    h.left = c.x; h.right = c.y; h.start = c.z; h.end = c.w;
                     for (int z = 0; z < 3; z++) { h.mn[z] = gb.box[6 * id + z]; h.mx[z] = gb.box[6 * id + 3 + z]; }
-                    ob.nodes[pre[id]] = h;
+                    ob.nodes[id] = h;
                 }
             });
+            ob.bfs = true;
             ob.root = nn > 0 ? 0 : -1;
             s->bvh_gpu_objects++;
-            sub.lap(" preorder");
+            sub.lap(" nodes");
         } else {
             ob.nodes.reserve(2 * (size_t)np + 1);
             ob.root = construct_par(B, 0, np, 0, 0, 4);
@@ -1587,13 +1565,24 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         });
         const float pad = obj_pad;
         g.prune_pad = pad;
-        // linearise interior nodes (pre-order) into child-box nodes
+        // linearise interior nodes (in the tree's node order) into child-box nodes: per-chunk
+        // interior counts, then every chunk numbers its own interior nodes from its offset
         const hvec<HNode>& hn = ob.nodes;
-        std::vector<int> dev_index(hn.size(), -1);
-        int node_base = (int)dnodes.size();
-        int cnt = 0;
-        for (size_t k = 0; k < hn.size(); k++)
-            if (hn[k].left >= 0 || hn[k].right >= 0) dev_index[k] = node_base + cnt++;
+        hvec<int> dev_index(hn.size());
+        const int node_base = (int)dnodes.size();
+        std::vector<int> chunk_cnt(build_threads() + 1, 0);
+        const int TN = parallel_chunks(hn.size(), 1 << 15, [&](int ch, size_t k0, size_t k1) {
+            int c = 0;
+            for (size_t k = k0; k < k1; k++) c += (hn[k].left >= 0 || hn[k].right >= 0);
+            chunk_cnt[ch] = c;
+        });
+        std::vector<int> chunk_off(TN + 1, node_base);
+        for (int c = 0; c < TN; c++) chunk_off[c + 1] = chunk_off[c] + chunk_cnt[c];
+        const int cnt = chunk_off[TN] - node_base;
+        parallel_chunks(hn.size(), 1 << 15, [&](int ch, size_t k0, size_t k1) {
+            int at = chunk_off[ch];
+            for (size_t k = k0; k < k1; k++) dev_index[k] = (hn[k].left >= 0 || hn[k].right >= 0) ? at++ : -1;
+        });
         dnodes.resize(node_base + cnt);
         parallel_chunks(hn.size(), 1 << 15, [&](int, size_t k0, size_t k1) {
           for (size_t k = k0; k < k1; k++) {
@@ -1626,7 +1615,10 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         });
         // reference leaf of every position: its first position (tie order) and the box of the
         // interior node above it, which gates it (none under the root: closest_hit tests the root)
-        gates.resize(6 * (size_t)(g.prim_base + np), 0.0f);
+        gates.resize(6 * (size_t)(g.prim_base + np));
+        parallel_chunks(6 * (size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
+            std::fill(gates.begin() + 6 * (size_t)g.prim_base + k0, gates.begin() + 6 * (size_t)g.prim_base + k1, 0.0f);
+        });
         std::vector<int> leaf_start(np, 0);
         std::vector<char> gated(np, 0);
         if (ob.root >= 0 && hn[ob.root].left < 0 && hn[ob.root].right < 0)
@@ -2946,8 +2938,26 @@ int32_t rtg_scene_object_bvh(const rtg_scene* s, int32_t object, int32_t* num_pr
         if (num_prims) *num_prims = (int)b.perm.size();
         if (num_nodes) *num_nodes = (int)b.nodes.size();
         if (perm) memcpy(perm, b.perm.data(), sizeof(int) * b.perm.size());
+        // pre-order (node, left subtree, right subtree): a GPU-built tree is stored breadth-first
+        std::vector<int> order, pre;
+        if (b.bfs && !b.nodes.empty()) {
+            pre.assign(b.nodes.size(), -1);
+            std::vector<int> stk{b.root};
+            while (!stk.empty()) {
+                const int id = stk.back();
+                stk.pop_back();
+                pre[id] = (int)order.size();
+                order.push_back(id);
+                if (b.nodes[id].right >= 0) stk.push_back(b.nodes[id].right);
+                if (b.nodes[id].left >= 0) stk.push_back(b.nodes[id].left);
+            }
+        }
         for (size_t k = 0; k < b.nodes.size(); k++) {
-            const HNode& h = b.nodes[k];
+            HNode h = b.nodes[b.bfs ? order[k] : k];
+            if (b.bfs) {
+                if (h.left >= 0) h.left = pre[h.left];
+                if (h.right >= 0) h.right = pre[h.right];
+            }
             if (nodes) { nodes[4 * k] = h.left; nodes[4 * k + 1] = h.right; nodes[4 * k + 2] = h.start; nodes[4 * k + 3] = h.end; }
             if (boxes) for (int z = 0; z < 3; z++) { boxes[6 * k + z] = h.mn[z]; boxes[6 * k + 3 + z] = h.mx[z]; }
         }

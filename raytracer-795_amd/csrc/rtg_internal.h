@@ -484,7 +484,6 @@ struct GpuBvh {
     PinnedBuf<int> perm;
     PinnedBuf<int4> nodes;
     PinnedBuf<float> box;
-    std::vector<int> level_start;   // first node of each depth (the last entry = the node count)
     int root = -1;
 };
 int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, int n, GpuBvh& out, std::string& err,
