@@ -233,6 +233,8 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
             # finding the blocker vs proving it nearest (Light::IsShadow, src/Light.cpp:188-204)
             out["k_shadow"]["queries"]["blocked_steps_split"] = {
                 "steps_before_blocker_per_blocked": round(st_stats["shadow_blocked_steps_before"] / b, 3),
+                "wave_min_steps_before_blocker_per_blocked": round(
+                    st_stats.get("shadow_blocked_steps_before_wavemin", 0) / b, 3),
                 "steps_after_blocker_per_blocked": round(
                     (st_stats["shadow_blocked_steps"] - st_stats["shadow_blocked_steps_before"]) / b, 3),
                 "bins": ["0", "1", "2", "3-4", "5-8", "9-16", "17-32", ">32"],

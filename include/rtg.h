@@ -310,6 +310,9 @@ typedef struct rtg_render_stats {
     uint64_t shadow_hist_before[8];
     uint64_t shadow_hist_after[8];
     uint64_t shadow_blocked_steps_before;
+    /* ... and the same sum with each blocked query's steps before replaced by the fewest any blocked
+       query of its wave took (what sharing the first blocker found in a wave could save at most) */
+    uint64_t shadow_blocked_steps_before_wavemin;
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */

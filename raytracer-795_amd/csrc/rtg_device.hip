@@ -2353,6 +2353,10 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             atomicAdd(&ctr->shadow_hist_after[bin(after)], 1ull);
             atomicAdd(&ctr->shadow_blocked_steps_before, (unsigned long long)before);
         }
+        // the fewest steps before its blocker any blocked query of this wave took
+        unsigned wmin = was_blocked ? st.win_step : 0xFFFFFFFFu;
+        for (int off = 32; off > 0; off >>= 1) wmin = min(wmin, (unsigned)__shfl_xor((int)wmin, off));
+        unsigned long long wm = was_blocked ? (unsigned long long)wmin : 0ull;
         unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries;
         unsigned long long bq = was_blocked ? 1ull : 0ull, bs = was_blocked ? st.steps : 0ull,
                            bt = was_blocked ? st.tris : 0ull;
@@ -2366,6 +2370,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             bq += __shfl_down(bq, off);
             bs += __shfl_down(bs, off);
             bt += __shfl_down(bt, off);
+            wm += __shfl_down(wm, off);
             mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
         }
         if ((threadIdx.x & 63) == 0) {
@@ -2376,6 +2381,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             atomicAdd(&ctr->shadow_blocked, bq);
             atomicAdd(&ctr->shadow_blocked_steps, bs);
             atomicAdd(&ctr->shadow_blocked_tris, bt);
+            atomicAdd(&ctr->shadow_blocked_steps_before_wavemin, wm);
             atomicAdd(&ctr->shadow_entry_visits, ne);
             atomicAdd(&ctr->shadow_entry_slots, 64ull * mc);
         }

@@ -2726,6 +2726,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         stt.shadow_hist_after[b] = ctr.shadow_hist_after[b];
     }
     stt.shadow_blocked_steps_before = ctr.shadow_blocked_steps_before;
+    stt.shadow_blocked_steps_before_wavemin = ctr.shadow_blocked_steps_before_wavemin;
     stt.devices = 1;
     s->stats = stt;
     return RTG_OK;

@@ -377,6 +377,7 @@ struct Counters {
     // blocked shadow queries: histograms (bins 0, 1, 2, 3-4, 5-8, 9-16, 17-32, >32) of the node steps
     // taken before the blocker was accepted and after it, and the summed steps before
     unsigned long long shadow_hist_before[8], shadow_hist_after[8], shadow_blocked_steps_before;
+    unsigned long long shadow_blocked_steps_before_wavemin;
 };
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------

@@ -204,6 +204,7 @@ void add_stats(rtg_render_stats& a, const rtg_render_stats& b) {
         a.shadow_hist_after[k] += b.shadow_hist_after[k];
     }
     a.shadow_blocked_steps_before += b.shadow_blocked_steps_before;
+    a.shadow_blocked_steps_before_wavemin += b.shadow_blocked_steps_before_wavemin;
     a.resolve_ms += b.resolve_ms;
     a.accumulate_ms += b.accumulate_ms;
     a.resolve_launches += b.resolve_launches;

@@ -129,7 +129,8 @@ class RenderStats(C.Structure):
                 ("trace_entry_visits", C.c_uint64), ("trace_entry_slots", C.c_uint64),
                 ("shadow_entry_visits", C.c_uint64), ("shadow_entry_slots", C.c_uint64),
                 ("shadow_hist_before", C.c_uint64 * 8), ("shadow_hist_after", C.c_uint64 * 8),
-                ("shadow_blocked_steps_before", C.c_uint64)]
+                ("shadow_blocked_steps_before", C.c_uint64),
+                ("shadow_blocked_steps_before_wavemin", C.c_uint64)]
 
 RTG_COMM_ID_BYTES = 128
 

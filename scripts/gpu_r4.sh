@@ -34,9 +34,12 @@ for step in "$@"; do
     eb:*) IFS=: read -r _ kv wl <<< "$step"; name="eb_${kv//=/_}_$wl"
           run $name 300 env $kv python3 bench.py --no-cpu --workload $wl ;;
     lib:*) IFS=: read -r _ lib wl <<< "$step"; run lib_${lib}_$wl 300 env RTG_LIBRARY=raytracer-795_amd/rtg/$lib.so python3 bench.py --no-cpu --workload $wl ;;
-    shardenv:*) IFS=: read -r _ kv <<< "$step"; run shard_${kv//=/_} 300 env $kv python3 scripts/shard_probe.py 1 8 ;;
+    shardenv:*) IFS=: read -r _ kv <<< "$step"; n=${kv//=/_}; run shard_${n//,/_} 300 env ${kv//,/ } python3 scripts/shard_probe.py 1 8 ;;
     kt_*) wl=${step#kt_}; run $step 300 rocprofv3 --kernel-trace --stats -d $D/$step -o kt --output-format csv -- python3 scripts/tl_probe.py $wl 2
           python3 scripts/tl_util.py $(ls $D/$step/*kernel_trace.csv | head -1) > $D/${step}_util.txt; cat $D/${step}_util.txt ;;
+    ktshardenv:*) IFS=: read -r _ kv wl <<< "$step"; name="ktshard_${kv//=/_}_$wl"
+          run $name 300 env $kv rocprofv3 --kernel-trace --stats -d $D/$name -o kt --output-format csv -- python3 scripts/tl_probe.py $wl 3 0 8
+          python3 scripts/tl_util.py $(ls $D/$name/*kernel_trace.csv | head -1) > $D/${name}_util.txt; cat $D/${name}_util.txt ;;
     ktshard_*) wl=${step#ktshard_}; run $step 300 rocprofv3 --kernel-trace --stats -d $D/$step -o kt --output-format csv -- python3 scripts/tl_probe.py $wl 3 0 8
           python3 scripts/tl_util.py $(ls $D/$step/*kernel_trace.csv | head -1) > $D/${step}_util.txt; cat $D/${step}_util.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
