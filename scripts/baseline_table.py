@@ -17,12 +17,14 @@ def row(d):
     par = f"rows {p['rows'][0]}–{p['rows'][1]}: {p['differing']} differing" if p else "—"
     e = d["end_to_end_ms"]
     name = c["workload"].split(":")[0]
+    again = e.get("scene_create_again")
+    create = f"{e['scene_create']:.0f}" + (f" / {again['ms']:.0f}" if again else "")
     return (f"| {name} | {c['spp']} | {d['ms_per_step']:.2f} | {d['value']:,.0f} | {d['primary_msamples_s']:,.0f} | "
-            f"{d['ms_per_frame_to_host']:.2f} | {e['scene_create']:.0f} | {e['first_frame_to_host']:.0f} | {hbm} | {par} |")
+            f"{d['ms_per_frame_to_host']:.2f} | {create} | {e['first_frame_to_host']:.0f} | {hbm} | {par} |")
 
 
 def main():
-    print("| config (workload) | spp | ms/frame | Mray/s | primary Msamples/s | ms/frame incl. D2H | scene create ms "
+    print("| config (workload) | spp | ms/frame | Mray/s | primary Msamples/s | ms/frame incl. D2H | scene create ms (first / again) "
           "| first frame incl. D2H ms | frame HBM GB/s (frac of 8 TB/s) | parity vs oracle |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     for f in sys.argv[1:]:
