@@ -122,11 +122,19 @@ DEV float stdmin(float a, float b) { return (b < a) ? b : a; }
 DEV float vget(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 
 // transcendental convention: (float) of the double-precision function
+#if defined(RTG_TIMING_FAST_TRIG)   // timing experiment only: single-precision libm (NOT bit-exact)
+DEV float f_acos(float x) { return acosf(x); }
+DEV float f_atan2(float y, float x) { return atan2f(y, x); }
+DEV float f_cos(float x) { return cosf(x); }
+DEV float f_sin(float x) { return sinf(x); }
+DEV float f_exp(float x) { return expf(x); }
+#else
 DEV float f_acos(float x) { return (float)acos((double)x); }
 DEV float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 DEV float f_cos(float x) { return (float)cos((double)x); }
 DEV float f_sin(float x) { return (float)sin((double)x); }
 DEV float f_exp(float x) { return (float)exp((double)x); }
+#endif
 // std::pow(float, int) == (float)pow(double, double).  Integer exponent by binary powering in
 // double: within ~log2(n) double ulps of the exact power, so the float result is the
 // correctly rounded one except within ~1e-15 of a float rounding boundary.
