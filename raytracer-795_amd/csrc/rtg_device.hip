@@ -58,6 +58,11 @@ namespace rtg {
 #ifndef RTG_ROOT_WINDOW
 #define RTG_ROOT_WINDOW 1
 #endif
+// Triangle tests reject a candidate beyond the walk's parameter window (tri_test's thi) before
+// the barycentric determinants and the exact divisions (round 4).
+#ifndef RTG_TRI_WINDOW
+#define RTG_TRI_WINDOW 1
+#endif
 // Object-light shadow queries bounded where the blocking test stops being satisfiable
 // (emit_shadow_tmax) instead of just beyond the light.
 #ifndef RTG_EMIT_TMAX
@@ -122,19 +127,11 @@ DEV float stdmin(float a, float b) { return (b < a) ? b : a; }
 DEV float vget(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 
 // transcendental convention: (float) of the double-precision function
-#if defined(RTG_TIMING_FAST_TRIG)   // timing experiment only: single-precision libm (NOT bit-exact)
-DEV float f_acos(float x) { return acosf(x); }
-DEV float f_atan2(float y, float x) { return atan2f(y, x); }
-DEV float f_cos(float x) { return cosf(x); }
-DEV float f_sin(float x) { return sinf(x); }
-DEV float f_exp(float x) { return expf(x); }
-#else
 DEV float f_acos(float x) { return (float)acos((double)x); }
 DEV float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 DEV float f_cos(float x) { return (float)cos((double)x); }
 DEV float f_sin(float x) { return (float)sin((double)x); }
 DEV float f_exp(float x) { return (float)exp((double)x); }
-#endif
 // std::pow(float, int) == (float)pow(double, double).  Integer exponent by binary powering in
 // double: within ~log2(n) double ulps of the exact power, so the float result is the
 // correctly rounded one except within ~1e-15 of a float rounding boundary.
@@ -276,26 +273,42 @@ struct Cand {           // Triangle::bvhIntersect acceptance + point (src/Shape.
     float beta, gamma, t;
     f3 p;
 };
-DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps) {
+// thi (the caller's parameter window, RTG_TRI_WINDOW): a candidate whose t lies beyond it cannot
+// become the object's winner that matters -- the same bound the traversal's slot boxes are pruned
+// with (visit_object) -- so it may be rejected as well; INFINITY keeps every candidate.
+DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps, float thi = INFINITY) {
     f3 a = mk(g.p0.x, g.p0.y, g.p0.z);
     f3 amb = mk(g.p0.w, g.p1.x, g.p1.y);
     f3 amc = mk(g.p1.z, g.p1.w, g.p2.x);
     f3 amo = a - o;
     Cand c;
     float det = det3(amb, amc, d);
-    float nb = det3(amo, amc, d), ng = det3(amb, amo, d), nt = det3(amb, amc, amo);
+    float nt = det3(amb, amc, amo);
     // Fast rejection: quotients formed with v_rcp_f32 (1 ulp) lie within 2^-21 (relative) of
     // the correctly rounded ones, so a quotient that misses the acceptance bounds by more than
     // 2^-20 of its magnitude is rejected by the exact test too.  Everything else (and any
     // det outside [1e-30, 1e30] or non-finite operand, whose comparisons come out false)
-    // takes the exact divisions below.
+    // takes the exact divisions below.  The ray parameter is tested first, against
+    // [-eps, thi]: a candidate behind the origin or beyond the window costs two determinants,
+    // not four (round 4).
     const float ad = fabsf(det);
-    if (ad >= 1e-30f && ad <= 1e30f) {
-        const float r = __builtin_amdgcn_rcpf(det);
-        const float bq = nb * r, gq = ng * r, tq = nt * r;
-        const float m = 9.5367431640625e-7f;   // 2^-20
-        if (tq < (-eps - fabsf(tq) * m) - 1e-37f || bq < (-eps - fabsf(bq) * m) - 1e-37f ||
-            gq < (-eps - fabsf(gq) * m) - 1e-37f || bq + gq > (1.0f + (fabsf(bq) + fabsf(gq)) * (2.0f * m)) + m) {
+    const bool fastq = ad >= 1e-30f && ad <= 1e30f;
+    const float r = __builtin_amdgcn_rcpf(det);
+    const float m = 9.5367431640625e-7f;   // 2^-20
+    if (fastq) {
+        const float tq = nt * r;
+        if (tq < (-eps - fabsf(tq) * m) - 1e-37f || tq > (thi + fabsf(tq) * m) + 1e-37f) {
+            c.ok = false;
+            c.beta = c.gamma = c.t = 0.0f;
+            c.p = o;
+            return c;
+        }
+    }
+    float nb = det3(amo, amc, d), ng = det3(amb, amo, d);
+    if (fastq) {
+        const float bq = nb * r, gq = ng * r;
+        if (bq < (-eps - fabsf(bq) * m) - 1e-37f || gq < (-eps - fabsf(gq) * m) - 1e-37f ||
+            bq + gq > (1.0f + (fabsf(bq) + fabsf(gq)) * (2.0f * m)) + m) {
             c.ok = false;
             c.beta = c.gamma = c.t = 0.0f;
             c.p = o;
@@ -473,7 +486,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
         auto test_prim = [&](const TriGeom& tg, int k, int start) {
             if (STATS) st.tris++;
-            Cand c = tri_test(tg, o2, d2, eps);
+            Cand c = tri_test(tg, o2, d2, eps, RTG_TRI_WINDOW ? thi : INFINITY);
             if (c.ok) {
                 float dist = norm(c.p - o2);
                 if (dist < FLT_MAX &&
@@ -587,7 +600,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                 int nflag = 0;            // stack entries whose key is <= tau (sign bit set)
                 auto test_sah = [&](const TriGeom& tg) {
                     if (STATS) st.tris++;
-                    Cand c = tri_test(tg, o2, d2, eps);
+                    Cand c = tri_test(tg, o2, d2, eps, RTG_TRI_WINDOW ? thi : INFINITY);
                     if (!c.ok) return;
                     const float dist = norm(c.p - o2);
                     const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
