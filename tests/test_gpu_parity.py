@@ -30,7 +30,25 @@ SCENES = {
     "bgtex": lambda: scenegen.bgtex(48, 32, spp=1),
     "bgtex_ms": lambda: scenegen.bgtex(48, 32, spp=3, interp=1),
     "glass_nest": lambda: scenegen.glass_nest(32, 24, spp=2, max_depth=6),   # rays double per level
+    # the full shading variants by light set (round 4, SceneView::heavy): textures / BRDFs without a
+    # spot or environment light, and an area light together with a spot light
+    "textured_point": lambda: _spot_to_point(scenegen.textured(48, 36)),
+    "cornell_spot": lambda: _with_spot(scenegen.cornell(40, 30, spp=2)),
 }
+
+
+def _spot_to_point(sc):
+    for L in sc.lights:
+        if L.type == rtg._abi.LIGHT_SPOT:
+            L.type = rtg._abi.LIGHT_POINT
+    assert all(L.type not in (rtg._abi.LIGHT_SPOT, rtg._abi.LIGHT_ENVIRONMENT) for L in sc.lights)
+    return sc
+
+
+def _with_spot(sc):
+    sc.lights.append(rtg.Light(type=rtg._abi.LIGHT_SPOT, position=(2.0, 8.0, 2.0), direction=(-0.3, -1.0, -0.4),
+                               intensity=(600.0, 500.0, 400.0), coverage_deg=50.0, falloff_deg=30.0))
+    return sc
 
 
 def _cmp(img, ref):
