@@ -95,7 +95,11 @@ namespace rtg {
 #ifndef RTG_PT_WAVES
 #define RTG_PT_WAVES 3
 #endif
-#define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? RTG_PT_WAVES : 1)))
+// BRDF-only variants without Torrance-Sparrow models (round 4): 143 VGPRs uncapped
+#ifndef RTG_PT_WAVES_NOTS
+#define RTG_PT_WAVES_NOTS 3
+#endif
+#define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? (BRDF == 1 ? RTG_PT_WAVES_NOTS : RTG_PT_WAVES) : 1)))
 #ifndef RTG_PT_BLOCK
 #define RTG_PT_BLOCK 256
 #endif
@@ -1179,6 +1183,10 @@ DEV float distribution_ts(float cosAlpha, int p) {       // Light.cpp:12-16
     x = (float)((double)x * pow((double)cosAlpha, (double)p));
     return x;
 }
+// TS: the Torrance-Sparrow models compiled in (their distribution term is a double-precision
+// pow(cos, p), whose code alone takes the path tracer's BRDF shading from 143 to 189 VGPRs); a scene
+// without TS / TSF materials runs the variants without it (SceneView::brdf_ts).
+template <bool TS = true>
 DEV f3 term_brdf(f3 wi, f3 wo, f3 n, const MaterialDev& m) {   // Light.cpp:62-155
     f3 kd = ld3(m.diffuse), ks = ld3(m.specular);
     int p = m.phong_exp;
@@ -1212,7 +1220,7 @@ DEV f3 term_brdf(f3 wi, f3 wo, f3 n, const MaterialDev& m) {   // Light.cpp:62-1
         return kd / (float)PI_D + (ks * (float)((p + 8) / (8 * PI_D))) * f_powi(cosAngle, p);
     }
     case RTG_BRDF_TS:
-    case RTG_BRDF_TSF: {
+    case RTG_BRDF_TSF: if constexpr (TS) {
         f3 wh = normalized(wo + wi);
         float f = 0;
         f3 dp = kd / (float)PI_D;
@@ -1232,8 +1240,9 @@ DEV f3 term_brdf(f3 wi, f3 wo, f3 n, const MaterialDev& m) {   // Light.cpp:62-1
         return mk(0, 0, 0);
     }
 }
+template <bool TS = true>
 DEV f3 brdf(f3 wi, f3 wo, f3 n, f3 radiance, const MaterialDev& m) {   // Light.cpp:157-162
-    f3 t = term_brdf(wi, wo, n, m);
+    f3 t = term_brdf<TS>(wi, wo, n, m);
     float cosAngle = fmax0(dot(wi, n));
     return cw(radiance, t) * cosAngle;
 }
@@ -1248,9 +1257,10 @@ DEV f3 specular_term(f3 LC, f3 wo, f3 wi, const Ret& ret, const MaterialDev& m) 
     float alpha = fmax0(dot(ret.normal, h));
     return cw(LC, ld3(m.specular) * f_powi(alpha, m.phong_exp));
 }
-template <bool FULL = true>
+// BRDF: 0 the reference's Blinn-Phong terms only, 1 the BRDF models without Torrance-Sparrow, 2 all
+template <int BRDF = 2>
 DEV f3 phong_or_brdf(f3 LC, f3 wo, f3 wi, const Ret& ret, const MaterialDev& m) {
-    if (FULL && m.brdf != RTG_BRDF_NONE) return brdf(wi, wo, ret.normal, LC, m);
+    if (BRDF != 0 && m.brdf != RTG_BRDF_NONE) return brdf<BRDF == 2>(wi, wo, ret.normal, LC, m);
     float alpha = fmax0(dot(ret.normal, wi));
     return diffuse_term(LC, ret, m, alpha) + specular_term(LC, wo, wi, ret, m);
 }
@@ -1302,7 +1312,7 @@ DEV float emit_shadow_tmax(f3 origin, f3 p, f3 lp, f3 d, float eps) {
 // rejection loop) sets the register peak of the shading kernels: inlined into the full k_shade it
 // takes the light loop from 79 to 244 VGPRs (cross-compiled resource usage, round 4), so scenes
 // without such lights get variants without that code.
-template <bool FULL = true, bool SPOT = true, bool BRDF = FULL, bool EMIT = true>
+template <bool FULL = true, bool SPOT = true, int BRDF = FULL ? 2 : 0, bool EMIT = true>
 DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, const Ret& ret, const MaterialDev& m,
                       uint64_t seed, uint32_t pixel, uint32_t sample, uint64_t path, ShadowRec& sr) {
     const LightDev& L = sv.lights[li];
@@ -1798,7 +1808,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                     nd.cr = amb.x; nd.cg = amb.y; nd.cb = amb.z;
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
-                        light_sample<FULL, SPOT, FULL && TEX, false>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
+                        light_sample<FULL, SPOT, (FULL && TEX) ? 2 : 0, false>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         // one light: a query that is not traced is never read (k_light_sum reads
                         // every record when there are several)
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
@@ -1983,7 +1993,7 @@ constexpr int kContrib = 0x200;   // NodeRec.kind: the vertex adds T (x) colour 
 // (separate instantiations, as k_shade).  A queued ray's level is lv_in[i] when the schedule
 // mixes levels in one launch (stream steps), else `level_in`; lv_out (when set) receives the
 // continuation's level.
-template <bool FULL, bool SPOT, bool BRDF, bool GEN = false>
+template <bool FULL, bool SPOT, int BRDF, bool GEN = false>
 __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const SceneView sv, const CameraDev cam, int level_in, const PassDev ps,
                                                   uint64_t seed, const RayQ rays,
                                                   const RayMeta* __restrict__ meta, const HitRec* __restrict__ hits,
@@ -2700,11 +2710,14 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
     } while (0)
     // textures / area / environment lights need the full variant; BRDFs alone do not
     if (sv.full && !sv.brdf_only) {
-        if (sv.heavy) RTG_PT_LAUNCH(true, true, true); else RTG_PT_LAUNCH(true, false, true);
+        if (sv.heavy) RTG_PT_LAUNCH(true, true, 2); else RTG_PT_LAUNCH(true, false, 2);
     }
-    else if (sv.full) { if (sv.spot) RTG_PT_LAUNCH(false, true, true); else RTG_PT_LAUNCH(false, false, true); }
-    else if (sv.spot) RTG_PT_LAUNCH(false, true, false);
-    else RTG_PT_LAUNCH(false, false, false);
+    else if (sv.full) {    // BRDFs only: with / without the Torrance-Sparrow models
+        if (sv.spot) { if (sv.brdf_ts) RTG_PT_LAUNCH(false, true, 2); else RTG_PT_LAUNCH(false, true, 1); }
+        else { if (sv.brdf_ts) RTG_PT_LAUNCH(false, false, 2); else RTG_PT_LAUNCH(false, false, 1); }
+    }
+    else if (sv.spot) RTG_PT_LAUNCH(false, true, 0);
+    else RTG_PT_LAUNCH(false, false, 0);
 #undef RTG_PT_LAUNCH
 #undef RTG_PT_LAUNCH1
 }

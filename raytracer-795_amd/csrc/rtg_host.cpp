@@ -1979,6 +1979,10 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     int any_brdf = 0;
     for (int i = 0; i < d->num_materials; i++) any_brdf |= d->materials[i].brdf != RTG_BRDF_NONE;
     sv.brdf_only = !sv.full && any_brdf;
+    sv.brdf_ts = 0;
+    for (int i = 0; i < d->num_materials; i++)
+        sv.brdf_ts |= d->materials[i].brdf == RTG_BRDF_TS || d->materials[i].brdf == RTG_BRDF_TSF;
+    if (const char* e = getenv("RTG_PT_TS")) sv.brdf_ts |= atoi(e) != 0;   // A/B: the variants with them
     sv.tex = any_brdf;
     for (int i = 0; i < d->num_objects; i++) sv.tex |= d->objects[i].num_textures > 0;
     sv.full |= any_brdf;

@@ -190,6 +190,8 @@ struct SceneView {
     int heavy;                     // a spot or environment light: the full shading variants compile in
                                    // their double-precision libm code only then (light_sample)
     int brdf_only;                 // full only because of BRDFs (no textures / area / environment)
+    int brdf_ts;                   // a Torrance-Sparrow (TS / TSF) material: the path tracer's BRDF variants
+                                   // compile those models in only then
     int tex;                       // any textured object or BRDF material (k_shade's TEX variant)
     int meta_free;                 // Whitted: no RNG below level 0 (no textures / area / environment
                                    // lights / rough materials): child rays need no RayMeta (their

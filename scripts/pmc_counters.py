@@ -29,7 +29,10 @@ COMBINED = ("rtg::k_trace<false, false", "rtg::k_shadow<false, false", "rtg::k_s
             "rtg::k_shade<true, true, 256, false", "rtg::k_shade<true, true, 256, true",
             "rtg::k_shade<true, false, 256, false", "rtg::k_shade<true, false, 256, true",
             "rtg::k_pt_shade<false, false, true", "rtg::k_pt_shade<false, false, false", "rtg::k_pt_shade<false, true, true",
-            "rtg::k_pt_shade<true, true, true", "rtg::k_pt_shade<true, false, true")
+            "rtg::k_pt_shade<true, true, true", "rtg::k_pt_shade<true, false, true",
+            "rtg::k_pt_shade<false, false, 0", "rtg::k_pt_shade<false, false, 1", "rtg::k_pt_shade<false, false, 2",
+            "rtg::k_pt_shade<false, true, 0", "rtg::k_pt_shade<false, true, 1", "rtg::k_pt_shade<false, true, 2",
+            "rtg::k_pt_shade<true, true, 2", "rtg::k_pt_shade<true, false, 2")
 
 
 def keys_of(k):

@@ -38,6 +38,22 @@ def _phong(sc):
     return sc
 
 
+@pytest.mark.parametrize("flags", [I | N | R, N])
+def test_path_trace_torrance_sparrow_variant_matches_oracle(gpu, flags):
+    """BRDF-only scene with Torrance-Sparrow materials: the k_pt_shade<false, false, 2> variant (the
+    cornell_pt default, without them, runs k_pt_shade<false, false, 1>; round 4)."""
+    sc = scenegen.cornell_pt(32, 24, spp=4, flags=flags)
+    sc.materials[0].brdf = A.BRDF_TS
+    sc.materials[3].brdf = A.BRDF_TSF
+    sc.materials[3].refraction_index, sc.materials[3].absorption_index = 1.3, 2.0
+    with rtg.Renderer(sc, device=gpu) as r:
+        img = r.render(0)
+    ref, _, _, _ = pyoracle.Oracle(sc).render(0)
+    linf, frac, nanm = _cmp(img, ref)
+    assert nanm == 0
+    assert linf < TOL
+
+
 @pytest.mark.parametrize("flags", FLAGS)
 def test_path_trace_matches_oracle(gpu, flags):
     sc = scenegen.cornell_pt(40, 30, spp=6, flags=flags)
