@@ -86,6 +86,13 @@ namespace rtg {
 #ifndef RTG_SHADE_LIGHT_WAVES
 #define RTG_SHADE_LIGHT_WAVES 5
 #endif
+// Its block size: 512 threads like the simple variant (256 dated from the 2-wave days).  C4
+// cornell_dynamic 1080p64, streams=1 frame: k_shade 6.04 -> 5.2 ms (three A/B pairs, same box,
+// profiles/r5e_ab_light_block.txt); the 8-lane frame is unchanged (16.5 ms), where its shading
+// overlaps other lanes' traversals.
+#ifndef RTG_SHADE_LIGHT_BLOCK
+#define RTG_SHADE_LIGHT_BLOCK 512
+#endif
 #define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? (!SPOT && !TEX ? RTG_SHADE_LIGHT_WAVES : RTG_SHADE_FULL_WAVES) \
                                                             : SPOT ? 2 : RTG_SHADE_WAVES)))
 // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
@@ -2669,7 +2676,8 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
     if (sv.full && sv.tex && sv.heavy) RTG_SHADE(true, true, 256, true, dim3(nblk(n, 256)), dim3(256));
     else if (sv.full && sv.tex) RTG_SHADE(true, false, 256, true, dim3(nblk(n, 256)), dim3(256));
     else if (sv.full && sv.heavy) RTG_SHADE(true, true, 256, false, dim3(nblk(n, 256)), dim3(256));
-    else if (sv.full) RTG_SHADE(true, false, 256, false, dim3(nblk(n, 256)), dim3(256));
+    else if (sv.full)
+        RTG_SHADE(true, false, RTG_SHADE_LIGHT_BLOCK, false, dim3(nblk(n, RTG_SHADE_LIGHT_BLOCK)), dim3(RTG_SHADE_LIGHT_BLOCK));
     else if (sv.spot) RTG_SHADE(false, true, kShadeBlock, false, g, b);
     else RTG_SHADE(false, false, kShadeBlock, false, g, b);
 #undef RTG_SHADE

@@ -12,6 +12,8 @@ mkdir -p $D
 stop() { echo "step $1 ended with rc $2: stopping"; exit $2; }
 run() {   # run <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
+  local i=2; local base=$name
+  while [ -e $D/$name.out ]; do name=${base}_$i; i=$((i+1)); done   # repeated steps keep their outputs
   timeout -k 10 $secs "$@" > $D/$name.out 2> $D/$name.err
   local rc=$?
   echo "[$name] rc=$rc"
