@@ -350,7 +350,15 @@ def main():
         args.cpu_rows = {"cornell_pt": 96, "spheres": 32}.get(args.workload, 540)
     scene = getattr(scenegen, make)(args.width, args.height, spp=args.spp or spp_default)
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
+    # The process's first kernel launch pays the HIP runtime's one-time set-up (100-170 ms on MI355X,
+    # profiles/r4i_hip_init_probe_kernel_first.txt: torch's own first fill).  It is timed here on its
+    # own (end_to_end_ms.runtime_init) so that scene_create is the library's cost in a process whose
+    # device is in use, as in any PyTorch program; librtg's own code-object load stays in it.
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    torch.zeros(1, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+    runtime_init_ms = (time.perf_counter() - t0) * 1e3
     t0 = time.perf_counter()
     r = rtg.Renderer(scene, device=local, tlas={"auto": 0, "off": 1, "on": 2}[args.tlas])
     create_ms = (time.perf_counter() - t0) * 1e3
@@ -475,8 +483,8 @@ def main():
         r2 = rtg.Renderer(scene, device=local, tlas={"auto": 0, "off": 1, "on": 2}[args.tlas])
         again_ms = (time.perf_counter() - t0) * 1e3
         again = {"ms": round(again_ms, 1), "phases": create_phases(r2.build_stats(), again_ms),
-                 "note": "a second Renderer(scene) in the same process; the first one's extra time is the HIP "
-                         "runtime's first-use set-up, which it overlaps with the host build"}
+                 "note": "a second Renderer(scene) in the same process (librtg's code objects loaded, its "
+                         "host threads and device allocator warm)"}
         r2.close()
         counters = load_counters(args.workload)
         roof = roofline(counters, st_roof, st_stats, args.workload, ms_per_step, pt)
@@ -509,12 +517,15 @@ def main():
                 "rays_per_frame": rays_frame,
                 "primary_msamples_s": round(cam.nx * cam.ny * cam.num_samples / (ms_per_step * 1e-3) / 1e6, 1),
                 "ms_per_frame_to_host": round(elapsed_h * 1e3 / args.steps, 2),
-                "end_to_end_ms": {"scene_create": round(create_ms, 1), "first_frame_to_host": round(first_frame_ms, 1),
-                                  "total": round(create_ms + first_frame_ms, 1),
+                "end_to_end_ms": {"runtime_init": round(runtime_init_ms, 1),
+                                  "scene_create": round(create_ms, 1), "first_frame_to_host": round(first_frame_ms, 1),
+                                  "total": round(runtime_init_ms + create_ms + first_frame_ms, 1),
                                   "scene_create_phases": create_phases(r.build_stats(), create_ms),
                                   "scene_create_again": again,
-                                  "note": "Renderer(scene) = the Python host's descriptor (desc_python) + "
-                                          "rtg_scene_create (library phases), then the first frame incl. its D2H copy"},
+                                  "note": "runtime_init = the process's first kernel launch (torch.zeros, the HIP "
+                                          "runtime's one-time set-up); Renderer(scene) = the Python host's descriptor "
+                                          "(desc_python) + rtg_scene_create (library phases), then the first frame incl. "
+                                          "its D2H copy"},
                 "rays_rank0": {k: st[k] for k in ("primary_rays", "secondary_rays", "shadow_rays")},
                 "kernel_ms_rank0_streams1": {k: round(st_roof[f"{k}_ms"], 2)
                                              for k in ("trace", "shade", "shadow", "resolve", "accumulate")},

@@ -1129,6 +1129,7 @@ struct rtg_scene {
     int bvh_builder = RTG_BVH_AUTO;
     double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
     rtg_build_stats bst{};                   // last scene build: per-phase wall times
+    std::chrono::steady_clock::time_point build_end{};   // build_scene's last statement (RTG_BUILD_TIMING)
     int bvh_gpu_objects = 0;                 // objects whose BVH the GPU built
     bool replica = false;                    // device copy made by scene_replicate (no host-side structures)
     rtg::MultiState* multi = nullptr;        // num_devices fan-out: replicas, RCCL communicators (rtg_multi.cpp)
@@ -2006,6 +2007,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.lean_shadow = d->num_lights == 1 &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);
+    pc.lap("view");
+    s->build_end = std::chrono::steady_clock::now();
     return RTG_OK;
 }
 
@@ -2078,6 +2081,14 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
                 (void)hipStreamSynchronize(nullptr);
             });
         rc = build_scene(s, desc);
+        if (getenv("RTG_BUILD_TIMING") && rc == RTG_OK)
+            fprintf(stderr, "[rtg] phase %-16s %7.2f ms\n", "release",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s->build_end).count());
+        if (warm.joinable()) {
+            PhaseClock wc;
+            warm.join();
+            wc.lap("warm_join");
+        }
         if (rc) {
             scene_free(s);
             delete s;
