@@ -468,27 +468,45 @@ inline float sah_ctr(const SahRec& r, int z) { return 0.5f * (r.lo[z] + r.hi[z])
 // worker threads (per-chunk bounds and bins combined in chunk order; a stable partition through
 // `tmp`), smaller ones on the calling thread (std::partition).
 constexpr int kSahParMin = 1 << 18;
-int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd) {
+// Box and centroid bounds of a range of records (min / max: exact in any order).
+struct SahBounds {
+    float lo[3], hi[3], clo[3], chi[3];
+    void clear() { for (int z = 0; z < 3; z++) { lo[z] = clo[z] = FLT_MAX; hi[z] = chi[z] = -FLT_MAX; } }
+    void add(const SahRec& q) {
+        for (int z = 0; z < 3; z++) {
+            const float c = sah_ctr(q, z);
+            lo[z] = std::min(lo[z], q.lo[z]);
+            hi[z] = std::max(hi[z], q.hi[z]);
+            clo[z] = std::min(clo[z], c);
+            chi[z] = std::max(chi[z], c);
+        }
+    }
+    void add(const SahBounds& b) {
+        for (int z = 0; z < 3; z++) {
+            lo[z] = std::min(lo[z], b.lo[z]); hi[z] = std::max(hi[z], b.hi[z]);
+            clo[z] = std::min(clo[z], b.clo[z]); chi[z] = std::max(chi[z], b.chi[z]);
+        }
+    }
+};
+// `pre`: the range's bounds when the parent's partition formed them (nullptr: computed here, one
+// more pass over the range); `outl` / `outr` receive the two halves' bounds, formed while
+// partitioning (*kids_ok = false when the split fell back to halving by count).
+int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd, const SahBounds* pre = nullptr,
+              SahBounds* outl = nullptr, SahBounds* outr = nullptr, bool* kids_ok = nullptr) {
     const int n = e - s;
     const bool par = n >= kSahParMin;
-    struct Bounds { float lo[3], hi[3], clo[3], chi[3]; };
+    if (kids_ok) *kids_ok = false;
+    using Bounds = SahBounds;
     auto bounds_of = [&](size_t k0, size_t k1) {
         Bounds B;
-        for (int z = 0; z < 3; z++) { B.lo[z] = B.clo[z] = FLT_MAX; B.hi[z] = B.chi[z] = -FLT_MAX; }
-        for (size_t k = k0; k < k1; k++) {
-            const SahRec& q = r[k];
-            for (int z = 0; z < 3; z++) {
-                const float c = sah_ctr(q, z);
-                B.lo[z] = std::min(B.lo[z], q.lo[z]);
-                B.hi[z] = std::max(B.hi[z], q.hi[z]);
-                B.clo[z] = std::min(B.clo[z], c);
-                B.chi[z] = std::max(B.chi[z], c);
-            }
-        }
+        B.clear();
+        for (size_t k = k0; k < k1; k++) B.add(r[k]);
         return B;
     };
     Bounds B;
-    if (par) {
+    if (pre) {
+        B = *pre;
+    } else if (par) {
         std::vector<Bounds> part(build_threads());
         const int T = parallel_chunks((size_t)n, 1 << 15, [&](int ch, size_t k0, size_t k1) { part[ch] = bounds_of(s + k0, s + k1); });
         B = part[0];
@@ -570,9 +588,12 @@ int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd) {
         if (n <= kSahMaxLeaf && (best_b < 0 || leaf_cost <= sah_area(nd.lo, nd.hi) + best)) return -1;
         if (best_b >= 0) {
             auto left = [&](const SahRec& q) { return bin_of(q) <= best_b; };
+            Bounds BL, BR;
+            BL.clear(); BR.clear();
             if (par) {
                 // stable: per-chunk left counts, then every chunk scatters its records to their
-                // places in tmp, then back
+                // places in tmp (forming each side's bounds), then back
+                std::vector<Bounds> pl(build_threads() + 1), pr(build_threads() + 1);
                 std::vector<int> nl(build_threads() + 1, 0), nr(build_threads() + 1, 0);
                 const int T = parallel_chunks((size_t)n, 1 << 15, [&](int ch, size_t k0, size_t k1) {
                     int c = 0;
@@ -587,16 +608,49 @@ int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd) {
                 for (int c = 0; c < T; c++) { hi_at[c] = acc; acc += nr[c]; }
                 parallel_chunks((size_t)n, 1 << 15, [&](int ch, size_t k0, size_t k1) {
                     int a = lo_at[ch], b2 = hi_at[ch];
+                    Bounds L, R;
+                    L.clear(); R.clear();
                     for (size_t k = k0; k < k1; k++) {
                         const SahRec& q = r[s + k];
-                        if (left(q)) tmp[s + a++] = q; else tmp[s + b2++] = q;
+                        if (left(q)) { tmp[s + a++] = q; L.add(q); } else { tmp[s + b2++] = q; R.add(q); }
                     }
+                    pl[ch] = L; pr[ch] = R;
                 });
+                for (int c = 0; c < T; c++) { BL.add(pl[c]); BR.add(pr[c]); }
                 parallel_chunks((size_t)n, 1 << 16, [&](int, size_t k0, size_t k1) {
                     std::copy(tmp + s + k0, tmp + s + k1, r + s + k0);
                 });
             } else {
-                mid = (int)(std::partition(r + s, r + e, left) - r);
+                // std::partition's bidirectional scheme (same resulting order), each record added
+                // to its side's bounds once
+                SahRec* f = r + s;
+                SahRec* l = r + e;
+                for (;;) {
+                    for (;;) {
+                        if (f == l) goto parted;
+                        if (!left(*f)) break;
+                        BL.add(*f);
+                        ++f;
+                    }
+                    --l;
+                    for (;;) {
+                        if (f == l) { BR.add(*f); goto parted; }   // *f: the right record the scan above stopped at
+                        if (left(*l)) break;
+                        BR.add(*l);
+                        --l;
+                    }
+                    std::iter_swap(f, l);
+                    BL.add(*f);
+                    BR.add(*l);
+                    ++f;
+                }
+            parted:
+                mid = (int)(f - r);
+            }
+            if (outl && outr && mid > s && mid < e) {
+                *outl = BL;
+                *outr = BR;
+                if (kids_ok) *kids_ok = true;
             }
         }
     } else if (n <= kSahMaxLeaf) {
@@ -606,15 +660,26 @@ int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd) {
     return mid;
 }
 
+// Levels of the SAH recursion whose subtrees get threads of their own (env RTG_SAH_DEPTH, A/B).
+static int sah_depth() {
+    static const int d = [] {
+        const char* e = getenv("RTG_SAH_DEPTH");
+        return e ? std::max(0, std::min(8, atoi(e))) : 6;   // 4 / 5 / 6: second creation 136-147 / 121-153 / 120-128 ms
+    }();
+    return d;
+}
+
 // Binned SAH BVH2 over [s, e), nodes appended depth first (node, left subtree, right subtree).
-int sah_rec(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out) {
+int sah_rec(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out, const SahBounds* pre = nullptr) {
     SahNode2 nd;
-    const int mid = sah_split(r, tmp, s, e, nd);
+    SahBounds bl, br;
+    bool kids = false;
+    const int mid = sah_split(r, tmp, s, e, nd, pre, &bl, &br, &kids);
     const int me = (int)out.size();
     out.push_back(nd);
     if (mid < 0) return me;
-    const int l = sah_rec(r, tmp, s, mid, out);
-    const int rr = sah_rec(r, tmp, mid, e, out);
+    const int l = sah_rec(r, tmp, s, mid, out, kids ? &bl : nullptr);
+    const int rr = sah_rec(r, tmp, mid, e, out, kids ? &br : nullptr);
     out[me].left = l;
     out[me].right = rr;
     return me;
@@ -624,10 +689,13 @@ int sah_rec(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out) {
 // into their own node arrays and appended in sah_rec's depth-first order: the result is identical
 // to sah_rec's, node numbering included (1 M-triangle dragon on the GPU box's host: 247 -> 78 ms).
 // The two halves partition disjoint ranges of r (and of tmp).
-int sah_rec_par(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out, int depth) {
-    if (depth <= 0 || e - s < (1 << 16)) return sah_rec(r, tmp, s, e, out);
+int sah_rec_par(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out, int depth,
+                const SahBounds* pre = nullptr) {
+    if (depth <= 0 || e - s < (1 << 16)) return sah_rec(r, tmp, s, e, out, pre);
     SahNode2 nd;
-    const int mid = sah_split(r, tmp, s, e, nd);
+    SahBounds bl, br;
+    bool kids = false;
+    const int mid = sah_split(r, tmp, s, e, nd, pre, &bl, &br, &kids);
     const int me = (int)out.size();
     out.push_back(nd);
     if (mid < 0) return me;
@@ -635,13 +703,13 @@ int sah_rec_par(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out
     std::exception_ptr err;
     std::thread t([&] {
         try {
-            sah_rec_par(r, tmp, s, mid, L, depth - 1);
+            sah_rec_par(r, tmp, s, mid, L, depth - 1, kids ? &bl : nullptr);
         } catch (...) {
             err = std::current_exception();
         }
     });
     try {
-        sah_rec_par(r, tmp, mid, e, R, depth - 1);
+        sah_rec_par(r, tmp, mid, e, R, depth - 1, kids ? &br : nullptr);
     } catch (...) {
         t.join();
         throw;
@@ -1369,6 +1437,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     hvec<float> gates;                       // per reference position: its leaf's parent box
     hvec<TriGeom> tris;
     hvec<int4> primidx;
+    bool early_upload = false;               // dnodes / gates / tris / primidx / orig_prim / vnormals already uploaded
     s->orig_prim.clear();
     s->bvh.assign(d->num_objects, ObjBVH());
     const float ieps = d->intersection_test_eps;
@@ -1456,7 +1525,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             sah_thread = std::thread([&] {
                 try {
                     PhaseClock tc;
-                    sah_rec_par(sah_rec_buf.data(), sah_tmp.data(), 0, np, sah_bn, 4);
+                    sah_rec_par(sah_rec_buf.data(), sah_tmp.data(), 0, np, sah_bn, sah_depth());
                     parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
                         for (size_t k = k0; k < k1; k++) sah_idx[k] = sah_rec_buf[k].idx;
                     });
@@ -1470,6 +1539,16 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                             for (size_t k = k0; k < k1; k++) sah_tris[k] = tri_geom(verts, pv, (size_t)sah_idx[k]);
                         });
                         tc.lap(" sah_tris (thread)");
+                        if (getenv("RTG_SAH_HASH")) {    // tree identity check (dev)
+                            uint64_t h = 1469598103934665603ull;
+                            auto mix = [&](const void* p, size_t nb) {
+                                const unsigned char* c = (const unsigned char*)p;
+                                for (size_t k = 0; k < nb; k++) { h ^= c[k]; h *= 1099511628211ull; }
+                            };
+                            mix(sah_nodes.data(), sah_nodes.size() * sizeof(Node4));
+                            mix(sah_idx.data(), sah_idx.size() * sizeof(int));
+                            fprintf(stderr, "[rtg] sah hash %zu nodes %016llx\n", sah_nodes.size(), (unsigned long long)h);
+                        }
                     }
                 } catch (...) {
                     sah_err = std::current_exception();
@@ -1647,6 +1726,18 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         const bool sah_ok = sah_try && ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0);
         bs.records_ms += pc.lap("records");
         PhaseClock sub;
+        // The last object's reference-tree records are final now: while the SAH thread finishes,
+        // this thread uploads them (the rest goes up after the top level).  Dragon1m: the wait for
+        // the SAH thread was 30-45 ms, these uploads ~10 ms of it.
+        if (s->device >= 0 && i == d->num_objects - 1 && sah_thread.joinable()) {
+            int rc2;
+            if ((rc2 = upload(s->d_nodes, dnodes)) || (rc2 = upload(s->d_gates, gates)) || (rc2 = upload(s->d_tris, tris)) ||
+                (rc2 = upload(s->d_primidx, primidx)) || (rc2 = upload(s->d_origprim, s->orig_prim)) ||
+                (rc2 = upload(s->d_vnormals, s->vnormals)))
+                return rc2;
+            early_upload = true;
+            sub.lap(" early_upload");
+        }
         if (sah_thread.joinable()) sah_thread.join();
         if (sah_err) std::rethrow_exception(sah_err);
         sub.lap(" sah_join_wait");
@@ -1937,17 +2028,24 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     }
 
     bs.top_level_ms += pc.lap("top_level");
-    if (s->device < 0) return RTG_OK;   // host-only build (introspection / CPU tests)
+    if (s->device < 0) {                // host-only build (introspection / CPU tests)
+        s->build_end = std::chrono::steady_clock::now();
+        return RTG_OK;
+    }
     std::vector<float> vflat(d->vertices, d->vertices + 3 * (size_t)nv);
     std::vector<float> tcflat;
     if (d->num_texcoords > 0) tcflat.assign(d->texcoords, d->texcoords + 2 * (size_t)d->num_texcoords);
     int rc;
-    if ((rc = upload(s->d_tops, tops)) || (rc = upload(s->d_geoms, geoms)) || (rc = upload(s->d_nodes, dnodes)) ||
-        (rc = (RTG_QNODES ? upload(s->d_nodes4, qnodes) : upload(s->d_nodes4, snodes))) || (rc = upload(s->d_stris, stris)) || (rc = upload(s->d_gates, gates)) ||
-        (rc = upload(s->d_tris, tris)) || (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_vertices, vflat)) ||
-        (rc = upload(s->d_vnormals, s->vnormals)) || (rc = upload(s->d_texcoords, tcflat)) ||
+    if (!early_upload &&
+        ((rc = upload(s->d_nodes, dnodes)) || (rc = upload(s->d_gates, gates)) || (rc = upload(s->d_tris, tris)) ||
+         (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_origprim, s->orig_prim)) ||
+         (rc = upload(s->d_vnormals, s->vnormals))))
+        return rc;
+    if ((rc = upload(s->d_tops, tops)) || (rc = upload(s->d_geoms, geoms)) ||
+        (rc = (RTG_QNODES ? upload(s->d_nodes4, qnodes) : upload(s->d_nodes4, snodes))) || (rc = upload(s->d_stris, stris)) ||
+        (rc = upload(s->d_vertices, vflat)) || (rc = upload(s->d_texcoords, tcflat)) ||
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
-        (rc = upload(s->d_lights, lights)) || (rc = upload(s->d_origprim, s->orig_prim)) ||
+        (rc = upload(s->d_lights, lights)) ||
         (rc = upload(s->d_topemit, top_emit)) || (rc = upload(s->d_etris, etris)) || (rc = upload(s->d_ecdf, ecdf)) ||
         (rc = upload(s->d_tlas, tlas_nodes)) || (rc = upload(s->d_tlasidx, tlas_idx)))
         return rc;
@@ -2008,6 +2106,26 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);
     pc.lap("view");
+    // The host copies of the uploaded records (~300 MB for a 1 M-triangle mesh) are freed on a
+    // detached thread: unmapping them took 18-25 ms of rtg_scene_create on the GPU box's host
+    // (RTG_BUILD_TIMING "release").  Only memory owned by this call goes there.
+    {
+        struct Grave {
+            hvec<Node> dnodes; hvec<Node4> snodes; hvec<TriGeom> stris, tris; hvec<float> gates; hvec<int4> primidx;
+            std::vector<V3> verts, vn; std::vector<ObjPrims> op; std::vector<float> vflat;
+        };
+        Grave* g = new (std::nothrow) Grave;
+        if (g) {
+            g->dnodes.swap(dnodes); g->snodes.swap(snodes); g->stris.swap(stris); g->tris.swap(tris);
+            g->gates.swap(gates); g->primidx.swap(primidx); g->verts.swap(verts); g->vn.swap(vn); g->op.swap(op);
+            g->vflat.swap(vflat);
+            try {
+                std::thread([g] { delete g; }).detach();
+            } catch (...) {
+                delete g;                    // no thread: free here
+            }
+        }
+    }
     s->build_end = std::chrono::steady_clock::now();
     return RTG_OK;
 }

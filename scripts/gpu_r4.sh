@@ -31,6 +31,7 @@ for step in "$@"; do
     nocpu_*) run $step 300 python3 bench.py --no-cpu --workload ${step#nocpu_} ;;
     hipinit) run hipinit 120 python3 scripts/hip_init_probe.py ;;
     create) run create 300 env RTG_BUILD_TIMING=1 python3 scripts/create_probe.py 3 ;;
+    createenv:*) IFS=: read -r _ kv <<< "$step"; n=${kv//=/_}; run create_${n//,/_} 300 env RTG_BUILD_TIMING=1 ${kv//,/ } python3 scripts/create_probe.py 3 ;;
     create_*) run $step 300 env RTG_BUILD_TIMING=1 python3 scripts/create_probe.py 3 ${step#create_} ;;
     shard) run shard 300 python3 scripts/shard_probe.py 1 8 ;;
     eb:*) IFS=: read -r _ kv wl <<< "$step"; name="eb_${kv//=/_}_$wl"
