@@ -46,6 +46,14 @@ namespace rtg {
 #ifndef RTG_SHADOW_CERT_OBJ
 #define RTG_SHADOW_CERT_OBJ 0
 #endif
+// Camera-sample waves of k_trace (level 0) walk the traversal tree wave-uniformly (visit_object).
+#ifndef RTG_UNI_PRIMARY
+#define RTG_UNI_PRIMARY 1
+#endif
+// ... and k_shadow's queries of level-0 nodes (A/B switch)
+#ifndef RTG_UNI_SHADOW
+#define RTG_UNI_SHADOW 1
+#endif
 // Shading of a flat triangle from its TriGeom record alone (hit_record).
 #ifndef RTG_FLAT_NORMAL
 #define RTG_FLAT_NORMAL 1
@@ -425,10 +433,10 @@ DEV int stk_get(const int* stack, int sstride, const int* spill, int sp) {
     return (kLdsStack >= kStackDepth || sp < kLdsStack) ? stack[sp * sstride] : spill[sp - kLdsStack];
 }
 
-template <bool EXHAUSTIVE, bool STATS, bool CERT>
+template <bool EXHAUSTIVE, bool STATS, bool CERT, bool UNI = false>
 DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, const float time, const bool fin,
                       float& nearest, HitRec& out, HitBary* bary, bool& certified, int* stack, int sstride, Stats& st,
-                      const float tcert, int* spill) {
+                      const float tcert, int* spill, const bool uni = false) {
     const float eps = sv.int_eps;
     const TopObject& T = sv.tops[i];
     const Geometry& g = sv.geoms[T.geom];
@@ -641,6 +649,81 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                 // at the object-level t < nearest)
                 if (g.flat_count > 0) {             // (flat_split < 0 here: sah_base >= 0)
                     for (int q = g.flat_first; q < g.flat_first + g.flat_count; q++) test_sah(sv.stris[q]);
+                } else if (UNI && uni) {
+                    // Wave-uniform walk (coherent waves: a pixel's camera samples).  The wave visits a
+                    // node when any of its lanes needs it; node, triangle and stack values are
+                    // uniform, so they come through the scalar cache instead of 64 identical vector
+                    // gathers.  Each lane still prunes by its own window and accepts by its own test,
+                    // so it sees a superset of its own walk's candidates, every one of which is a
+                    // valid candidate: the winner, the minimum of a total order, is unchanged.
+                    while (true) {
+                        cur = __builtin_amdgcn_readfirstlane(cur);
+                        if (STATS) { st.nodes += 4; st.steps++; }
+                        const Node4 nd = sv.snodes[cur];
+                        const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
+                        const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
+                        const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w};
+                        const float hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
+                        const float hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
+                        const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
+                        const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
+                        const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
+                        float key[4];
+                        int okm = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
+                            const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
+                            const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
+                            const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                            const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                            const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
+                            const float lo = le - e, hi = sl + e;
+                            key[j] = lo;
+                            okm |= (inf[j] >= 0 && !(hi < lo || hi < tlo || lo > thi)) << j;
+                        }
+                        // leaf slots any lane still needs, each lane testing only its own
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            if (inf[j] <= 0) continue;
+                            const bool mine = ((okm >> j) & 1) && !(key[j] > thi);
+                            if (__ballot(mine) == 0ull) continue;
+                            if (mine)
+                                for (int q = rf[j]; q < rf[j] + inf[j]; q++) test_sah(sv.stris[q]);
+                        }
+                        // interior slots any lane needs, in the first such lane's near-first order
+                        float k4[4];
+                        int r4[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const bool take = inf[j] == 0 && ((okm >> j) & 1) && !(key[j] > thi);
+                            const bool any = __ballot(take) != 0ull;
+                            const unsigned long long tm = __ballot(take);
+                            const float kf = take ? key[j] : INFINITY;
+                            const int lead = any ? (int)__builtin_ctzll(tm) : 0;
+                            k4[j] = any ? __shfl(kf, lead) : INFINITY;
+                            r4[j] = any ? rf[j] : -1;
+                        }
+                        auto ce = [&](int a, int b) {
+                            const bool sw = k4[b] < k4[a];
+                            const float ka = k4[a], kb = k4[b];
+                            const int ra = r4[a], rb = r4[b];
+                            k4[a] = sw ? kb : ka; k4[b] = sw ? ka : kb;
+                            r4[a] = sw ? rb : ra; r4[b] = sw ? ra : rb;
+                        };
+                        ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+                        const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
+                        if (sp + npush > kStackDepth) { use2 = true; break; }
+                        for (int j = 3; j >= 1; j--)
+                            if (r4[j] >= 0) { stk_put(stack, sstride, spill, sp, r4[j]); sp++; }
+                        if (r4[0] >= 0) {
+                            cur = r4[0];
+                        } else {
+                            if (sp == 0) break;
+                            sp--;
+                            cur = stk_get(stack, sstride, spill, sp);
+                        }
+                    }
                 } else
                 while (true) {
                     if (STATS) { st.nodes += 4; st.steps++; }   // one node = four 32-B child records (the model's unit)
@@ -781,9 +864,9 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
     }
 }
 
-template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool CERT = false>
+template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool CERT = false, bool UNI = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
-                       short* tstack = nullptr, float tcert = -INFINITY, HitBary* bary = nullptr) {
+                       short* tstack = nullptr, float tcert = -INFINITY, HitBary* bary = nullptr, bool uni = false) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
@@ -792,8 +875,8 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     const bool fin = ray_finite(o, d, time);
     int spill[kStackDepth > kLdsStack ? kStackDepth - kLdsStack : 1];
     auto visit = [&](const int i) {
-        visit_object<EXHAUSTIVE, STATS, CERT>(sv, i, o, d, time, fin, nearest, out, bary, certified, stack, sstride, st,
-                                              tcert, spill);
+        visit_object<EXHAUSTIVE, STATS, CERT, UNI>(sv, i, o, d, time, fin, nearest, out, bary, certified, stack, sstride,
+                                                   st, tcert, spill, uni);
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
@@ -1640,9 +1723,11 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
             tmax = FLT_MAX;
         }
         HitBary hb = {0.0f, 0.0f, 0.0f};
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st,
-                                                        s_tstack + (TLAS ? threadIdx.x : 0), -INFINITY,
-                                                        RTG_HIT_STORED ? &hb : nullptr);
+        // a wave of camera samples only (a pixel's samples, or adjacent pixels'): the wave-uniform walk
+        const bool uni = RTG_UNI_PRIMARY && GEN && !TLAS && !EXHAUSTIVE && (int)(blockIdx.x * blockDim.x) >= nq;
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, false, GEN && !TLAS && !EXHAUSTIVE && RTG_UNI_PRIMARY>(
+            sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0), -INFINITY,
+            RTG_HIT_STORED ? &hb : nullptr, uni);
         if (compact) {
             const HitPlanes hp = hit_planes(hits, n);
             hp.id[i] = make_int2(h.obj, h.prim);
@@ -2243,7 +2328,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        const ShadowPlanes shadows, bool lean,
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount, const NodePlanes nodes,
-                                                                       unsigned* nan_queries, Counters* ctr) {
+                                                                       unsigned* nan_queries, Counters* ctr,
+                                                                       bool uni_level) {
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2318,9 +2404,12 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 if (tc > 0.0f) tcert = tc;
             }
         }
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KCERT>(
+        // queries of camera-sample nodes (level 0 of a pass): a wave's queries leave neighbouring
+        // points of one or two pixels, so they walk wave-uniformly (visit_object)
+        constexpr bool KUNI = RTG_UNI_SHADOW && !EXHAUSTIVE && !TLAS && !KCERT;
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KCERT, KUNI>(
             sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
-            s_tstack + (TLAS ? threadIdx.x : 0), tcert);
+            s_tstack + (TLAS ? threadIdx.x : 0), tcert, nullptr, KUNI && uni_level);
         const float mode = query_mode();
         bool blocked;
         if (h.pad == 1) {
@@ -2683,7 +2772,7 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
 #undef RTG_SHADE
 }
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted) {
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted, bool uni) {
     if (n <= 0 || sv.num_lights == 0) return;
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
@@ -2691,11 +2780,11 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     const ShadowPlanes sp = shadow_planes(shadows, cap);
     const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
     const bool tl = sv.tlas_root >= 0;
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
-    else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
-    else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr);
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
+    else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
+    else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
     if (sv.num_lights > 1 && whitted)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, sp, np, n);
 }

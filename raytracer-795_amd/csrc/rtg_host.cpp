@@ -2427,7 +2427,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
         launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
-                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt);
+                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni=*/level == 0);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt) {
