@@ -50,6 +50,10 @@ namespace rtg {
 #ifndef RTG_UNI_PRIMARY
 #define RTG_UNI_PRIMARY 1
 #endif
+// every wave, every level (timing experiments)
+#ifndef RTG_UNI_ALL
+#define RTG_UNI_ALL 0
+#endif
 // ... and k_shadow's queries of level-0 nodes (A/B switch)
 #ifndef RTG_UNI_SHADOW
 #define RTG_UNI_SHADOW 1
@@ -1724,8 +1728,9 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
         }
         HitBary hb = {0.0f, 0.0f, 0.0f};
         // a wave of camera samples only (a pixel's samples, or adjacent pixels'): the wave-uniform walk
-        const bool uni = RTG_UNI_PRIMARY && GEN && !TLAS && !EXHAUSTIVE && (int)(blockIdx.x * blockDim.x) >= nq;
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, false, GEN && !TLAS && !EXHAUSTIVE && RTG_UNI_PRIMARY>(
+        const bool uni = RTG_UNI_PRIMARY && (GEN || RTG_UNI_ALL) && !TLAS && !EXHAUSTIVE &&
+                         (RTG_UNI_ALL || (int)(blockIdx.x * blockDim.x) >= nq);
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, false, (GEN || RTG_UNI_ALL) && !TLAS && !EXHAUSTIVE && RTG_UNI_PRIMARY>(
             sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0), -INFINITY,
             RTG_HIT_STORED ? &hb : nullptr, uni);
         if (compact) {
@@ -2329,7 +2334,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount, const NodePlanes nodes,
                                                                        unsigned* nan_queries, Counters* ctr,
-                                                                       bool uni_level) {
+                                                                       int uni_from) {
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2404,12 +2409,14 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 if (tc > 0.0f) tcert = tc;
             }
         }
-        // queries of camera-sample nodes (level 0 of a pass): a wave's queries leave neighbouring
-        // points of one or two pixels, so they walk wave-uniformly (visit_object)
+        // queries of camera-sample nodes (nodes >= uni_from: level 0 of a pass, a stream step's new
+        // samples): a wave whose queries all leave such nodes -- neighbouring points of one or two
+        // pixels -- walks wave-uniformly (visit_object)
         constexpr bool KUNI = RTG_UNI_SHADOW && !EXHAUSTIVE && !TLAS && !KCERT;
+        const bool uni = KUNI && (RTG_UNI_ALL || __ballot(i < uni_from) == 0ull);
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KCERT, KUNI>(
             sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
-            s_tstack + (TLAS ? threadIdx.x : 0), tcert, nullptr, KUNI && uni_level);
+            s_tstack + (TLAS ? threadIdx.x : 0), tcert, nullptr, uni);
         const float mode = query_mode();
         bool blocked;
         if (h.pad == 1) {
@@ -2772,7 +2779,7 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
 #undef RTG_SHADE
 }
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted, bool uni) {
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted, int uni_from) {
     if (n <= 0 || sv.num_lights == 0) return;
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
@@ -2780,11 +2787,11 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     const ShadowPlanes sp = shadow_planes(shadows, cap);
     const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
     const bool tl = sv.tlas_root >= 0;
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
-    else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
-    else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni);
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
+    else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
+    else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
     if (sv.num_lights > 1 && whitted)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, sp, np, n);
 }

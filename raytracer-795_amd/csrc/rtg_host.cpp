@@ -2427,7 +2427,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
         launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
-                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni=*/level == 0);
+                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni_from=*/level == 0 ? 0 : INT_MAX);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt) {
@@ -2631,7 +2631,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
             launch_shadow(sv, W.shadows.as<ShadowRec>(), W.slist.as<int>(), reinterpret_cast<const unsigned*>(qc) + 1,
-                          nodes->as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*whitted=*/!pt);
+                          nodes->as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*whitted=*/!pt,
+                          /*uni_from=*/g > 0 ? m : INT_MAX);   // the step's new camera samples: nodes [m, n)
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
             if (pt)
                 launch_pt_gather(nodes->as<NodeRec>(), A.paths.as<PathRec>(), W.shadows.as<ShadowRec>(), nL,

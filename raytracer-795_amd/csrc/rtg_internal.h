@@ -2,6 +2,7 @@
 // HIP kernels (rtg_device.hip).  Everything here is device-resident, read-only data
 // laid out for gfx950 gathers, plus the per-level wavefront queue records.
 #pragma once
+#include <climits>
 #include <stdint.h>
 
 #include <string>
@@ -404,7 +405,7 @@ void launch_resolve_planes(const SceneView& sv, const NodePlanes& self, const No
 void launch_accumulate_planes(const SceneView& sv, const NodePlanes& level0, const NodePlanes& level1, bool resolve,
                               float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
-                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted = true, bool uni = false);
+                   int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted = true, int uni_from = INT_MAX);  // uni_from: first camera-sample node (wave-uniform walk)
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
