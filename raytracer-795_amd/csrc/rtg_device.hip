@@ -54,6 +54,19 @@ namespace rtg {
 #ifndef RTG_UNI_ALL
 #define RTG_UNI_ALL 0
 #endif
+// ... and queued rays / shadow queries of waves that are coherent (wave_coherent; A/B switch, off:
+// with cones of 0.02 / 0.05 / 0.15 and boxes of 0.005 / 0.02 / 0.05 (relative) the dragon frame took
+// 30.8 / 30.8 / 31.2 ms against 30.7, cornell_pt 351 / 351 against 348 ms -- profiles/r5n_ab_uniform_adapt.txt)
+#ifndef RTG_UNI_ADAPT
+#define RTG_UNI_ADAPT 0
+#endif
+#ifndef RTG_UNI_DIR
+#define RTG_UNI_DIR 0.05f
+#endif
+#ifndef RTG_UNI_ORG
+#define RTG_UNI_ORG 0.02f
+#endif
+constexpr float kUniDir = RTG_UNI_DIR, kUniOrg = RTG_UNI_ORG;
 // ... and k_shadow's queries of level-0 nodes (A/B switch)
 #ifndef RTG_UNI_SHADOW
 #define RTG_UNI_SHADOW 1
@@ -866,6 +879,20 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             out.obj = i; out.prim = bprim; out.t = t; out.pad = 1;
         }
     }
+}
+
+// A wave whose active lanes' rays start within a small box and point within a small cone of its
+// first lane's ray (RTG_UNI_ADAPT: coherent queued rays, e.g. one pixel's reflections off a
+// smooth sphere).  NaN components count as incoherent.
+DEV float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+DEV bool wave_coherent(f3 o, f3 d) {
+    const f3 o0 = mk(rfl(o.x), rfl(o.y), rfl(o.z)), d0 = mk(rfl(d.x), rfl(d.y), rfl(d.z));
+    const float ds = fmaxf(fmaxf(fabsf(d0.x), fabsf(d0.y)), fabsf(d0.z));
+    const float os = fmaxf(fmaxf(fabsf(o0.x), fabsf(o0.y)), fabsf(o0.z)) + 1.0f;
+    const float dd = fmaxf(fmaxf(fabsf(d.x - d0.x), fabsf(d.y - d0.y)), fabsf(d.z - d0.z));
+    const float od = fmaxf(fmaxf(fabsf(o.x - o0.x), fabsf(o.y - o0.y)), fabsf(o.z - o0.z));
+    const bool ok = dd <= kUniDir * ds && od <= kUniOrg * os;
+    return __ballot(!ok) == 0ull;
 }
 
 template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool CERT = false, bool UNI = false>
@@ -1728,9 +1755,10 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
         }
         HitBary hb = {0.0f, 0.0f, 0.0f};
         // a wave of camera samples only (a pixel's samples, or adjacent pixels'): the wave-uniform walk
-        const bool uni = RTG_UNI_PRIMARY && (GEN || RTG_UNI_ALL) && !TLAS && !EXHAUSTIVE &&
-                         (RTG_UNI_ALL || (int)(blockIdx.x * blockDim.x) >= nq);
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, false, (GEN || RTG_UNI_ALL) && !TLAS && !EXHAUSTIVE && RTG_UNI_PRIMARY>(
+        constexpr bool KUNI = (GEN || RTG_UNI_ALL || RTG_UNI_ADAPT) && !TLAS && !EXHAUSTIVE && RTG_UNI_PRIMARY;
+        const bool uni = KUNI && (RTG_UNI_ALL || (GEN && (int)(blockIdx.x * blockDim.x) >= nq) ||
+                                  (RTG_UNI_ADAPT && wave_coherent(o, d)));
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, false, KUNI>(
             sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0), -INFINITY,
             RTG_HIT_STORED ? &hb : nullptr, uni);
         if (compact) {
@@ -2413,7 +2441,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         // samples): a wave whose queries all leave such nodes -- neighbouring points of one or two
         // pixels -- walks wave-uniformly (visit_object)
         constexpr bool KUNI = RTG_UNI_SHADOW && !EXHAUSTIVE && !TLAS && !KCERT;
-        const bool uni = KUNI && (RTG_UNI_ALL || __ballot(i < uni_from) == 0ull);
+        const bool uni = KUNI && (RTG_UNI_ALL || __ballot(i < uni_from) == 0ull || (RTG_UNI_ADAPT && wave_coherent(o, d)));
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KCERT, KUNI>(
             sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
             s_tstack + (TLAS ? threadIdx.x : 0), tcert, nullptr, uni);
