@@ -28,6 +28,7 @@ def kname(k):
 COMBINED = ("rtg::k_trace<false, false", "rtg::k_shadow<false, false", "rtg::k_shade<false, false, 512, false", "rtg::k_shade<false, true, 512, false",
             "rtg::k_shade<true, true, 256, false", "rtg::k_shade<true, true, 256, true",
             "rtg::k_shade<true, false, 256, false", "rtg::k_shade<true, false, 256, true",
+            "rtg::k_shade<true, false, 512, false",
             "rtg::k_pt_shade<false, false, true", "rtg::k_pt_shade<false, false, false", "rtg::k_pt_shade<false, true, true",
             "rtg::k_pt_shade<true, true, true", "rtg::k_pt_shade<true, false, true",
             "rtg::k_pt_shade<false, false, 0", "rtg::k_pt_shade<false, false, 1", "rtg::k_pt_shade<false, false, 2",
