@@ -1756,8 +1756,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
         HitBary hb = {0.0f, 0.0f, 0.0f};
         // a wave of camera samples only (a pixel's samples, or adjacent pixels'): the wave-uniform walk
         constexpr bool KUNI = (GEN || RTG_UNI_ALL || RTG_UNI_ADAPT) && !TLAS && !EXHAUSTIVE && RTG_UNI_PRIMARY;
-        const bool uni = KUNI && (RTG_UNI_ALL || (GEN && (int)(blockIdx.x * blockDim.x) >= nq) ||
-                                  (RTG_UNI_ADAPT && wave_coherent(o, d)));
+        const bool uni = KUNI && sv.uni_walk && (RTG_UNI_ALL || (GEN && (int)(blockIdx.x * blockDim.x) >= nq) ||
+                                                 (RTG_UNI_ADAPT && wave_coherent(o, d)));
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, false, KUNI>(
             sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0), -INFINITY,
             RTG_HIT_STORED ? &hb : nullptr, uni);
@@ -2441,7 +2441,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         // samples): a wave whose queries all leave such nodes -- neighbouring points of one or two
         // pixels -- walks wave-uniformly (visit_object)
         constexpr bool KUNI = RTG_UNI_SHADOW && !EXHAUSTIVE && !TLAS && !KCERT;
-        const bool uni = KUNI && (RTG_UNI_ALL || __ballot(i < uni_from) == 0ull || (RTG_UNI_ADAPT && wave_coherent(o, d)));
+        const bool uni = KUNI && sv.uni_walk &&
+                         (RTG_UNI_ALL || __ballot(i < uni_from) == 0ull || (RTG_UNI_ADAPT && wave_coherent(o, d)));
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KCERT, KUNI>(
             sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
             s_tstack + (TLAS ? threadIdx.x : 0), tcert, nullptr, uni);

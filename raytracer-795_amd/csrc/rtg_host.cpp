@@ -2102,6 +2102,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         const rtg_object_desc& o = d->objects[i];
         if (o.type == RTG_OBJ_TRIANGLE || (o.type == RTG_OBJ_MESH && (o.smooth || o.num_textures > 0))) sv.bary = 1;
     }
+    sv.uni_walk = 1;
+    if (const char* e = getenv("RTG_UNI_WALK")) sv.uni_walk = atoi(e) != 0;
     sv.lean_shadow = d->num_lights == 1 &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);

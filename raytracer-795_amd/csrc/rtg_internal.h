@@ -203,6 +203,9 @@ struct SceneView {
                                    // ray queues carry times (RayQ::t)
     int bary;                      // some triangle is smooth-shaded or textured: the render path's
                                    // hit records carry the winner's barycentrics (HitPlanes::bg)
+    int uni_walk;                  // camera-sample waves may walk the traversal tree wave-uniformly
+                                   // (default 1; env RTG_UNI_WALK=0 at scene creation: per-lane walks,
+                                   // for the parity test that the two agree)
     // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
     // lights into num_lights)
     const int* top_emit;           // per top-level entry: emitter light index, -1 if not a light
