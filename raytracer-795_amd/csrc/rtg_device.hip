@@ -67,6 +67,10 @@ namespace rtg {
 #define RTG_UNI_ORG 0.02f
 #endif
 constexpr float kUniDir = RTG_UNI_DIR, kUniOrg = RTG_UNI_ORG;
+// k_shade: waves whose hits share one entry read its records through the scalar cache (A/B switch)
+#ifndef RTG_UNI_SHADE
+#define RTG_UNI_SHADE 1
+#endif
 // ... and k_shadow's queries of level-0 nodes (A/B switch)
 #ifndef RTG_UNI_SHADOW
 #define RTG_UNI_SHADOW 1
@@ -1862,13 +1866,26 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
             }
         } else {
             hit = true;
-            Ret ret = hit_record<FULL && TEX, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+            // a wave whose hits are all on one entry (a pixel's samples on the dragon, say) reads that
+            // entry's records and material through the scalar cache: the same calls with the entry index
+            // made wave-uniform (readfirstlane), instead of 64 identical per-lane gathers
+            Ret ret;
+            MaterialDev m;
+            const int ob0 = __builtin_amdgcn_readfirstlane(h.obj);
+            if (RTG_UNI_SHADE && __ballot(h.obj != ob0) == 0ull) {
+                HitRec hu = h;
+                hu.obj = ob0;
+                ret = hit_record<FULL && TEX, RTG_HIT_STORED>(sv, o, d, time, hu, hin.pt, hin.beta, hin.gamma);
+                m = sv.materials[sv.tops[ob0].material - 1];
+            } else {
+                ret = hit_record<FULL && TEX, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+                m = sv.materials[ret.matIndex - 1];
+            }
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (level == 0 && ret.dm == RTG_DECAL_REPLACE_ALL) {          // Scene::Shading Scene.cpp:230-241
                 nd.cr = ret.tc.x; nd.cg = ret.tc.y; nd.cb = ret.tc.z;
             } else {
-                const MaterialDev m = sv.materials[ret.matIndex - 1];
                 int depth = mt.depth;
                 uint64_t p0 = 2 * path, p1 = 2 * path + 1;
                 if (m.type == RTG_MAT_NORMAL || depth <= 0) {            // RecursiveShading Scene.cpp:148-158
