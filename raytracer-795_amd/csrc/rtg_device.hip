@@ -2203,7 +2203,17 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                 kind |= kContrib;
             }
         } else {
-            const Ret ret = hit_record<FULL, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+            // one entry for the whole wave (camera samples on one surface): its records through the
+            // scalar cache (as k_shade)
+            Ret ret;
+            const int ob0 = __builtin_amdgcn_readfirstlane(h.obj);
+            if (RTG_UNI_SHADE && __ballot(h.obj != ob0) == 0ull) {
+                HitRec hu = h;
+                hu.obj = ob0;
+                ret = hit_record<FULL, RTG_HIT_STORED>(sv, o, d, time, hu, hin.pt, hin.beta, hin.gamma);
+            } else {
+                ret = hit_record<FULL, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+            }
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
             if (medium) {                                              // Beer's law inside
@@ -2223,7 +2233,10 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                 nd.cr = ret.tc.x; nd.cg = ret.tc.y; nd.cb = ret.tc.z;
                 kind |= kContrib;
             } else {
-                const MaterialDev m = sv.materials[ret.matIndex - 1];
+                MaterialDev m;
+                const int mi0 = __builtin_amdgcn_readfirstlane(ret.matIndex);
+                if (RTG_UNI_SHADE && __ballot(ret.matIndex != mi0) == 0ull) m = sv.materials[mi0 - 1];
+                else m = sv.materials[ret.matIndex - 1];
                 DielSplit ds;
                 ds.entering = true; ds.tir = false; ds.F = 0.0f;
                 if (m.type == RTG_MAT_DIELECTRIC) ds = dielectric_split(sv, d, ret, m);
