@@ -660,6 +660,12 @@ int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd, const SahBound
     return mid;
 }
 
+// Pass-schedule levels whose shadow queries all walk wave-uniformly (level 0: camera samples; levels
+// 0-1 / 0-2 measured slower on the dragon, k_shadow 10.6 -> 11.3 / 12.4 ms: profiles/r5s_*)
+#ifndef RTG_UNI_SHADOW_LEVELS
+#define RTG_UNI_SHADOW_LEVELS 1
+#endif
+
 // Levels of the SAH recursion whose subtrees get threads of their own (env RTG_SAH_DEPTH, A/B).
 static int sah_depth() {
     static const int d = [] {
@@ -2429,7 +2435,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
         launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
-                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni_from=*/level == 0 ? 0 : INT_MAX);
+                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni_from=*/level < RTG_UNI_SHADOW_LEVELS ? 0 : INT_MAX);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt) {
