@@ -316,6 +316,12 @@ def main():
                     help="render through rtg_render_ranked (RCCL shard + gather) even with one rank")
     ap.add_argument("--tlas", choices=["auto", "off", "on"], default="auto",
                     help="top-level BVH over objects / instances (rtg_build_opts.tlas; auto: from 16 entries)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="HIP streams (lanes) of every frame (rtg_render_opts.streams; 0 = library default). "
+                         "PMC passes use 1 so each dispatch is one pass's launch (scripts/pmc_counters.py)")
+    ap.add_argument("--timeout-s", type=int, default=300,
+                    help="N > 1: bound on every wait for a peer rank (process group set-up, id exchange, "
+                         "librtg's RCCL set-up / failure agreement / gather); a dead peer is an error, not a hang")
     args = ap.parse_args()
     # stdout carries exactly the one JSON line: libraries that print banners there (RCCL's
     # "RCCL version ..." at communicator init) are sent to stderr with everything else
@@ -332,17 +338,22 @@ def main():
     if rehearse:
         local = 0
     torch.cuda.set_device(local)
+    id_group = None
     if world > 1:
+        from datetime import timedelta
+
         import torch.distributed as dist
+        tmo = timedelta(seconds=args.timeout_s)
         if rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
+            id_group = dist.new_group(backend="gloo", timeout=tmo)     # host-side id exchange
 
     import rtg
     from rtg import _abi as rtg_abi
     from rtg import scenegen
-    from rtg.shard import ROW_BLOCK, gather_frame, max_shard_rows, shard_opts
+    from rtg.shard import ROW_BLOCK, exchange_comm_id, gather_frame, max_shard_rows, shard_opts
 
     t0 = time.perf_counter()
     make, spp_default, wl_text, data_text = WORKLOADS[args.workload]
@@ -351,7 +362,7 @@ def main():
     scene = getattr(scenegen, make)(args.width, args.height, spp=args.spp or spp_default)
     log(f"[rank {rank}] scene: {scene.num_triangles()} triangles, gen {time.perf_counter() - t0:.1f}s")
     # The process's first kernel launch pays the HIP runtime's one-time set-up (100-170 ms on MI355X,
-    # profiles/r4i_hip_init_probe_kernel_first.txt: torch's own first fill).  It is timed here on its
+    # profiles/history/r4i_hip_init_probe_kernel_first.txt: torch's own first fill).  It is timed here on its
     # own (end_to_end_ms.runtime_init) so that scene_create is the library's cost in a process whose
     # device is in use, as in any PyTorch program; librtg's own code-object load stays in it.
     torch.cuda.synchronize()
@@ -371,20 +382,22 @@ def main():
     comm = None
     part = None
     if (world > 1 or args.ranked) and not rehearse:
-        # librtg's own RCCL communicator (ncclCommInitRank); its id travels over torch.distributed
-        uid = [rtg.Comm.unique_id() if rank == 0 else None]
-        if dist is not None:
-            dist.broadcast_object_list(uid, src=0)
-        comm = rtg.Comm(uid[0], world, rank, local)
+        # librtg's own RCCL communicator (ncclCommInitRank, non-blocking with a deadline); its id
+        # travels over a gloo group of torch.distributed, bounded by the same timeout
+        uid = exchange_comm_id(dist, rank, rtg.Comm.unique_id, group=id_group) if dist is not None \
+            else rtg.Comm.unique_id()
+        comm = rtg.Comm(uid, world, rank, local, timeout_ms=args.timeout_s * 1000)
     elif world > 1:
         part = torch.zeros((max_shard_rows(cam.ny, world), cam.nx, 3), dtype=torch.float32, device=frame.device)
     sharded = comm is not None or part is not None
 
     def single(buf, **kw):
+        kw.setdefault("streams", args.streams)
         r.render_device(0, buf.data_ptr(), stream, **kw)
         return r.stats()
 
     def step(**kw):
+        kw.setdefault("streams", args.streams)
         if comm is not None:       # shard + RCCL gather inside librtg (rtg_render_ranked)
             r.render_ranked(0, comm, frame.data_ptr(), stream, row_block=ROW_BLOCK, **kw)
         elif part is not None:     # rehearsal: compact shard, gloo gather in Python
@@ -435,11 +448,14 @@ def main():
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        gather_max = st.get("gather_ms", 0.0) if st else 0.0
         if dist is not None:
             dev = frame.device if not rehearse else "cpu"
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            t = torch.tensor([elapsed, gather_max], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+            elapsed, gather_max = float(t[0].item()), float(t[1].item())
+            if st is not None:
+                st = dict(st, gather_ms_max_over_ranks=gather_max)
             rt = torch.tensor([rays], dtype=torch.float64, device=dev)
             dist.all_reduce(rt, op=dist.ReduceOp.SUM)
             rays = int(rt.item())
@@ -466,7 +482,11 @@ def main():
                  "gather": "rehearsal: gloo gather through host memory (all ranks on one GPU)" if rehearse
                  else "RCCL point-to-point rows gather inside librtg (rtg_render_ranked)",
                  "single_device_frame_ms": round(single_ms, 2), "row_block": ROW_BLOCK,
-                 "gather_ms_rank0": round(st.get("gather_ms", 0.0), 3)}
+                 "gather_ms_rank0": round(st.get("gather_ms", 0.0), 3),
+                 "gather_ms_max_over_ranks": round(st.get("gather_ms_max_over_ranks", 0.0), 3),
+                 "gather_note": "per rank: librtg's failure agreement + RCCL rows gather after the rank's shard "
+                                "finished (rtg_render_stats.gather_ms), last timed step",
+                 "timeout_s": args.timeout_s}
         if rehearse and not same:
             raise SystemExit("rehearsal: gathered frame differs from the single-device frame")
         st_stats, st_roof = roofline_frames(full)
@@ -477,7 +497,7 @@ def main():
     if rank == 0:
         # the same scene created again in this process (outside every timed region): the first
         # rtg_scene_create also pays the HIP runtime's one-time first-use set-up, ~100-150 ms for the
-        # first launch / copy of a process (scripts/micro/init_probe.hip, profiles/r4m_init_probe.txt)
+        # first launch / copy of a process (scripts/micro/init_probe.hip, profiles/history/r4m_init_probe.txt)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         r2 = rtg.Renderer(scene, device=local, tlas={"auto": 0, "off": 1, "on": 2}[args.tlas])

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 7
+#define RTG_ABI_VERSION 8
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -250,6 +250,15 @@ typedef struct rtg_render_opts {
        samples (DESIGN.md §4 "Schedules"); max_batch_rays then caps the rays of one step.  Results
        are bit-identical either way. */
     int32_t schedule;
+    /* ABI 8 (these replace the environment knobs of earlier builds; 0 = the library default) */
+    int32_t tile_band;       /* pixel order: bands this many 64-pixel tiles high, walked in columns of
+                                tiles (0 = 16).  Results do not depend on it. */
+    int32_t segment_pixels;  /* stream schedule, path tracer: pixels whose samples' radiance is buffered
+                                per segment (0 = as many as an eighth of the device memory holds) */
+    int32_t segment_nodes;   /* stream schedule, reference integrator: a segment takes no new samples
+                                once its node records exceed this many (0 = a quarter of the device
+                                memory's worth).  Results do not depend on either. */
+    int32_t pad_abi8;
 } rtg_render_opts;
 #define RTG_SCHEDULE_AUTO 0
 #define RTG_SCHEDULE_PASSES 1
@@ -355,10 +364,13 @@ typedef struct rtg_build_opts {
     int32_t tlas;            /* top-level BVH over objects and instances, replacing the reference's
                                 linear object loop (src/Helper.cpp:32-73) with the same result (ties
                                 to the first entry): 0 = auto (>= 16 entries), 1 = off, 2 = on
-                                (>= 2 entries); env RTG_TLAS=0/1 overrides */
+                                (>= 2 entries) */
     int32_t traversal_tree;  /* 0 = fast rays walk an SAH 4-wide tree per mesh (candidates checked for
                                 reachability in the reference tree, ties in its order: same results);
-                                1 = the reference tree only; env RTG_SAH=0/1 overrides */
+                                1 = the reference tree only */
+    /* ABI 8: 0 = waves of camera samples and of their shadow queries walk the traversal tree
+       together (wave-uniform node loads); 1 = every lane walks alone.  Same results. */
+    int32_t uniform_walk;
 } rtg_build_opts;
 /* rtg_scene_create with build options (NULL = defaults). */
 int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rtg_build_opts* opts,
@@ -408,6 +420,12 @@ typedef struct rtg_comm rtg_comm;
 int32_t rtg_comm_unique_id(uint8_t id[RTG_COMM_ID_BYTES]);
 int32_t rtg_comm_init_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
                            rtg_comm** out);
+/* ABI 8: the same with a bound on every wait of the rank (communicator set-up, the failure agreement
+   and the gather of rtg_render_ranked): a rank whose peers do not join within timeout_ms aborts the
+   communicator (ncclCommAbort) and returns RTG_ERR_HIP instead of blocking; the communicator is then
+   unusable (destroy it).  timeout_ms <= 0: 120000.  rtg_comm_init_rank uses the default. */
+int32_t rtg_comm_init_rank_timeout(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
+                                   int32_t timeout_ms, rtg_comm** out);
 int32_t rtg_comm_destroy(rtg_comm* comm);
 int32_t rtg_render_ranked(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_opts* opts, rtg_comm* comm,
                           float* frame_device, void* stream);

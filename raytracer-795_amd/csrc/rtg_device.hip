@@ -20,89 +20,28 @@ namespace rtg {
 // Traversal occupancy.  Round 1: k_shadow 135 -> 128 VGPRs (3 -> 4 waves/SIMD): 32.6 -> 30.9 ms per
 // dragon frame.  Round 3: k_trace / k_shadow at 6 waves per SIMD (80 VGPRs, 16-96 B of spill besides
 // the stack's scratch part), possible since the LDS stack holds 16 entries (rtg_internal.h kLdsStack):
-// dragon 33.0 -> 31.6 ms, cornell_pt 392.8 -> 364.3 ms (profiles/r3_ab_ldsstack.jsonl).
+// dragon 33.0 -> 31.6 ms, cornell_pt 392.8 -> 364.3 ms (profiles/history/r3_ab_ldsstack.jsonl).
 #ifndef RTG_TRAVERSAL_WAVES
 #define RTG_TRAVERSAL_WAVES 6
 #endif
 // the top-level-BVH instantiations (many-entry scenes, LDS also holds their 16-entry top-level
 // stack) keep the previous target: spheres 1080p64 37.3 -> 32.3 ms against 6 waves
-// (profiles/r3_ab_tlaswaves.jsonl)
+// (profiles/history/r3_ab_tlaswaves.jsonl)
 #ifndef RTG_TLAS_WAVES
 #define RTG_TLAS_WAVES 4
 #endif
 #define RTG_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(TLAS ? RTG_TLAS_WAVES : RTG_TRAVERSAL_WAVES)))
 #define RTG_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(TLAS ? RTG_TLAS_WAVES : RTG_TRAVERSAL_WAVES)))
-// k_shadow's certified early exit (closest_hit CERT), off by default: measured on the 1080p64
-// dragon (round 3, scripts/gpu_ab3.sh, same box) it cuts a blocked query's node steps 18.9 ->
-// 14.4 (all queries 8.81 -> 7.93) but k_shadow takes 12.9 instead of 12.4 ms per frame -- the
-// flag bookkeeping costs more per step than the steps it saves.  -DRTG_SHADOW_CERT=1
-// builds it (bit-identical frames: tests/test_gpu_parity.py, test_gpu_fullsize.py).
-#ifndef RTG_SHADOW_CERT
-#define RTG_SHADOW_CERT 0
-#endif
-// Object-level part of the certification alone: after an entry's complete walk, a winner with
-// gett() in (0, tcert] blocks whatever the remaining entries hold, so the object loop stops (no
-// per-step bookkeeping inside the walk).
-#ifndef RTG_SHADOW_CERT_OBJ
-#define RTG_SHADOW_CERT_OBJ 0
-#endif
-// Camera-sample waves of k_trace (level 0) walk the traversal tree wave-uniformly (visit_object).
-#ifndef RTG_UNI_PRIMARY
-#define RTG_UNI_PRIMARY 1
-#endif
-// every wave, every level (timing experiments)
-#ifndef RTG_UNI_ALL
-#define RTG_UNI_ALL 0
-#endif
-// ... and queued rays / shadow queries of waves that are coherent (wave_coherent; A/B switch, off:
-// with cones of 0.02 / 0.05 / 0.15 and boxes of 0.005 / 0.02 / 0.05 (relative) the dragon frame took
-// 30.8 / 30.8 / 31.2 ms against 30.7, cornell_pt 351 / 351 against 348 ms -- profiles/r5n_ab_uniform_adapt.txt)
-#ifndef RTG_UNI_ADAPT
-#define RTG_UNI_ADAPT 0
-#endif
-#ifndef RTG_UNI_DIR
-#define RTG_UNI_DIR 0.05f
-#endif
-#ifndef RTG_UNI_ORG
-#define RTG_UNI_ORG 0.02f
-#endif
-constexpr float kUniDir = RTG_UNI_DIR, kUniOrg = RTG_UNI_ORG;
-// k_shade: waves whose hits share one entry read its records through the scalar cache (A/B switch)
-#ifndef RTG_UNI_SHADE
-#define RTG_UNI_SHADE 1
-#endif
-// ... and k_shadow's queries of level-0 nodes (A/B switch)
-#ifndef RTG_UNI_SHADOW
-#define RTG_UNI_SHADOW 1
-#endif
-// Shading of a flat triangle from its TriGeom record alone (hit_record).
-#ifndef RTG_FLAT_NORMAL
-#define RTG_FLAT_NORMAL 1
-#endif
-// Line test of a transformed entry's world box before its ray transform (closest_hit).
-#ifndef RTG_ENTRY_BOX
-#define RTG_ENTRY_BOX 1
-#endif
-// Window test of an object's root box before its walk (visit_object).
-#ifndef RTG_ROOT_WINDOW
-#define RTG_ROOT_WINDOW 1
-#endif
-// Triangle tests reject a candidate beyond the walk's parameter window (tri_test's thi) before
-// the barycentric determinants and the exact divisions (round 4).
-#ifndef RTG_TRI_WINDOW
-#define RTG_TRI_WINDOW 1
-#endif
-// Object-light shadow queries bounded where the blocking test stops being satisfiable
-// (emit_shadow_tmax) instead of just beyond the light.
-#ifndef RTG_EMIT_TMAX
-#define RTG_EMIT_TMAX 1
-#endif
+// Kept traversal / shading shortcuts (each measured and kept): the wave-uniform walk of
+// camera-sample waves and their shadow queries, uniform-entry record reads in shading, flat-triangle
+// normals from the TriGeom record, entry world boxes, root-box windows, windowed triangle tests and the
+// object-light shadow bound.  Experiments measured and not kept were removed in round 5.
 // k_shade: the full variant (textures / BRDFs / area & environment lights) needs > 256 registers;
 // capped at 2 waves per SIMD it spills 236 B/lane and is still faster (cornell_dynamic 1080p64:
 // 34.0 -> 29.7 ms).
 // The simple variant (point / directional lights, no textures or BRDFs) at 6 waves per SIMD: 90 -> 80
 // VGPRs with an 8-byte spill, dragon k_shade 8.80 -> 7.87 ms per frame (7 waves: 8.6 ms;
-// profiles/r3_ab_shadewaves.jsonl); the spot variant (182 VGPRs) keeps the minimum of 2.
+// profiles/history/r3_ab_shadewaves.jsonl); the spot variant (182 VGPRs) keeps the minimum of 2.
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 6
 #endif
@@ -117,17 +56,15 @@ constexpr float kUniDir = RTG_UNI_DIR, kUniOrg = RTG_UNI_ORG;
 #endif
 // Its block size: 512 threads like the simple variant (256 dated from the 2-wave days).  C4
 // cornell_dynamic 1080p64, streams=1 frame: k_shade 6.04 -> 5.2 ms (three A/B pairs, same box,
-// profiles/r5e_ab_light_block.txt); the 8-lane frame is unchanged (16.5 ms), where its shading
+// profiles/history/r5e_ab_light_block.txt); the 8-lane frame is unchanged (16.5 ms), where its shading
 // overlaps other lanes' traversals.
-#ifndef RTG_SHADE_LIGHT_BLOCK
-#define RTG_SHADE_LIGHT_BLOCK 512
-#endif
+constexpr int kShadeLightBlock = 512;
 #define RTG_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(FULL ? (!SPOT && !TEX ? RTG_SHADE_LIGHT_WAVES : RTG_SHADE_FULL_WAVES) \
                                                             : SPOT ? 2 : RTG_SHADE_WAVES)))
 // k_pt_shade: the simple / BRDF-only variants at 3 waves per SIMD (192 -> 168 VGPRs, 64 B/lane
 // spill): cornell_pt 1080p256 585 -> 576 ms; 4 waves (236 B spill) is slower (594 ms); round 3, with
 // one BRDF call site (167 VGPRs, no spill at 3 waves): 4 waves spill 140-164 B and lose, 398 -> 404
-// ms (profiles/r3_ab_ptwaves.jsonl); the full variants keep the default
+// ms (profiles/history/r3_ab_ptwaves.jsonl); the full variants keep the default
 #ifndef RTG_PT_WAVES
 #define RTG_PT_WAVES 3
 #endif
@@ -136,10 +73,7 @@ constexpr float kUniDir = RTG_UNI_DIR, kUniOrg = RTG_UNI_ORG;
 #define RTG_PT_WAVES_NOTS 3
 #endif
 #define RTG_PT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((!FULL && !SPOT) ? (BRDF == 1 ? RTG_PT_WAVES_NOTS : RTG_PT_WAVES) : 1)))
-#ifndef RTG_PT_BLOCK
-#define RTG_PT_BLOCK 256
-#endif
-constexpr int kPtBlock = RTG_PT_BLOCK;     // k_pt_shade threads per block
+constexpr int kPtBlock = 256;      // k_pt_shade threads per block (128 / 64: slower, r3_ab_ptblock.jsonl)
 constexpr double PI_D = 3.14159265358979323846;
 
 // ------------------------------------------------------------------ vectors (Eigen order)
@@ -313,7 +247,7 @@ struct Cand {           // Triangle::bvhIntersect acceptance + point (src/Shape.
     float beta, gamma, t;
     f3 p;
 };
-// thi (the caller's parameter window, RTG_TRI_WINDOW): a candidate whose t lies beyond it cannot
+// thi (the caller's parameter window, round 4's windowed test): a candidate whose t lies beyond it cannot
 // become the object's winner that matters -- the same bound the traversal's slot boxes are pruned
 // with (visit_object) -- so it may be rejected as well; INFINITY keeps every candidate.
 DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps, float thi = INFINITY) {
@@ -428,20 +362,7 @@ struct Stats { unsigned nodes, tris, steps, entries, considered, cand_step, win_
 // an accepted hit at t <= nearest skipped) instead of the reference's linear loop; an entry
 // replaces the winner iff t < nearest, or t == nearest and it comes earlier in the loop order
 // (objects before instances, lower index first), which is the loop's first-wins rule.
-//
-// CERT (shadow queries, linear object loop): certified early exit.  The caller's decision depends
-// only on the final nearest accepted t (src/Light.cpp:188-204 via src/Helper.cpp:39-49), and every
-// accepted t in (0, tcert] gives "blocked".  Inside an object the reference's winner is the
-// minimal-distance reachable candidate, and it is accepted only if its gett() is > 0: a
-// candidate within eps behind the origin can hide nearer-in-front hits (the t >= -eps acceptance,
-// src/Shape.cpp:330, and the top-level t > 0 test, src/Helper.cpp:41).  So once the object's best candidate so far has gett() in (0, tcert] AND
-// no unexplored subtree can hold a candidate with t <= tau (every remaining subtree's entry key
-// is > tau, where tau bounds gett()'s rounding so that t > tau implies gett() > 0), the object's
-// winner -- the best so far or a nearer unexplored candidate, both with 0 < t <= tcert -- is
-// accepted and the query is blocked, whatever the remaining objects hold.  Stack entries whose
-// key is <= tau carry the sign bit; `nflag` counts them.  out.pad = 1 marks a certified result.
-// bary (optional): the winner's object-space ray parameter and barycentrics (render-path hit records).
-struct HitBary { float pt, beta, gamma; };
+
 // One top-level entry of BVHMethods::FindIntersection's loop (src/Helper.cpp:32-73): the object's
 // winner (closest_hit's comments) and the top-level acceptance against `nearest` / `out`.
 // Traversal stack entry sp of a lane: LDS for the first kLdsStack entries, the lane's scratch array
@@ -454,10 +375,9 @@ DEV int stk_get(const int* stack, int sstride, const int* spill, int sp) {
     return (kLdsStack >= kStackDepth || sp < kLdsStack) ? stack[sp * sstride] : spill[sp - kLdsStack];
 }
 
-template <bool EXHAUSTIVE, bool STATS, bool CERT, bool UNI = false>
+template <bool EXHAUSTIVE, bool STATS, bool UNI = false>
 DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, const float time, const bool fin,
-                      float& nearest, HitRec& out, HitBary* bary, bool& certified, int* stack, int sstride, Stats& st,
-                      const float tcert, int* spill, const bool uni = false) {
+                      float& nearest, HitRec& out, int* stack, int sstride, Stats& st, int* spill, const bool uni = false) {
     const float eps = sv.int_eps;
     const TopObject& T = sv.tops[i];
     const Geometry& g = sv.geoms[T.geom];
@@ -466,9 +386,6 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
     bool found = false;
     int bprim = -1;
     f3 bp = mk(0, 0, 0);
-    // mesh winner's ray parameter and barycentrics, tracked only for the render path's hit records
-    // (bp itself is kept: deriving it from bt at the end of the walk cost k_shadow SGPR spills)
-    float bt = 0.0f, bb = 0.0f, bg = 0.0f;
     if (g.type == RTG_OBJ_SPHERE) {
         if (g.nprims > 0) {
             f3 ip;
@@ -519,21 +436,20 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         // The root box, widened by the eps overhang (win_*), meets the line only outside the window:
         // no candidate of this object can matter (behind the origin, or beyond the winner so far /
         // the shadow query's bound), so the walk would prune every slot of its first node.
-        if (RTG_ROOT_WINDOW && !EXHAUSTIVE && fast && g.win &&
+        if (!EXHAUSTIVE && fast && g.win &&
             !window_meets(o2, inv, g.win_min[0], g.win_min[1], g.win_min[2], g.win_max[0], g.win_max[1], g.win_max[2],
                           tlo, thi))
             return;
         // all primitives of one leaf, ties -> rightmost leaf (larger start), then lower index
         auto test_prim = [&](const TriGeom& tg, int k, int start) {
             if (STATS) st.tris++;
-            Cand c = tri_test(tg, o2, d2, eps, RTG_TRI_WINDOW ? thi : INFINITY);
+            Cand c = tri_test(tg, o2, d2, eps, thi);
             if (c.ok) {
                 float dist = norm(c.p - o2);
                 if (dist < FLT_MAX &&
                     (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))) {
                     best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
                     if (STATS) st.cand_step = st.steps;
-                    if (bary) { bt = c.t; bb = c.beta; bg = c.gamma; }
                     if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                 }
             }
@@ -621,26 +537,11 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             // Exhaustive traversal, rays with a zero / denormal / huge direction component and
             // a stack that would overflow (> kStackDepth entries) use the reference tree's BVH2
             // walk; candidates already accepted stay valid (they are reachable).
-            // the quantised tree also needs moderate coordinates and direction components (every t term
-            // a finite normal float, rtg_internal.h kQCoordMax / kQDirMax)
-            const bool qfast = !RTG_QNODES ||
-                               (adx >= 1.0f / kQDirMax && adx <= kQDirMax && ady >= 1.0f / kQDirMax && ady <= kQDirMax &&
-                                adz >= 1.0f / kQDirMax && adz <= kQDirMax && fabsf(o2.x) < kQCoordMax &&
-                                fabsf(o2.y) < kQCoordMax && fabsf(o2.z) < kQCoordMax);
-            bool use2 = EXHAUSTIVE || !fast || !qfast || g.sah_base < 0;
+            bool use2 = EXHAUSTIVE || !fast || g.sah_base < 0;
             if (!use2) {
-                // CERT: tau bounds gett()'s rounding (4u |o_a| / |d_a|, as the object-loop bound
-                // above) with a 4x margin: a candidate with t > tau has gett() > 0
-                constexpr bool WCERT = CERT && RTG_SHADOW_CERT;   // the walk's part (else object level only)
-                const bool cert_on = WCERT && tcert > 0.0f;
-                const float tau = cert_on ? (16.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * 1.01f + 1e-30f : -INFINITY;
-                // > 0: the best candidate so far has gett() in (0, tcert] (a float, not a lane
-                // mask: SGPRs are the scarce register file of this loop)
-                float best_cert = -1.0f;
-                int nflag = 0;            // stack entries whose key is <= tau (sign bit set)
                 auto test_sah = [&](const TriGeom& tg) {
                     if (STATS) st.tris++;
-                    Cand c = tri_test(tg, o2, d2, eps, RTG_TRI_WINDOW ? thi : INFINITY);
+                    Cand c = tri_test(tg, o2, d2, eps, thi);
                     if (!c.ok) return;
                     const float dist = norm(c.p - o2);
                     const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
@@ -653,14 +554,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     }
                     best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
                     if (STATS) st.cand_step = st.steps;
-                    if (bary) { bt = c.t; bb = c.beta; bg = c.gamma; }
                     if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                    if (WCERT) {
-                        // gett() of a fast ray is its first quotient (d2.x finite, nonzero); a NaN
-                        // compares false (not certified)
-                        const float tg_ = (c.p.x - o2.x) / d2.x;
-                        best_cert = (tg_ > 0 && tg_ * (1.0f + 2e-5f) <= tcert) ? 1.0f : -1.0f;
-                    }
                 };
                 int sp = 0;
                 int cur = g.sah_base;
@@ -748,24 +642,6 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                 } else
                 while (true) {
                     if (STATS) { st.nodes += 4; st.steps++; }   // one node = four 32-B child records (the model's unit)
-#if RTG_QNODES
-                    // 64-byte quantised node: t of slot j's plane q on axis a = fma(q, s_a / d_a, (o_a - O_a) / d_a)
-                    const Node4q nq = sv.qnodes[cur];
-                    const float Ax = (__uint_as_float(nq.a.x) - o2.x) * inv.x;
-                    const float Ay = (__uint_as_float(nq.a.y) - o2.y) * inv.y;
-                    const float Az = (__uint_as_float(nq.a.z) - o2.z) * inv.z;
-                    const float Sx = __uint_as_float((nq.a.w & 0xFFu) << 23) * inv.x;
-                    const float Sy = __uint_as_float(((nq.a.w >> 8) & 0xFFu) << 23) * inv.y;
-                    const float Sz = __uint_as_float(((nq.a.w >> 16) & 0xFFu) << 23) * inv.z;
-                    const int rf[4] = {(int)nq.d.x, (int)nq.d.y, (int)nq.d.z, (int)nq.d.w};
-                    int inf[4];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int b8 = (int)((nq.c.z >> (8 * j)) & 0xFFu);
-                        inf[j] = b8 == 255 ? -1 : b8;
-                    }
-                    auto qb = [](unsigned w, int j) { return (float)((w >> (8 * j)) & 0xFFu); };
-#else
                     const Node4 nd = sv.snodes[cur];
                     const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w};
                     const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w};
@@ -775,20 +651,13 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     const float hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
                     const int rf[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
                     const int inf[4] = {nd.info.x, nd.info.y, nd.info.z, nd.info.w};
-#endif
                     float key[4];
                     int okm = 0, leafm = 0;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-#if RTG_QNODES
-                        const float ax = __builtin_fmaf(qb(nq.b.x, j), Sx, Ax), bx = __builtin_fmaf(qb(nq.b.w, j), Sx, Ax);
-                        const float ay = __builtin_fmaf(qb(nq.b.y, j), Sy, Ay), by = __builtin_fmaf(qb(nq.c.x, j), Sy, Ay);
-                        const float az = __builtin_fmaf(qb(nq.b.z, j), Sz, Az), bz = __builtin_fmaf(qb(nq.c.y, j), Sz, Az);
-#else
                         const float ax = (lx[j] - o2.x) * inv.x, bx = (hx[j] - o2.x) * inv.x;
                         const float ay = (ly[j] - o2.y) * inv.y, by = (hy[j] - o2.y) * inv.y;
                         const float az = (lz[j] - o2.z) * inv.z, bz = (hz[j] - o2.z) * inv.z;
-#endif
                         const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
                         const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
                         const float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
@@ -831,30 +700,14 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
                     const int npush = (r4[1] >= 0) + (r4[2] >= 0) + (r4[3] >= 0);
                     if (sp + npush > kStackDepth) { use2 = true; break; }
-                    // CERT: pushes of subtrees that may hold a candidate with t <= tau carry the
-                    // sign bit (tau = -inf when certification is off: no flags)
-                    auto push = [&](int j) {
-                        if (r4[j] < 0) return;
-                        int e = r4[j];
-                        if (WCERT) {
-                            const bool fl = !(k4[j] > tau);
-                            nflag += fl;
-                            e |= fl ? (int)0x80000000u : 0;
-                        }
-                        stk_put(stack, sstride, spill, sp, e);
-                        sp++;
-                    };
-                    push(3); push(2); push(1);
+                    for (int j = 3; j >= 1; j--)
+                        if (r4[j] >= 0) { stk_put(stack, sstride, spill, sp, r4[j]); sp++; }
                     if (r4[0] >= 0) {
-                        if (WCERT && best_cert > 0.0f && nflag == 0 && k4[0] > tau) break;
                         cur = r4[0];
                     } else {
-                        if (WCERT && best_cert > 0.0f && nflag == 0) break;
                         if (sp == 0) break;
                         sp--;
-                        const int e = stk_get(stack, sstride, spill, sp);
-                        if (WCERT) nflag -= e < 0;
-                        cur = WCERT ? (e & 0x7fffffff) : e;
+                        cur = stk_get(stack, sstride, spill, sp);
                     }
                 }
             }
@@ -874,44 +727,21 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             nearest = t;
             out.obj = i; out.prim = bprim; out.t = t;
             if (STATS) st.win_step = st.cand_step;
-            if (bary) { bary->pt = bt; bary->beta = bb; bary->gamma = bg; }
-        }
-        // the object's winner is this candidate (a complete walk, a sphere) or, after the walk's
-        // early exit, lies in (0, t]: either way the final nearest t is in (0, tcert]
-        if (CERT && t > 0 && t * (1.0f + 2e-5f) <= tcert) {
-            certified = true;
-            out.obj = i; out.prim = bprim; out.t = t; out.pad = 1;
         }
     }
 }
 
-// A wave whose active lanes' rays start within a small box and point within a small cone of its
-// first lane's ray (RTG_UNI_ADAPT: coherent queued rays, e.g. one pixel's reflections off a
-// smooth sphere).  NaN components count as incoherent.
-DEV float rfl(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-DEV bool wave_coherent(f3 o, f3 d) {
-    const f3 o0 = mk(rfl(o.x), rfl(o.y), rfl(o.z)), d0 = mk(rfl(d.x), rfl(d.y), rfl(d.z));
-    const float ds = fmaxf(fmaxf(fabsf(d0.x), fabsf(d0.y)), fabsf(d0.z));
-    const float os = fmaxf(fmaxf(fabsf(o0.x), fabsf(o0.y)), fabsf(o0.z)) + 1.0f;
-    const float dd = fmaxf(fmaxf(fabsf(d.x - d0.x), fabsf(d.y - d0.y)), fabsf(d.z - d0.z));
-    const float od = fmaxf(fmaxf(fabsf(o.x - o0.x), fabsf(o.y - o0.y)), fabsf(o.z - o0.z));
-    const bool ok = dd <= kUniDir * ds && od <= kUniOrg * os;
-    return __ballot(!ok) == 0ull;
-}
-
-template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool CERT = false, bool UNI = false>
+template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool UNI = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
-                       short* tstack = nullptr, float tcert = -INFINITY, HitBary* bary = nullptr, bool uni = false) {
+                       short* tstack = nullptr, bool uni = false) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
     float nearest = tmax;
-    bool certified = false;
     const bool fin = ray_finite(o, d, time);
     int spill[kStackDepth > kLdsStack ? kStackDepth - kLdsStack : 1];
     auto visit = [&](const int i) {
-        visit_object<EXHAUSTIVE, STATS, CERT, UNI>(sv, i, o, d, time, fin, nearest, out, bary, certified, stack, sstride,
-                                                   st, tcert, spill, uni);
+        visit_object<EXHAUSTIVE, STATS, UNI>(sv, i, o, d, time, fin, nearest, out, stack, sstride, st, spill, uni);
     };
     const float adx = fabsf(d.x), ady = fabsf(d.y), adz = fabsf(d.z);
     const bool wfast = adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f;
@@ -923,7 +753,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {   // wfast is per lane: the others walk on
         for (int i = 0; i < sv.num_tops; i++) {
             if (STATS) st.considered++;
-            if (RTG_ENTRY_BOX && !EXHAUSTIVE && sv.tops[i].wbox && wfast && tin) {
+            if (!EXHAUSTIVE && sv.tops[i].wbox && wfast && tin) {
                 const TopObject& T = sv.tops[i];
                 const f3 wi = mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
                 const float ax = (T.wlo[0] - o.x) * wi.x, bx = (T.whi[0] - o.x) * wi.x;
@@ -936,7 +766,6 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
             }
             if (STATS) st.entries++;
             visit(i);
-            if (CERT && certified) break;
         }
         return out;
     }
@@ -1222,12 +1051,8 @@ DEV void triangle_texture(const SceneView& sv, const Geometry& g, int4 vi, f3 e1
 // object-space intersection (identical arithmetic), texturing, then the top-level
 // world point and TransformNormal (src/Helper.cpp:39-77).
 // FULL = false: the scene has no textures (the host checks), so texturing is compiled out.
-// STORED: the render path -- the winner's ray parameter pt and barycentrics come from k_trace's
-// hit record (HitPlanes), so the point o2 + d2 pt and the normal are rebuilt without re-running the
-// test (identical operands and operations, so identical bits).
-template <bool FULL = true, bool STORED = false>
-DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h, float pt = 0.0f, float beta = 0.0f,
-                   float gamma = 0.0f) {
+template <bool FULL = true>
+DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h) {
     const TopObject& T = sv.tops[h.obj];
     const Geometry& g = sv.geoms[T.geom];
     f3 o2, d2;
@@ -1244,7 +1069,7 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h,
         f3 pc = ip - ld3(g.center);
         ret.normal = pc / norm(pc);
         if (FULL) sphere_texture(sv, g, ret);
-    } else if (RTG_FLAT_NORMAL && !FULL && !STORED && !(g.type == RTG_OBJ_TRIANGLE || g.smooth)) {
+    } else if (!FULL && !(g.type == RTG_OBJ_TRIANGLE || g.smooth)) {
         // flat triangle, no texturing: the normal from the record's a - b and c - b (prim_idx.w is
         // the object's smooth flag, 1 for Triangle objects: Shape.cpp:262-276), no vertex loads
         const TriGeom tg = sv.tris[h.prim];
@@ -1254,17 +1079,9 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h,
         ret.point = c.p;
     } else {
         int4 vi = sv.prim_idx[h.prim];
-        Cand c;
-        f3 a;
-        if (STORED) {
-            c.beta = beta; c.gamma = gamma; c.t = pt;
-            c.p = o2 + d2 * pt;
-            a = ld3(sv.vertices + 3 * (vi.x - 1));
-        } else {
-            const TriGeom tg = sv.tris[h.prim];
-            c = tri_test(tg, o2, d2, sv.int_eps);
-            a = mk(tg.p0.x, tg.p0.y, tg.p0.z);
-        }
+        const TriGeom tg = sv.tris[h.prim];
+        const Cand c = tri_test(tg, o2, d2, sv.int_eps);
+        const f3 a = mk(tg.p0.x, tg.p0.y, tg.p0.z);
         f3 b = ld3(sv.vertices + 3 * (vi.y - 1)), cc = ld3(sv.vertices + 3 * (vi.z - 1));
         f3 normal;
         if (vi.w) {
@@ -1598,7 +1415,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     if ((mode == 1.0f || mode == 2.0f) && (__float_as_uint(c.x) | __float_as_uint(c.y) | __float_as_uint(c.z)) == 0u)
         mode = 0.0f;
     if (mode == 1.0f || mode == 3.0f) tmax = shadow_tmax(origin, ret.point, lp, sv.shadow_eps);
-    if (RTG_EMIT_TMAX && mode == 3.0f) tmax = fminf(tmax, emit_shadow_tmax(origin, ret.point, lp, dir, sv.shadow_eps));
+    if (mode == 3.0f) tmax = fminf(tmax, emit_shadow_tmax(origin, ret.point, lp, dir, sv.shadow_eps));
     sr.o = make_float4(origin.x, origin.y, origin.z, time);
     sr.d = make_float4(dir.x, dir.y, dir.z, tmax);
     sr.c = make_float4(c.x, c.y, c.z, mode);
@@ -1704,20 +1521,15 @@ DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int
     o_out = o; d_out = d; time_out = time;
 }
 
-// Render-path hit records (HitPlanes): k_shade / k_pt_shade rebuild the hit from (object,
-// primitive, ray parameter[, barycentrics]) -- 12 or 20 bytes per ray instead of the 16-byte HitRec
-// of the rtg_trace_closest path plus a 48-byte TriGeom re-read.
-struct HitIn { HitRec h; float pt, beta, gamma; };
-DEV HitIn load_hit_planes(const SceneView& sv, const HitRec* hits, int n, int i) {
+// Render-path hit records: 8 bytes per ray, (object, primitive); k_shade / k_pt_shade rebuild the
+// hit by re-running the winning test (hit_record) -- cheaper than storing and gathering its ray
+// parameter and barycentrics (DESIGN.md §4 "hit records").
+struct HitIn { HitRec h; };
+DEV HitIn load_hit_planes(const HitRec* hits, int n, int i) {
     const HitPlanes hp = hit_planes(const_cast<HitRec*>(hits), n);
     const int2 v = hp.id[i];
     HitIn r;
     r.h.obj = v.x; r.h.prim = v.y; r.h.t = 0.0f; r.h.pad = 0;
-    r.pt = 0.0f; r.beta = 0.0f; r.gamma = 0.0f;
-    if (RTG_HIT_STORED && v.x >= 0) {
-        r.pt = hp.pt[i];
-        if (sv.bary) { const float2 bg = hp.bg[i]; r.beta = bg.x; r.gamma = bg.y; }
-    }
     return r;
 }
 
@@ -1757,21 +1569,13 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
             load_ray(rays, i, o, d, time);
             tmax = FLT_MAX;
         }
-        HitBary hb = {0.0f, 0.0f, 0.0f};
         // a wave of camera samples only (a pixel's samples, or adjacent pixels'): the wave-uniform walk
-        constexpr bool KUNI = (GEN || RTG_UNI_ALL || RTG_UNI_ADAPT) && !TLAS && !EXHAUSTIVE && RTG_UNI_PRIMARY;
-        const bool uni = KUNI && sv.uni_walk && (RTG_UNI_ALL || (GEN && (int)(blockIdx.x * blockDim.x) >= nq) ||
-                                                 (RTG_UNI_ADAPT && wave_coherent(o, d)));
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, false, KUNI>(
-            sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st, s_tstack + (TLAS ? threadIdx.x : 0), -INFINITY,
-            RTG_HIT_STORED ? &hb : nullptr, uni);
+        constexpr bool KUNI = GEN && !TLAS && !EXHAUSTIVE;
+        const bool uni = KUNI && sv.uni_walk && (int)(blockIdx.x * blockDim.x) >= nq;
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KUNI>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st,
+                                                             s_tstack + (TLAS ? threadIdx.x : 0), uni);
         if (compact) {
-            const HitPlanes hp = hit_planes(hits, n);
-            hp.id[i] = make_int2(h.obj, h.prim);
-            if (RTG_HIT_STORED) {
-                hp.pt[i] = hb.pt;
-                if (sv.bary) hp.bg[i] = make_float2(hb.beta, hb.gamma);
-            }
+            hit_planes(hits, n).id[i] = make_int2(h.obj, h.prim);
         } else {
             hits[i] = h;
         }
@@ -1835,7 +1639,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                    int n, const HitIn& hin, const f3 o, const f3 d, const float time, const RayMeta& mt,
                    const NodePlanes& nodes, const ShadowPlanes& shadows, int* __restrict__ slist,
                    const RayQ& next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount,
-                   int* __restrict__ rlist, unsigned* rcount, unsigned char* __restrict__ lv_out) {
+                   unsigned char* __restrict__ lv_out) {
     const HitRec& h = hin.h;
     int nchild = 0;
     QRay c0r, c1r;
@@ -1872,13 +1676,13 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
             Ret ret;
             MaterialDev m;
             const int ob0 = __builtin_amdgcn_readfirstlane(h.obj);
-            if (RTG_UNI_SHADE && __ballot(h.obj != ob0) == 0ull) {
+            if (__ballot(h.obj != ob0) == 0ull) {
                 HitRec hu = h;
                 hu.obj = ob0;
-                ret = hit_record<FULL && TEX, RTG_HIT_STORED>(sv, o, d, time, hu, hin.pt, hin.beta, hin.gamma);
+                ret = hit_record<FULL && TEX>(sv, o, d, time, hu);
                 m = sv.materials[sv.tops[ob0].material - 1];
             } else {
-                ret = hit_record<FULL && TEX, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+                ret = hit_record<FULL && TEX>(sv, o, d, time, h);
                 m = sv.materials[ret.matIndex - 1];
             }
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
@@ -1984,31 +1788,26 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
     // totals combined in LDS, ONE 64-bit atomic per block on the level's queue counter
     // (low word: rays, high word: shadow entries).  Same-address atomics serialise at the L2
     // (~11 ns each), so they are kept to one per block.
-    __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64], s_wr[BLOCK / 64];
+    __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64];
     __shared__ unsigned long long s_base;
-    __shared__ unsigned s_rbase;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long lt = __lanemask_lt();
     const unsigned long long m1 = __ballot(nchild >= 1), m2 = __ballot(nchild >= 2);
     const unsigned coff = __popcll(m1 & lt) + __popcll(m2 & lt);
-    // non-final nodes of levels >= 1: the list k_resolve walks (level 0 resolves in k_accumulate)
-    const unsigned long long mr = __ballot(RTG_RESOLVE_LIST && level > 0 && i < n && (nd.kind & 0xFF) != NK_FINAL);
     unsigned stot = 0;
     for (int li = 0; li < sv.num_lights; li++) stot += __popcll(__ballot((smask >> li) & 1ull));
-    if (lane == 0) { s_wc[w] = __popcll(m1) + __popcll(m2); s_ws[w] = stot; s_wr[w] = __popcll(mr); }
+    if (lane == 0) { s_wc[w] = __popcll(m1) + __popcll(m2); s_ws[w] = stot; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned c = 0, sh = 0, rr = 0;
+        unsigned c = 0, sh = 0;
         for (int k = 0; k < BLOCK / 64; k++) {
-            const unsigned a = s_wc[k], b = s_ws[k], e = s_wr[k];
-            s_wc[k] = c; s_ws[k] = sh; s_wr[k] = rr;
-            c += a; sh += b; rr += e;
+            const unsigned a = s_wc[k], b = s_ws[k];
+            s_wc[k] = c; s_ws[k] = sh;
+            c += a; sh += b;
         }
         s_base = (c | sh) ? atomicAdd(qcount, ((unsigned long long)sh << 32) | c) : 0ull;
-        s_rbase = rr ? atomicAdd(rcount, rr) : 0u;
     }
     __syncthreads();
-    if ((mr >> lane) & 1ull) rlist[s_rbase + s_wr[w] + __popcll(mr & lt)] = i;
     int idx = (int)((unsigned)s_base + s_wc[w] + coff);
     if (i < n) {
         auto put_ray = [&](int k, const QRay& rr, const RayMeta& mm) {
@@ -2065,20 +1864,18 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
                                                const HitRec* __restrict__ hits, const NodePlanes nodes,
                                                const ShadowPlanes shadows, int* __restrict__ slist,
                                                const RayQ next_rays, RayMeta* __restrict__ next_meta,
-                                               unsigned long long* qcount, int* __restrict__ rlist,
-                                               unsigned* rcount, int n, int nq, int gbase,
+                                               unsigned long long* qcount, int n, int nq, int gbase,
                                                const unsigned char* __restrict__ lv_in,
                                                unsigned char* __restrict__ lv_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     HitIn h;
     h.h.obj = -1; h.h.prim = -1; h.h.t = 0.0f; h.h.pad = 0;
-    h.pt = h.beta = h.gamma = 0.0f;
     f3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     float time = 0.0f;
     RayMeta mt = {};
     int level = level_in;
     if (i < n) {
-        h = load_hit_planes(sv, hits, n, i);
+        h = load_hit_planes(hits, n, i);
         if (GEN && i >= nq) {
             const int slot = gbase + (i - nq);
             primary_ray(cam, ps, seed, slot, o, d, time);
@@ -2091,7 +1888,7 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
         }
     }
     shade_ray<FULL, SPOT, BLOCK, TEX>(sv, cam, level, ps, seed, i, n, h, o, d, time, mt, nodes, shadows, slist,
-                                      next_rays, next_meta, qcount, rlist, rcount, lv_out);
+                                      next_rays, next_meta, qcount, lv_out);
 }
 
 // ------------------------------------------------------------------ hw7 path tracer
@@ -2173,7 +1970,7 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
             mt.slot = reinterpret_cast<const int*>(meta)[i];
             mt.path_lo = (unsigned)level + 1u; mt.path_hi = 0u; mt.depth = sv.max_depth - level;
         }
-        const HitIn hin = load_hit_planes(sv, hits, n, i);
+        const HitIn hin = load_hit_planes(hits, n, i);
         const HitRec& h = hin.h;
         uint32_t pixel, sample;
         int x, y;
@@ -2207,12 +2004,12 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
             // scalar cache (as k_shade)
             Ret ret;
             const int ob0 = __builtin_amdgcn_readfirstlane(h.obj);
-            if (RTG_UNI_SHADE && __ballot(h.obj != ob0) == 0ull) {
+            if (__ballot(h.obj != ob0) == 0ull) {
                 HitRec hu = h;
                 hu.obj = ob0;
-                ret = hit_record<FULL, RTG_HIT_STORED>(sv, o, d, time, hu, hin.pt, hin.beta, hin.gamma);
+                ret = hit_record<FULL>(sv, o, d, time, hu);
             } else {
-                ret = hit_record<FULL, RTG_HIT_STORED>(sv, o, d, time, h, hin.pt, hin.beta, hin.gamma);
+                ret = hit_record<FULL>(sv, o, d, time, h);
             }
             nd.px = ret.point.x; nd.py = ret.point.y; nd.pz = ret.point.z;
             nd.material = ret.matIndex;
@@ -2235,7 +2032,7 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
             } else {
                 MaterialDev m;
                 const int mi0 = __builtin_amdgcn_readfirstlane(ret.matIndex);
-                if (RTG_UNI_SHADE && __ballot(ret.matIndex != mi0) == 0ull) m = sv.materials[mi0 - 1];
+                if (__ballot(ret.matIndex != mi0) == 0ull) m = sv.materials[mi0 - 1];
                 else m = sv.materials[ret.matIndex - 1];
                 DielSplit ds;
                 ds.entering = true; ds.tir = false; ds.F = 0.0f;
@@ -2439,48 +2236,17 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             return lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f)
                          : ld(reinterpret_cast<const float*>(shadows.c + idx) + 3);
         };
-        // Certified early exit (closest_hit CERT): every accepted t in (0, tcert] blocks.  With
-        // hp = o + d t, |p - hp| <= |o - p| + t |d| (|d| = 1 up to rounding), so the distance test
-        // |p - L| > |p - hp| (mode 1) or |p - hp| < dl - (eps + 1e-4 dl) (mode 3) holds for every
-        // t <= tcert below, margins (1e-5 relative) far above the rounding of both sides;
-        // directional / environment queries (mode 2) are blocked by any accepted hit.
-        float tcert = -INFINITY;
-        constexpr bool KCERT = (RTG_SHADOW_CERT || RTG_SHADOW_CERT_OBJ) && !EXHAUSTIVE && !TLAS;
-        if (KCERT) {
-            const float m0 = query_mode();
-            if (m0 == 2.0f) {
-                tcert = INFINITY;
-            } else if (m0 == 1.0f || m0 == 3.0f) {
-                f3 pq, lq;
-                const float4 pf = nodes.pnt[i];
-                pq = mk(pf.x, pf.y, pf.z);
-                if (lean) {
-                    lq = ld3(sv.lights[0].pos);
-                } else {
-                    const float4 lf = shadows.L[idx];
-                    lq = mk(lf.x, lf.y, lf.z);
-                }
-                const float dl = norm(pq - lq);
-                const float lim = m0 == 1.0f ? dl : dl - (sv.shadow_eps + 1e-4f * dl);
-                const float op = norm(o - pq);
-                const float tc = (lim * (1.0f - 1e-5f) - op * (1.0f + 1e-5f) - 1e-6f * (op + dl)) * (1.0f - 1e-5f);
-                if (tc > 0.0f) tcert = tc;
-            }
-        }
         // queries of camera-sample nodes (nodes >= uni_from: level 0 of a pass, a stream step's new
         // samples): a wave whose queries all leave such nodes -- neighbouring points of one or two
         // pixels -- walks wave-uniformly (visit_object)
-        constexpr bool KUNI = RTG_UNI_SHADOW && !EXHAUSTIVE && !TLAS && !KCERT;
-        const bool uni = KUNI && sv.uni_walk &&
-                         (RTG_UNI_ALL || __ballot(i < uni_from) == 0ull || (RTG_UNI_ADAPT && wave_coherent(o, d)));
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KCERT, KUNI>(
-            sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax, s_stack + threadIdx.x, kTraceBlock, st,
-            s_tstack + (TLAS ? threadIdx.x : 0), tcert, nullptr, uni);
+        constexpr bool KUNI = !EXHAUSTIVE && !TLAS;
+        const bool uni = KUNI && sv.uni_walk && __ballot(i < uni_from) == 0ull;
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KUNI>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax,
+                                                             s_stack + threadIdx.x, kTraceBlock, st,
+                                                             s_tstack + (TLAS ? threadIdx.x : 0), uni);
         const float mode = query_mode();
         bool blocked;
-        if (h.pad == 1) {
-            blocked = true;                     // certified by the early exit
-        } else if (mode == 1.0f || mode == 3.0f) {
+        if (mode == 1.0f || mode == 3.0f) {
             blocked = false;
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
@@ -2658,12 +2424,11 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
 }
 
 // One level of the bottom-up pass (levels >= 1; level 0 is resolved inside k_accumulate).
-// One thread per non-final node of the level (k_shade's compacted list; final nodes are not read).
+// One thread per node of the level; final nodes only read their colour's kind word.
 __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodePlanes nodes, const NodePlanes child,
-                                                 const int* __restrict__ rlist, const unsigned* rcount, int n) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= (RTG_RESOLVE_LIST ? (int)*rcount : n)) return;
-    const int i = RTG_RESOLVE_LIST ? rlist[j] : j;
+                                                 int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
     const float4 nc = nodes.col[i];
     if ((__float_as_int(nc.w) & 0xFF) == NK_FINAL) return;
     const f3 res = resolve_node(sv, nc, i, nodes, child);
@@ -2811,7 +2576,7 @@ void device_warm(hipStream_t st) { hipLaunchKernelGGL(k_warm, dim3(1), dim3(64),
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                   const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
-                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st,
+                  unsigned long long* qcount, int n, hipStream_t st,
                   int gen, int nq, int gbase, const unsigned char* lv_in, unsigned char* lv_out) {
     if (n <= 0) return;
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
@@ -2822,17 +2587,17 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
     do {                                                                                                          \
         if (G)                                                                                                    \
             hipLaunchKernelGGL((k_shade<F, S, B, T, true>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
-                               slist, next_rays, next_meta, qcount, rlist, rcount, n, nq, gbase, lv_in, lv_out); \
+                               slist, next_rays, next_meta, qcount, n, nq, gbase, lv_in, lv_out); \
         else                                                                                                      \
             hipLaunchKernelGGL((k_shade<F, S, B, T, false>), gr, bl, 0, st, sv, cam, level, ps, seed, rays, meta, hits, np, sp, \
-                               slist, next_rays, next_meta, qcount, rlist, rcount, n, nq, gbase, lv_in, lv_out); \
+                               slist, next_rays, next_meta, qcount, n, nq, gbase, lv_in, lv_out); \
     } while (0)
     // full variants: SPOT = a spot or environment light (their libm code compiled in)
     if (sv.full && sv.tex && sv.heavy) RTG_SHADE(true, true, 256, true, dim3(nblk(n, 256)), dim3(256));
     else if (sv.full && sv.tex) RTG_SHADE(true, false, 256, true, dim3(nblk(n, 256)), dim3(256));
     else if (sv.full && sv.heavy) RTG_SHADE(true, true, 256, false, dim3(nblk(n, 256)), dim3(256));
     else if (sv.full)
-        RTG_SHADE(true, false, RTG_SHADE_LIGHT_BLOCK, false, dim3(nblk(n, RTG_SHADE_LIGHT_BLOCK)), dim3(RTG_SHADE_LIGHT_BLOCK));
+        RTG_SHADE(true, false, kShadeLightBlock, false, dim3(nblk(n, kShadeLightBlock)), dim3(kShadeLightBlock));
     else if (sv.spot) RTG_SHADE(false, true, kShadeBlock, false, g, b);
     else RTG_SHADE(false, false, kShadeBlock, false, g, b);
 #undef RTG_SHADE
@@ -2892,16 +2657,15 @@ void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRe
                        node_planes(rad, n_rad), nq, n);
 }
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
-                    const int* rlist, const unsigned* rcount, hipStream_t st) {
+                    hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_resolve, dim3(nblk(n, 256)), dim3(256), 0, st, sv, node_planes(nodes, n),
-                       node_planes(const_cast<NodeRec*>(child_nodes), n_child), rlist, rcount, n);
+                       node_planes(const_cast<NodeRec*>(child_nodes), n_child), n);
 }
 void launch_resolve_planes(const SceneView& sv, const NodePlanes& self, const NodePlanes& child, int count,
                            hipStream_t st) {
     if (count <= 0) return;
-    hipLaunchKernelGGL(k_resolve, dim3(nblk(count, 256)), dim3(256), 0, st, sv, self, child, (const int*)nullptr,
-                       (const unsigned*)nullptr, count);
+    hipLaunchKernelGGL(k_resolve, dim3(nblk(count, 256)), dim3(256), 0, st, sv, self, child, count);
 }
 void launch_accumulate_planes(const SceneView& sv, const NodePlanes& level0, const NodePlanes& level1, bool resolve,
                               float* acc, const PassDev& ps, int nx, int mode, hipStream_t st) {

@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <new>
 #include <string>
 #include <deque>
@@ -240,8 +242,7 @@ template <class T> using hvec = std::vector<T, NoInit<T>>;
 // so per-chunk partial results combine deterministically.  Exceptions reach the caller.
 inline int build_threads() {
     static const int n = [] {
-        int t = (int)std::thread::hardware_concurrency();
-        if (const char* e = getenv("RTG_BUILD_THREADS")) t = atoi(e);
+        const int t = (int)std::thread::hardware_concurrency();
         return std::max(1, std::min(16, t));
     }();
     return n;
@@ -283,6 +284,7 @@ struct BuildCtx {
     hvec<int>* prims;             // current permutation
     hvec<HNode>* nodes;
     std::vector<float> scratch;
+    bool finite = true;           // every primitive box coordinate is finite (construct_par's chunked boxes)
 };
 
 void range_box(BuildCtx& B, int start, int end, float mn[3], float mx[3]) {   // ComputeBoundingBox BVH.cpp:268-283
@@ -345,8 +347,11 @@ int construct(BuildCtx& B, int start, int end, int splitType, int depth) {
 // threads, each into its own pre-order node array (its own BuildCtx), appended left then right with
 // their child numbers shifted: the same permutation and the same pre-order nodes as the recursion
 // (the two halves partition disjoint ranges of the permutation).  The top node's box is reduced in
-// parallel (min / max are exact in any order); the median selection and the reference's swap
-// partition stay sequential -- they define the permutation.
+// parallel when every coordinate is finite (min / max of finite floats are exact in any order, and
+// min2 / max2 keep the first of equal values in both forms); otherwise sequentially, since the
+// reference's fold (ComputeBoundingBox, BVH.cpp:268-283, `a <= b ? a : b`) drops everything before the
+// last NaN, which a merge of per-chunk results does not reproduce.  The median selection and the
+// reference's swap partition stay sequential -- they define the permutation.
 int construct_par(BuildCtx& B, int start, int end, int splitType, int depth, int pdepth) {
     if (pdepth <= 0 || end - start < (1 << 16) || start == end - 1 || depth >= 30) return construct(B, start, end, splitType, depth);
     if (splitType > 2) splitType = 0;
@@ -355,15 +360,19 @@ int construct_par(BuildCtx& B, int start, int end, int splitType, int depth, int
         HNode h;
         h.left = h.right = -1; h.start = start; h.end = end;
         const int len = end - start;
-        std::vector<std::array<float, 6>> part(build_threads());
-        const int T = parallel_chunks((size_t)len, 1 << 15, [&](int ch, size_t k0, size_t k1) {
-            float mn[3], mx[3];
-            range_box(B, start + (int)k0, start + (int)k1, mn, mx);
-            part[ch] = {mn[0], mn[1], mn[2], mx[0], mx[1], mx[2]};
-        });
-        for (int z = 0; z < 3; z++) { h.mn[z] = part[0][z]; h.mx[z] = part[0][3 + z]; }
-        for (int c = 1; c < T; c++)
-            for (int z = 0; z < 3; z++) { h.mn[z] = min2(h.mn[z], part[c][z]); h.mx[z] = max2(h.mx[z], part[c][3 + z]); }
+        if (!B.finite) {
+            range_box(B, start, end, h.mn, h.mx);
+        } else {
+            std::vector<std::array<float, 6>> part(build_threads());
+            const int T = parallel_chunks((size_t)len, 1 << 15, [&](int ch, size_t k0, size_t k1) {
+                float mn[3], mx[3];
+                range_box(B, start + (int)k0, start + (int)k1, mn, mx);
+                part[ch] = {mn[0], mn[1], mn[2], mx[0], mx[1], mx[2]};
+            });
+            for (int z = 0; z < 3; z++) { h.mn[z] = part[0][z]; h.mx[z] = part[0][3 + z]; }
+            for (int c = 1; c < T; c++)
+                for (int z = 0; z < 3; z++) { h.mn[z] = min2(h.mn[z], part[c][z]); h.mx[z] = max2(h.mx[z], part[c][3 + z]); }
+        }
         B.nodes->push_back(h);
     }
     int* p = B.prims->data();
@@ -387,7 +396,7 @@ int construct_par(BuildCtx& B, int start, int end, int splitType, int depth, int
         }
     }
     hvec<HNode> L, R;
-    BuildCtx BL{B.centers, B.bmin, B.bmax, B.prims, &L, {}}, BR{B.centers, B.bmin, B.bmax, B.prims, &R, {}};
+    BuildCtx BL{B.centers, B.bmin, B.bmax, B.prims, &L, {}, B.finite}, BR{B.centers, B.bmin, B.bmax, B.prims, &R, {}, B.finite};
     int l = -1, r = -1;
     std::exception_ptr err;
     std::thread t([&] {
@@ -437,17 +446,9 @@ struct SahNode2 {
 
 constexpr int kSahBins = 16;
 constexpr int kSahMaxLeaf = 4;
-#ifndef RTG_WIN_MIN_PRIMS
-#define RTG_WIN_MIN_PRIMS 1
-#endif
-constexpr int kWinMinPrims = RTG_WIN_MIN_PRIMS;   // Geometry::win threshold
-#ifndef RTG_FLAT_MAX
-#define RTG_FLAT_MAX 8
-#endif
-constexpr int kFlatMaxPrims = RTG_FLAT_MAX;       // Geometry::flat_count: meshes tested without a node
-#ifndef RTG_FLAT_REF
-#define RTG_FLAT_REF 1                             // ... including a reference root over two leaves
-#endif
+constexpr int kWinMinPrims = 1;    // Geometry::win threshold (64: dragon 34.7 -> 35.2 ms, r3_ab_window.jsonl)
+constexpr int kFlatMaxPrims = 8;   // Geometry::flat_count: meshes tested without a node (incl. a reference
+                                   // root over two leaves)
 
 inline double sah_area(const float lo[3], const float hi[3]) {
     const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
@@ -661,19 +662,12 @@ int sah_split(SahRec* r, SahRec* tmp, int s, int e, SahNode2& nd, const SahBound
 }
 
 // Pass-schedule levels whose shadow queries all walk wave-uniformly (level 0: camera samples; levels
-// 0-1 / 0-2 measured slower on the dragon, k_shadow 10.6 -> 11.3 / 12.4 ms: profiles/r5s_*)
-#ifndef RTG_UNI_SHADOW_LEVELS
-#define RTG_UNI_SHADOW_LEVELS 1
-#endif
+// 0-1 / 0-2 measured slower on the dragon, k_shadow 10.6 -> 11.3 / 12.4 ms: profiles/history/r5s_*)
+constexpr int kUniShadowLevels = 1;
 
-// Levels of the SAH recursion whose subtrees get threads of their own (env RTG_SAH_DEPTH, A/B).
-static int sah_depth() {
-    static const int d = [] {
-        const char* e = getenv("RTG_SAH_DEPTH");
-        return e ? std::max(0, std::min(8, atoi(e))) : 6;   // 4 / 5 / 6: second creation 136-147 / 121-153 / 120-128 ms
-    }();
-    return d;
-}
+// Levels of the SAH recursion whose subtrees get threads of their own (4 / 5 / 6: second creation
+// 136-147 / 121-153 / 120-128 ms on one box).
+static int sah_depth() { return 6; }
 
 // Binned SAH BVH2 over [s, e), nodes appended depth first (node, left subtree, right subtree).
 int sah_rec(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out, const SahBounds* pre = nullptr) {
@@ -849,72 +843,6 @@ int sah_collapse_par(const std::vector<SahNode2>& bn, int n, int tri_base, float
     return me;
 }
 
-// Node4 -> Node4q (rtg_internal.h).  Per axis: step s = the smallest power of 2 with
-// s >= extent / 251, s >= max|coordinate| * 2^-21 (the device's float rounding stays far below one
-// step) and s >= 2^-60; origin = (float) <= min - 2 s; then each slot's plane is rounded outwards to
-// the grid and moved one further step out: qlo = floor((lo - origin) / s) - 1,
-// qhi = ceil((hi - origin) / s) + 1 (exact in double: the values are floats, s a power of 2).
-// That extra step covers the device's error in t = fma(q, s / d, (origin - O) / d), which is below
-// 4 ulp of |t| + 255 |s / d| (the 2^-20 relative margin of the slab test covers the first term, the
-// step the second).  False when a coordinate is not finite, exceeds kQCoordMax or needs a step
-// beyond 2^50: the mesh then keeps the reference-tree walk.
-bool quantize_node4(const Node4& n, Node4q& out) {
-    const float lo[3][4] = {{n.lox.x, n.lox.y, n.lox.z, n.lox.w}, {n.loy.x, n.loy.y, n.loy.z, n.loy.w},
-                            {n.loz.x, n.loz.y, n.loz.z, n.loz.w}};
-    const float hi[3][4] = {{n.hix.x, n.hix.y, n.hix.z, n.hix.w}, {n.hiy.x, n.hiy.y, n.hiy.z, n.hiy.w},
-                            {n.hiz.x, n.hiz.y, n.hiz.z, n.hiz.w}};
-    const int info[4] = {n.info.x, n.info.y, n.info.z, n.info.w};
-    uint32_t w[16] = {};
-    uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0}, inf8 = 0, exps = 0;
-    for (int j = 0; j < 4; j++) {
-        const uint32_t b = info[j] < 0 ? 255u : (uint32_t)info[j];
-        if (info[j] > 254) return false;
-        inf8 |= b << (8 * j);
-    }
-    for (int z = 0; z < 3; z++) {
-        double mn = 1e300, mx = -1e300;
-        for (int j = 0; j < 4; j++) {
-            if (info[j] < 0) continue;
-            if (!std::isfinite(lo[z][j]) || !std::isfinite(hi[z][j])) return false;
-            if (std::fabs(lo[z][j]) > kQCoordMax || std::fabs(hi[z][j]) > kQCoordMax) return false;
-            mn = std::min(mn, (double)lo[z][j]);
-            mx = std::max(mx, (double)hi[z][j]);
-        }
-        if (mn > mx) { mn = 0.0; mx = 0.0; }            // no slot in use
-        const double need = std::max({(mx - mn) / 251.0, std::max(std::fabs(mn), std::fabs(mx)) * std::ldexp(1.0, -21),
-                                      std::ldexp(1.0, -60)});
-        int e = 0;
-        std::frexp(need, &e);                           // need < 2^e
-        if (e > 50) return false;
-        const double step = std::ldexp(1.0, e);
-        float org = (float)(mn - 2.0 * step);
-        if ((double)org > mn - 2.0 * step) org = std::nextafter(org, -FLT_MAX);
-        for (int j = 0; j < 4; j++) {
-            uint32_t ql = 255u, qh = 0u;               // empty slot: an inverted box
-            if (info[j] >= 0) {
-                const double a = std::floor(((double)lo[z][j] - org) / step) - 1.0;
-                const double b = std::ceil(((double)hi[z][j] - org) / step) + 1.0;
-                if (a < 0.0 || b > 255.0) return false;
-                ql = (uint32_t)a; qh = (uint32_t)b;
-            }
-            qlo[z] |= ql << (8 * j);
-            qhi[z] |= qh << (8 * j);
-        }
-        memcpy(&w[z], &org, 4);
-        exps |= (uint32_t)(e + 127) << (8 * z);      // float exponent field of 2^e
-    }
-    w[3] = exps;
-    w[4] = qlo[0]; w[5] = qlo[1]; w[6] = qlo[2];
-    w[7] = qhi[0]; w[8] = qhi[1]; w[9] = qhi[2];
-    w[10] = inf8;
-    const int ref[4] = {n.ref.x, n.ref.y, n.ref.z, n.ref.w};
-    memcpy(&w[12], ref, 16);
-    out.a = make_uint4(w[0], w[1], w[2], w[3]);
-    out.b = make_uint4(w[4], w[5], w[6], w[7]);
-    out.c = make_uint4(w[8], w[9], w[10], w[11]);
-    out.d = make_uint4(w[12], w[13], w[14], w[15]);
-    return true;
-}
 
 // ------------------------------------------------------------------ top-level BVH (TLAS)
 // World box of one top-level entry: its geometry's root range box expanded by the eps overhang
@@ -1114,12 +1042,12 @@ int upload(DBuf& b, const V& v) {
 }
 
 struct Level {
-    DBuf rays, meta, hits, nodes, shadows, slist, paths, rlist;   // rlist: non-final nodes (k_resolve)
+    DBuf rays, meta, hits, nodes, shadows, slist, paths;
     DBuf lv;                   // stream schedule: the queued rays' levels (1 byte each)
     long long rcap = 0;        // plane stride of `rays` (RayQ) as the previous level wrote them
     void release() {
         rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release();
-        paths.release(); rlist.release(); lv.release();
+        paths.release(); lv.release();
     }
 };
 
@@ -1133,8 +1061,7 @@ struct Lane {
     hipEvent_t ev_t[6] = {};                // trace start, trace end, shade end, shadow start, shadow end,
                                             // path-tracer gather end
     unsigned long long* h_count = nullptr;  // pinned host slot
-    DBuf qcnt;                              // 128 x u64 per pass: [level] next rays | shadow entries << 32,
-                                            // [64 + level] non-final nodes (k_resolve's list, RTG_RESOLVE_LIST)
+    DBuf qcnt;                              // 128 x u64 per pass: [level] next rays | shadow entries << 32
     std::vector<Level> levels;
     // current pass
     std::vector<int> passes;                // indices into the frame's pass list (this lane's, in order)
@@ -1193,13 +1120,10 @@ struct rtg_scene {
     DBuf d_acc, d_counters, d_stats;
     DBuf d_rad;                              // stream schedule: per-sample radiance of a segment
     rtg_render_stats stats{};
-    int num_lanes = 8;                       // default passes in flight (env RTG_STREAMS overrides)
-    int stream_lanes = 4;                    // path tracer's stream schedule (env RTG_STREAM_LANES)
-    int stream_pt = 1;                       // 0: path tracer on the pass schedule (env RTG_STREAM_PT)
-    int stream_seg_pix = 0;                  // > 0: pixels per stream segment (env RTG_STREAM_SEG_PIX, tests)
-    int stream_whitted = 0;                  // 1: reference integrator on the stream schedule by default (env RTG_STREAM_WHITTED)
-    int stream_div = 3;                      // about this many new-sample steps per lane (env RTG_STREAM_DIV)
-    long long stream_node_budget = 0;        // > 0: node-record bytes per segment (env RTG_STREAM_NODE_BUDGET, tests)
+    int num_lanes = 8;                       // default passes in flight (rtg_render_opts.streams overrides)
+    int stream_lanes = 4;                    // stream schedule's lanes (rtg_render_opts.streams overrides)
+    int stream_div = 3;                      // about this many new-sample steps per lane
+    int uni_walk = 1;                        // rtg_build_opts.uniform_walk == 0
     int bvh_builder = RTG_BVH_AUTO;
     double bvh_build_ms = 0.0;               // last scene build: BVH construction time (all objects)
     rtg_build_stats bst{};                   // last scene build: per-phase wall times
@@ -1307,8 +1231,7 @@ static void bind_view(rtg_scene* s) {
     sv.tops = s->d_tops.as<TopObject>();
     sv.geoms = s->d_geoms.as<Geometry>();
     sv.nodes = s->d_nodes.as<Node>();
-    sv.snodes = s->d_nodes4.as<Node4>();      // one of the two, per RTG_QNODES
-    sv.qnodes = s->d_nodes4.as<Node4q>();
+    sv.snodes = s->d_nodes4.as<Node4>();
     sv.stris = s->d_stris.as<TriGeom>();
     sv.gates = s->d_gates.as<float>();
     sv.tris = s->d_tris.as<TriGeom>();
@@ -1336,8 +1259,72 @@ static void scene_free(rtg_scene* s) {
     s->lanes.clear();
 }
 
+// Frees a scene build's host record arrays off the caller's thread (unmapping ~300 MB for a 1 M-triangle
+// mesh took 18-25 ms of rtg_scene_create).  One worker owned by the library: rtg_scene_destroy waits
+// until everything handed to it is freed, and the library's teardown (this object's destructor, at
+// process exit or dlclose) drains the queue and joins the worker -- no thread outlives the library.
+class Reaper {
+public:
+    // run del(p) on the worker (or here, if the worker cannot be started)
+    void submit(void* p, void (*del)(void*)) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!th_.joinable()) {
+                try {
+                    th_ = std::thread([this] { run(); });
+                } catch (...) {
+                    th_ = std::thread();
+                }
+            }
+            if (th_.joinable()) {
+                q_.emplace_back(p, del);
+                cv_.notify_one();
+                return;
+            }
+        }
+        del(p);
+    }
+    // wait until every submitted free has run
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu_);
+        idle_.wait(lk, [&] { return q_.empty() && !busy_; });
+    }
+    ~Reaper() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        if (th_.joinable()) th_.join();
+    }
+
+private:
+    void run() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            if (q_.empty()) return;                  // stop requested and nothing left
+            const auto job = q_.front();
+            q_.pop_front();
+            busy_ = true;
+            lk.unlock();
+            job.second(job.first);
+            lk.lock();
+            busy_ = false;
+            if (q_.empty()) idle_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, idle_;
+    std::deque<std::pair<void*, void (*)(void*)>> q_;
+    bool stop_ = false, busy_ = false;
+    std::thread th_;
+};
+static Reaper g_reaper;
+
 int32_t rtg_scene_destroy(rtg_scene* s) {
     if (!s) return RTG_OK;
+    g_reaper.drain();
     if (s->device >= 0) (void)hipSetDevice(s->device);
     scene_free(s);
     delete s;
@@ -1438,7 +1425,6 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     std::vector<Geometry> geoms(d->num_objects);
     hvec<Node> dnodes;
     hvec<Node4> snodes;                      // traversal trees (SAH, 4-wide)
-    std::vector<Node4q> qnodes;              // ... quantised (RTG_QNODES; uploaded instead of snodes)
     hvec<TriGeom> stris;                     // their triangles, SAH leaf order (p2 = ref position / leaf / gated)
     hvec<float> gates;                       // per reference position: its leaf's parent box
     hvec<TriGeom> tris;
@@ -1545,16 +1531,6 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                             for (size_t k = k0; k < k1; k++) sah_tris[k] = tri_geom(verts, pv, (size_t)sah_idx[k]);
                         });
                         tc.lap(" sah_tris (thread)");
-                        if (getenv("RTG_SAH_HASH")) {    // tree identity check (dev)
-                            uint64_t h = 1469598103934665603ull;
-                            auto mix = [&](const void* p, size_t nb) {
-                                const unsigned char* c = (const unsigned char*)p;
-                                for (size_t k = 0; k < nb; k++) { h ^= c[k]; h *= 1099511628211ull; }
-                            };
-                            mix(sah_nodes.data(), sah_nodes.size() * sizeof(Node4));
-                            mix(sah_idx.data(), sah_idx.size() * sizeof(int));
-                            fprintf(stderr, "[rtg] sah hash %zu nodes %016llx\n", sah_nodes.size(), (unsigned long long)h);
-                        }
                     }
                 } catch (...) {
                     sah_err = std::current_exception();
@@ -1601,6 +1577,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             sub.lap(" nodes");
         } else {
             ob.nodes.reserve(2 * (size_t)np + 1);
+            B.finite = all_finite;
             ob.root = construct_par(B, 0, np, 0, 0, 4);
         }
         const double bms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
@@ -1793,22 +1770,6 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                 g.sah_base = off;
                 sub.lap(" nodes");
                 if (nsub == 1 && np <= kFlatMaxPrims) { g.flat_first = tri_base; g.flat_count = np; }
-                if (RTG_QNODES) {
-                    // the quantised copy; a node that cannot be quantised drops the mesh's tree
-                    bool qok = true;
-                    for (size_t k = first; k < snodes.size() && qok; k++) {
-                        Node4q q;
-                        qok = quantize_node4(snodes[k], q);
-                        if (qok) qnodes.push_back(q);
-                    }
-                    if (!qok) {
-                        qnodes.resize(first);
-                        snodes.resize(first);
-                        stris.resize(tri_base);
-                        g.sah_base = -1;
-                        g.flat_count = 0;
-                    }
-                }
             }
         }
         bs.traversal_tree_ms += pc.lap("traversal_tree");
@@ -1829,12 +1790,12 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             }
             // every mesh by default: on the dragon the 2-triangle floor is skipped by every ray going
             // up (frame 35.9 -> 35.5 ms against meshes of >= 64 triangles only), cornell / cornell_pt
-            // lose about 1 % (profiles/r3_ab_flat.jsonl)
+            // lose about 1 % (profiles/history/r3_ab_flat.jsonl)
             g.win = g.nprims >= kWinMinPrims;
             // a reference root over two leaves (the walk always visits both: leaves carry no tested box)
             const HNode& rn = hn[ob.root];
             auto leaf_of = [&](int c) { return c >= 0 && hn[c].left < 0 && hn[c].right < 0 && hn[c].end > hn[c].start; };
-            if (RTG_FLAT_REF && g.sah_base < 0 && np <= kFlatMaxPrims && leaf_of(rn.left) && leaf_of(rn.right) &&
+            if (g.sah_base < 0 && np <= kFlatMaxPrims && leaf_of(rn.left) && leaf_of(rn.right) &&
                 hn[rn.right].start == hn[rn.left].end) {
                 g.flat_first = g.prim_base + hn[rn.left].start;
                 g.flat_split = g.prim_base + hn[rn.right].start;
@@ -2048,7 +2009,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
          (rc = upload(s->d_vnormals, s->vnormals))))
         return rc;
     if ((rc = upload(s->d_tops, tops)) || (rc = upload(s->d_geoms, geoms)) ||
-        (rc = (RTG_QNODES ? upload(s->d_nodes4, qnodes) : upload(s->d_nodes4, snodes))) || (rc = upload(s->d_stris, stris)) ||
+        (rc = upload(s->d_nodes4, snodes)) || (rc = upload(s->d_stris, stris)) ||
         (rc = upload(s->d_vertices, vflat)) || (rc = upload(s->d_texcoords, tcflat)) ||
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
         (rc = upload(s->d_lights, lights)) ||
@@ -2087,7 +2048,6 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.brdf_ts = 0;
     for (int i = 0; i < d->num_materials; i++)
         sv.brdf_ts |= d->materials[i].brdf == RTG_BRDF_TS || d->materials[i].brdf == RTG_BRDF_TSF;
-    if (const char* e = getenv("RTG_PT_TS")) sv.brdf_ts |= atoi(e) != 0;   // A/B: the variants with them
     sv.tex = any_brdf;
     for (int i = 0; i < d->num_objects; i++) sv.tex |= d->objects[i].num_textures > 0;
     sv.full |= any_brdf;
@@ -2108,15 +2068,14 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         const rtg_object_desc& o = d->objects[i];
         if (o.type == RTG_OBJ_TRIANGLE || (o.type == RTG_OBJ_MESH && (o.smooth || o.num_textures > 0))) sv.bary = 1;
     }
-    sv.uni_walk = 1;
-    if (const char* e = getenv("RTG_UNI_WALK")) sv.uni_walk = atoi(e) != 0;
+    sv.uni_walk = s->uni_walk;
     sv.lean_shadow = d->num_lights == 1 &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);
     pc.lap("view");
-    // The host copies of the uploaded records (~300 MB for a 1 M-triangle mesh) are freed on a
-    // detached thread: unmapping them took 18-25 ms of rtg_scene_create on the GPU box's host
-    // (RTG_BUILD_TIMING "release").  Only memory owned by this call goes there.
+    // The host copies of the uploaded records (~300 MB for a 1 M-triangle mesh) are freed by the
+    // library's reaper thread (Reaper, above): unmapping them took 18-25 ms of rtg_scene_create on the
+    // GPU box's host (RTG_BUILD_TIMING "release").  Only memory owned by this call goes there.
     {
         struct Grave {
             hvec<Node> dnodes; hvec<Node4> snodes; hvec<TriGeom> stris, tris; hvec<float> gates; hvec<int4> primidx;
@@ -2127,11 +2086,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             g->dnodes.swap(dnodes); g->snodes.swap(snodes); g->stris.swap(stris); g->tris.swap(tris);
             g->gates.swap(gates); g->primidx.swap(primidx); g->verts.swap(verts); g->vn.swap(vn); g->op.swap(op);
             g->vflat.swap(vflat);
-            try {
-                std::thread([g] { delete g; }).detach();
-            } catch (...) {
-                delete g;                    // no thread: free here
-            }
+            g_reaper.submit(g, [](void* p) { delete static_cast<Grave*>(p); });
         }
     }
     s->build_end = std::chrono::steady_clock::now();
@@ -2149,6 +2104,7 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
             return fail(RTG_ERR_INVALID, "bvh_builder");
         if (opts && (opts->tlas < 0 || opts->tlas > 2)) return fail(RTG_ERR_INVALID, "tlas");
         if (opts && (opts->traversal_tree < 0 || opts->traversal_tree > 1)) return fail(RTG_ERR_INVALID, "traversal_tree");
+        if (opts && (opts->uniform_walk < 0 || opts->uniform_walk > 1)) return fail(RTG_ERR_INVALID, "uniform_walk");
         *out = nullptr;
         PhaseClock whole;
         int rc = validate(desc);
@@ -2165,18 +2121,10 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
         rtg_scene* s = new (std::nothrow) rtg_scene();
         if (!s) return fail(RTG_ERR_OOM, "host allocation");
         s->device = device;
-        if (const char* e = getenv("RTG_STREAMS")) s->num_lanes = std::max(1, std::min(8, atoi(e)));
-        if (const char* e = getenv("RTG_STREAM_LANES")) s->stream_lanes = std::max(1, std::min(8, atoi(e)));
-        if (const char* e = getenv("RTG_STREAM_PT")) s->stream_pt = atoi(e) != 0;
-        if (const char* e = getenv("RTG_STREAM_SEG_PIX")) s->stream_seg_pix = std::max(0, atoi(e));
-        if (const char* e = getenv("RTG_STREAM_WHITTED")) s->stream_whitted = atoi(e) != 0;
-        if (const char* e = getenv("RTG_STREAM_DIV")) s->stream_div = std::max(1, atoi(e));
-        if (const char* e = getenv("RTG_STREAM_NODE_BUDGET")) s->stream_node_budget = std::max(0LL, atoll(e));
         s->bvh_builder = opts ? opts->bvh_builder : RTG_BVH_AUTO;
         s->tlas_mode = opts ? opts->tlas : 0;
         s->blas_mode = opts ? opts->traversal_tree : 0;
-        if (const char* e = getenv("RTG_SAH")) s->blas_mode = atoi(e) == 0 ? 1 : 0;
-        if (const char* e = getenv("RTG_TLAS")) s->tlas_mode = atoi(e) == 0 ? 1 : 2;
+        s->uni_walk = opts ? opts->uniform_walk == 0 : 1;
         s->bst.validate_ms = validate_ms;
         // The HIP runtime's first host-to-device copy in a process costs 90-145 ms (its copy path is
         // set up then: scripts/hip_init_probe.py on MI355X), even after the device context exists,
@@ -2348,8 +2296,9 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     // one-tile-high bands -> 16: k_trace 14.7 -> 13.3 ms, k_shadow 13.1 -> 12.3 ms per frame, frame
     // 36.9 -> 36.0 ms; a 1/8 row shard 5.6 -> 5.1 ms (its passes become blocks of columns instead of
     // row strips, so each holds a mix of sky, floor and glass).  4 / 8 / 32 / 64 tiles: in between.
-    int tile_s = 16;
-    if (const char* e = getenv("RTG_TILE_S")) tile_s = std::max(1, std::min(1 << 12, atoi(e)));
+    if (o.tile_band < 0 || o.segment_pixels < 0 || o.segment_nodes < 0)
+        return fail(RTG_ERR_INVALID, "tile_band / segment_pixels / segment_nodes");
+    int tile_s = o.tile_band > 0 ? std::min(o.tile_band, 1 << 12) : 16;
     // tile_pixel (device) forms band * (tile_h * tile_s * nx) in 32-bit ints: keep one band of the
     // widest tiles (tile_h <= 8) below 2^31 pixels
     if ((long long)8 * cam->nx >= (1LL << 31)) return fail(RTG_ERR_UNSUPPORTED, "image wider than 2^28 pixels");
@@ -2396,8 +2345,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         int rc2;
         if ((rc2 = Lc.hits.grow(std::max(sizeof(HitRec), kHitBytes) * (size_t)n)) || (rc2 = Lc.nodes.grow(sizeof(NodeRec) * (size_t)n)) ||
             (rc2 = Lc.shadows.grow(sizeof(ShadowRec) * (size_t)n * std::max(nL, 1))) ||
-            (rc2 = Lc.slist.grow(sizeof(int) * (size_t)n * std::max(nL, 1))) ||
-            (RTG_RESOLVE_LIST && !pt && level > 0 && (rc2 = Lc.rlist.grow(sizeof(int) * (size_t)n))))
+            (rc2 = Lc.slist.grow(sizeof(int) * (size_t)n * std::max(nL, 1))))
             return rc2;
         const bool may_spawn = level + 1 < max_levels;
         const size_t cap = may_spawn ? 2 * (size_t)n : 1;
@@ -2424,8 +2372,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             launch_shade(sv, cd, level, ps, o.seed, cur_q,
                          gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                          Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), next_q,
-                         Ln.meta.as<RayMeta>(), qc, level > 0 ? Lc.rlist.as<int>() : nullptr,
-                         reinterpret_cast<unsigned*>(ln.qcnt.as<unsigned long long>() + 64 + level), n, ln.st);
+                         Ln.meta.as<RayMeta>(), qc, n, ln.st);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
         // the next level's size is known once shade is done: read it back now, so the host can
         // enqueue that level while this level's shadow queries still run (no host round trip
@@ -2435,7 +2382,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
         launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                       reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
-                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni_from=*/level < RTG_UNI_SHADOW_LEVELS ? 0 : INT_MAX);
+                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni_from=*/level < kUniShadowLevels ? 0 : INT_MAX);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
         // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
         if (pt) {
@@ -2484,8 +2431,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         for (int l = level - 1; l >= 1 && !pt; l--)
             if ((rc2 = timed_launch(ln, [&] {
                      launch_resolve(sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(),
-                                    ln.counts[l], ln.counts[l + 1], ln.levels[l].rlist.as<int>(),
-                                    reinterpret_cast<const unsigned*>(ln.qcnt.as<unsigned long long>() + 64 + l), ln.st);
+                                    ln.counts[l], ln.counts[l + 1], ln.st);
                  }, stt.resolve_ms, stt.resolve_launches)))
                 return rc2;
         const int mode = (total == 1) ? 2 : (ps.s0 == 0 ? 1 : 0);
@@ -2535,9 +2481,9 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     //    of the device memory.
     if (o.schedule < RTG_SCHEDULE_AUTO || o.schedule > RTG_SCHEDULE_STREAM) return fail(RTG_ERR_INVALID, "schedule");
     const bool want_stream = o.schedule == RTG_SCHEDULE_STREAM ||
-                             (o.schedule == RTG_SCHEDULE_AUTO && (pt ? s->stream_pt : s->stream_whitted));
+                             (o.schedule == RTG_SCHEDULE_AUTO && pt);
     const bool stream = want_stream && npix > 0 && (long long)npix * total < (1LL << 31) &&
-                        (pt || !RTG_RESOLVE_LIST);
+                        true;
     if (stream) {
         const int SL = o.streams > 0 ? std::min(o.streams, 8) : s->stream_lanes;
         while ((int)s->lanes.size() < SL) {
@@ -2553,10 +2499,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                                                                        std::min(kR, share));
         const long long rad_slots = std::max<long long>(total, (long long)(dev_total_b ? dev_total_b / 8 / 16 : 1LL << 28));
         int seg_np = pt ? (int)std::max<long long>(1, std::min<long long>(npix, rad_slots / total)) : npix;
-        if (pt && s->stream_seg_pix > 0) seg_np = std::min(seg_np, s->stream_seg_pix);
+        if (pt && o.segment_pixels > 0) seg_np = std::min(seg_np, o.segment_pixels);
         if (pt && (rc = s->d_rad.grow((size_t)16 * (size_t)seg_np * total))) return rc;
-        const double node_budget = s->stream_node_budget > 0 ? (double)s->stream_node_budget
-                                                             : (dev_total_b ? 0.25 * (double)dev_total_b : 16e9);
+        const double node_budget = o.segment_nodes > 0 ? (double)sizeof(NodeRec) * o.segment_nodes
+                                                       : (dev_total_b ? 0.25 * (double)dev_total_b : 16e9);
         const int nLb = std::max(nL, 1);
         for (int k = 0; k < SL; k++) {
             Lane& ln = s->lanes[k];
@@ -2632,8 +2578,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                                 A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
             else
                 launch_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), W.hits.as<HitRec>(), nodes->as<NodeRec>(),
-                             W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q, B.meta.as<RayMeta>(), qc, nullptr,
-                             nullptr, n, ln.st, g > 0 ? 1 : 0, m, gbase, A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
+                             W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q, B.meta.as<RayMeta>(), qc, n, ln.st, g > 0 ? 1 : 0, m, gbase, A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[2], ln.st));
             HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
             HIP_TRY(hipEventRecord(ln.ev_count, ln.st));

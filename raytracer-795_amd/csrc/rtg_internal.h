@@ -19,16 +19,10 @@ constexpr int kStackDepth = 32;     // reference BVH depth cap 30 (src/BVH.cpp:5
 // The first 16 traversal-stack entries of a lane live in LDS (4 KB per 64-lane block), deeper ones
 // (up to kStackDepth: the reference-tree fallback can need 31) in the lane's scratch: with the
 // traversal kernels at 6 waves per SIMD, dragon 33.0 -> 31.6 ms, cornell_pt 392.8 -> 364.3 ms per
-// frame (round 3, profiles/r3_ab_ldsstack.jsonl; 32 entries in LDS held them at 5 waves).
-#ifndef RTG_LDS_STACK
-#define RTG_LDS_STACK 16
-#endif
-constexpr int kLdsStack = RTG_LDS_STACK;   // traversal-stack entries per lane in LDS; deeper ones in scratch
+// frame (round 3, profiles/history/r3_ab_ldsstack.jsonl; 32 entries in LDS held them at 5 waves).
+constexpr int kLdsStack = 16;       // traversal-stack entries per lane in LDS; deeper ones in scratch
 constexpr int kTraceBlock = 64;     // threads per traversal block (LDS stack: 128 B per lane)
-#ifndef RTG_SHADE_BLOCK
-#define RTG_SHADE_BLOCK 512
-#endif
-constexpr int kShadeBlock = RTG_SHADE_BLOCK;    // k_shade (simple variants): one queue atomic per block
+constexpr int kShadeBlock = 512;    // k_shade (simple variants): one queue atomic per block
 constexpr int kTlasMinEntries = 16; // top-level BVH over objects / instances from this many entries on
 constexpr int kTlasMaxDepth = 14;   // TLAS leaves at this depth take every remaining entry ...
 constexpr int kTlasStack = 16;      // ... so a near-first walk never pushes more than this
@@ -98,29 +92,6 @@ struct Node4 {
     int4 info;
 };
 
-// The same node quantised to 64 bytes (RTG_QNODES, rtg_host.cpp quantize_node4): per axis a power-of-2
-// step s_a (biased exponent byte) and an origin o_a; slot j's box on axis a is
-// [o_a + qlo_aj s_a, o_a + qhi_aj s_a] with 8-bit qlo / qhi, rounded outwards on the host by one
-// more step than needed, which covers the rounding of the device's t = fma(q, s_a / d_a, (o_a - O_a) / d_a)
-// (DESIGN.md §4).  Boxes are pruning filters only (reachability uses the exact gates[]), so a
-// conservative box keeps every result bit-identical.
-//   w[0..2] origin xyz (float bits), w[3] bytes 0-2: step exponents (float exponent field)
-//   w[4..6] qlo per axis (byte j = slot j), w[7] qhi x, w[8..9] qhi y, z
-//   w[10] info per slot (byte: 0 interior, 1..254 leaf count, 255 empty), w[11] unused, w[12..15] ref
-struct Node4q {
-    uint4 a, b, c, d;
-};
-// Off: measured bit-identical but slower (1080p64 dragon k_trace 13.1 -> 14.1, k_shadow 12.3 -> 12.6 ms;
-// cornell k_shadow 6.4 -> 7.9 ms; profiles/r3_ab_qnodes.jsonl) -- the looser boxes add 4-6 % node steps
-// and the decode VALU work, while the halved node bytes buy nothing: the walk is not bound by node traffic.
-#ifndef RTG_QNODES
-#define RTG_QNODES 0
-#endif
-// quantised-tree eligibility: object-space coordinates below this, direction components within
-// [1/kQDirMax, kQDirMax], steps within [2^-60, 2^50] (so every t term stays a finite normal float)
-constexpr float kQCoordMax = 1e15f;
-constexpr float kQDirMax = 1e16f;
-
 // Triangle in BVH order: the Cramer-rule operands of Triangle::bvhIntersect
 // (src/Shape.cpp:299-316): a, a-b, a-c.  w lanes: x = original face index.
 struct TriGeom {
@@ -168,7 +139,6 @@ struct SceneView {
     const Geometry* geoms;
     const Node* nodes;
     const Node4* snodes;           // traversal trees (SAH, 4-wide)
-    const Node4q* qnodes;          // the same trees quantised (RTG_QNODES)
     const TriGeom* stris;          // their triangles in leaf order; p2.y = reference position (int bits),
                                    // p2.z = first position of its reference leaf, p2.w = 1 if gated
     const float* gates;            // per reference position: min xyz, max xyz of its leaf's parent box
@@ -204,8 +174,8 @@ struct SceneView {
     int bary;                      // some triangle is smooth-shaded or textured: the render path's
                                    // hit records carry the winner's barycentrics (HitPlanes::bg)
     int uni_walk;                  // camera-sample waves may walk the traversal tree wave-uniformly
-                                   // (default 1; env RTG_UNI_WALK=0 at scene creation: per-lane walks,
-                                   // for the parity test that the two agree)
+                                   // (rtg_build_opts.uniform_walk; off: per-lane walks, for the parity
+                                   // test that the two agree)
     // hw7 path tracer (per render: the host sets pt_flags and, with NEE, counts the object
     // lights into num_lights)
     const int* top_emit;           // per top-level entry: emitter light index, -1 if not a light
@@ -287,31 +257,15 @@ struct HitRec {         // 16 B
     float t;            // gett distance
     int pad;
 };
-// A/B switches of two round-3 record trims, both measured slower and off:
-// RTG_HIT_STORED -- k_shade rebuilds the hit from the stored ray parameter / barycentrics instead of
-// re-running the winning test (1080p64 dragon k_shade 9.4 -> 9.9 ms, cornell 7.6 -> 8.6 ms);
-// RTG_RESOLVE_LIST -- k_resolve walks a list of the level's non-final nodes, appended by k_shade,
-// instead of every node (k_resolve 1.76 -> 1.98 ms, k_shade +0.3 ms per frame).
-#ifndef RTG_HIT_STORED
-#define RTG_HIT_STORED 0
-#endif
-#ifndef RTG_RESOLVE_LIST
-#define RTG_RESOLVE_LIST 0
-#endif
-// The render path's hit records (k_trace -> k_shade / k_pt_shade) as planes over a level's n rays:
-// (object, primitive), the winning triangle test's ray parameter in object space, and -- only when
-// SceneView::bary -- its barycentrics (beta, gamma).  k_shade rebuilds the hit point and normal
-// from them instead of re-running the test on a 48-byte TriGeom gather.  kHitBytes per ray.
+// The render path's hit records (k_trace -> k_shade / k_pt_shade): (object, primitive) per ray, 8 bytes.
+// k_shade re-runs the winning test (hit_record); storing the test's ray parameter and barycentrics
+// instead was measured slower (round 3, DESIGN.md §4 "hit records").
 struct HitPlanes {
     int2* id;       // obj, prim
-    float* pt;      // object-space ray parameter of the winning candidate (Triangle::bvhIntersect's t)
-    float2* bg;     // beta, gamma (SceneView::bary), else unused
 };
-constexpr size_t kHitBytes = RTG_HIT_STORED ? 20 : 8;
-__host__ __device__ inline HitPlanes hit_planes(void* base, long long n) {
-    char* p = static_cast<char*>(base);
-    return HitPlanes{reinterpret_cast<int2*>(p), reinterpret_cast<float*>(p + 8 * n),
-                     reinterpret_cast<float2*>(p + 12 * n)};
+constexpr size_t kHitBytes = 8;
+__host__ __device__ inline HitPlanes hit_planes(void* base, long long) {
+    return HitPlanes{reinterpret_cast<int2*>(base)};
 }
 
 enum NodeKind : int {
@@ -393,12 +347,11 @@ struct LevelBuffers;
 void launch_trace(const SceneView& sv, const RayQ rays, HitRec* hits, int n, int exhaustive,
                   Counters* ctr, hipStream_t st, const CameraDev* gen_cam = nullptr, const PassDev* gen_ps = nullptr,
                   uint64_t seed = 0, bool compact = false, int nq = 0, int gbase = 0);
-// rlist / rcount: the level's non-final nodes (levels >= 1), appended for k_resolve
 // gen: 1 = rays i >= nq are primary rays of slots gbase + i - nq, 0 = queued only, -1 = a pass's level
 // (primaries iff rays.a is null); lv_in / lv_out: per-ray levels of a stream step (or null)
 void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed, const RayQ rays, const RayMeta* meta, const HitRec* hits, NodeRec* nodes,
                   ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta,
-                  unsigned long long* qcount, int* rlist, unsigned* rcount, int n, hipStream_t st,
+                  unsigned long long* qcount, int n, hipStream_t st,
                   int gen = -1, int nq = 0, int gbase = 0, const unsigned char* lv_in = nullptr,
                   unsigned char* lv_out = nullptr);
 // the bottom-up step and the accumulation on explicit node planes (stream schedule: a step's nodes
@@ -419,7 +372,7 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* rad,
                       long long n_rad, int nq, int n, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
-                    const int* rlist, const unsigned* rcount, hipStream_t st);
+                    hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
 // level0 / level1 hold NodePlanes over n0 / n1 nodes; whitted: resolve level 0 against level 1
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,

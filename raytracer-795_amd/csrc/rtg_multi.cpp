@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <string>
@@ -47,6 +48,10 @@ struct Rccl {
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    // non-blocking communicators (rtg_comm_init_rank_timeout): optional, the bounded waits need them
+    ncclResult_t (*CommInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
+    ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
 };
 
 std::mutex g_rccl_mu;
@@ -81,7 +86,12 @@ int load_rccl(const Rccl** out) {
             sym(r.GroupStart, "ncclGroupStart");
             sym(r.GroupEnd, "ncclGroupEnd");
             sym(r.GetErrorString, "ncclGetErrorString");
-            if (ok) g_rccl = r;
+            if (ok) {
+                r.CommInitRankConfig = reinterpret_cast<decltype(r.CommInitRankConfig)>(dlsym(h, "ncclCommInitRankConfig"));
+                r.CommGetAsyncError = reinterpret_cast<decltype(r.CommGetAsyncError)>(dlsym(h, "ncclCommGetAsyncError"));
+                r.CommAbort = reinterpret_cast<decltype(r.CommAbort)>(dlsym(h, "ncclCommAbort"));
+                g_rccl = r;
+            }
             else g_rccl_err = "librccl.so.1 lacks an RCCL entry point";
         }
     }
@@ -147,8 +157,10 @@ rtg_render_opts shard_opts(const rtg_render_opts& o, int rank, int nranks, int b
 // Rank `rank` of `nranks` sends its compact rows (`part`) to rank 0; rank 0 receives every shard
 // (its own through an RCCL self send/recv) into `recv`, stacked in rank order, and places the rows
 // into `frame`.  Everything is enqueued on `st` (a stream of the rank's device).
+// settle (non-blocking communicators): waits until the grouped transfers are enqueued on `st`, before
+// anything else goes on the stream.
 int gather_rows(const Rccl& R, ncclComm_t comm, int rank, int nranks, int nx, int ny, int block, const float* part,
-                float* recv, float* frame, hipStream_t st) {
+                float* recv, float* frame, hipStream_t st, const std::function<int()>& settle = nullptr) {
     const ShardPrefix pre = shard_prefix(ny, nranks, block);
     const size_t row = (size_t)nx * 3;
     ncclResult_t e = R.GroupStart();
@@ -162,7 +174,10 @@ int gather_rows(const Rccl& R, ncclComm_t comm, int rank, int nranks, int nx, in
     if (e == ncclSuccess && mine) e = R.Send(part, mine, ncclFloat32, 0, comm, st);
     const ncclResult_t e2 = R.GroupEnd();
     if (e == ncclSuccess) e = e2;
+    if (settle && e == ncclInProgress) e = ncclSuccess;
     if (e != ncclSuccess) return nccl_fail(R, e, "RCCL gather");
+    if (settle)
+        if (int rc = settle()) return rc;
     if (rank == 0) {
         launch_place_rows(recv, frame, nx, ny, nranks, block, pre, st);
         const hipError_t he = hipGetLastError();
@@ -416,30 +431,102 @@ int render_multi(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_opts
 
 using namespace rtg;
 
-// One rank of a one-process-per-GPU job.
+// One rank of a one-process-per-GPU job.  The communicator is non-blocking when the RCCL library
+// has the config API (it does from NCCL 2.14 on): every wait of the rank -- set-up, the failure
+// agreement, the gather -- then polls with a deadline, and a rank whose peers never join aborts the
+// communicator and returns an error instead of blocking forever (`dead`: no further use).
 struct rtg_comm {
     const Rccl* R = nullptr;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1, device = 0;
+    int timeout_ms = 120000;
+    bool nonblocking = false;
+    bool dead = false;
     DevBuf part, recv, flag;
 };
 
 namespace rtg {
 namespace {
+using Clock = std::chrono::steady_clock;
+
+// Wait for a non-blocking communicator's pending operation (set-up, an enqueue) to leave
+// ncclInProgress, or for the deadline; on the deadline or an asynchronous error the communicator is
+// aborted.  Returns RTG_OK or the error (set_error).
+int comm_settle(rtg_comm* c, Clock::time_point deadline, const char* what) {
+    if (!c->nonblocking) return RTG_OK;
+    for (int spin = 0;; spin++) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t e = c->R->CommGetAsyncError(c->comm, &st);
+        if (e != ncclSuccess) st = e;
+        if (st == ncclSuccess) return RTG_OK;
+        if (st != ncclInProgress) {
+            (void)c->R->CommAbort(c->comm);
+            c->dead = true;
+            return nccl_fail(*c->R, st, what);
+        }
+        if (Clock::now() > deadline) {
+            (void)c->R->CommAbort(c->comm);
+            c->dead = true;
+            return set_error(RTG_ERR_HIP, std::string(what) + ": peers did not respond within " +
+                                              std::to_string(c->timeout_ms) + " ms (communicator aborted)");
+        }
+        if (spin < 64) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// Wait for the work enqueued on `st` (collectives of this communicator among it) with the same
+// deadline: a peer that never posts its side of a transfer leaves the RCCL kernel spinning, so the
+// stream is polled, and on the deadline the communicator is aborted (its kernels then exit).
+int comm_stream_wait(rtg_comm* c, hipStream_t st, Clock::time_point deadline, const char* what) {
+    if (!c->nonblocking) {
+        if (hipStreamSynchronize(st) != hipSuccess) return set_error(RTG_ERR_HIP, std::string(what) + " sync");
+        return RTG_OK;
+    }
+    for (int spin = 0;; spin++) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) return RTG_OK;
+        if (q != hipErrorNotReady) return set_error(RTG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(q));
+        ncclResult_t ae = ncclSuccess;
+        if (c->R->CommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+            (void)c->R->CommAbort(c->comm);
+            c->dead = true;
+            (void)hipStreamSynchronize(st);
+            return nccl_fail(*c->R, ae, what);
+        }
+        if (Clock::now() > deadline) {
+            (void)c->R->CommAbort(c->comm);
+            c->dead = true;
+            (void)hipStreamSynchronize(st);      // the aborted kernels return
+            return set_error(RTG_ERR_HIP, std::string(what) + ": peers did not complete within " +
+                                              std::to_string(c->timeout_ms) + " ms (communicator aborted)");
+        }
+        if (spin < 256) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
 // Every rank learns whether any rank failed before the gather (an allreduce-sum of 0 / 1
 // failure flags: the count of failed ranks), so a rank that fails early cannot leave the others
 // blocked in ncclRecv / ncclSend.
 // Returns the number of failed ranks seen (>= 1 means: do not gather), or < 0 when the
 // agreement itself failed (the communicator is then unusable).
-int agree_failures(rtg_comm* c, bool failed, hipStream_t st, std::string& why) {
+int agree_failures(rtg_comm* c, bool failed, hipStream_t st, Clock::time_point deadline, std::string& why) {
     if (c->flag.grow(c->device, sizeof(int32_t))) { why = "status buffer"; return -1; }
     const int32_t mine = failed ? 1 : 0;
     int32_t any = 0;
     if (hipMemcpyAsync(c->flag.p, &mine, sizeof mine, hipMemcpyHostToDevice, st) != hipSuccess) { why = "status copy"; return -1; }
     const ncclResult_t e = c->R->AllReduce(c->flag.p, c->flag.p, 1, ncclInt32, ncclSum, c->comm, st);
-    if (e != ncclSuccess) { why = std::string("ncclAllReduce: ") + c->R->GetErrorString(e); return -1; }
-    if (hipMemcpyAsync(&any, c->flag.p, sizeof any, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) { why = "status sync"; return -1; }
+    if (e != ncclSuccess && !(c->nonblocking && e == ncclInProgress)) {
+        why = std::string("ncclAllReduce: ") + c->R->GetErrorString(e);
+        return -1;
+    }
+    if (comm_settle(c, deadline, "failure agreement (enqueue)") ||
+        hipMemcpyAsync(&any, c->flag.p, sizeof any, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        comm_stream_wait(c, st, deadline, "failure agreement")) {
+        why = rtg_last_error();
+        return -1;
+    }
     return any;
 }
 }  // namespace
@@ -464,6 +551,11 @@ int32_t rtg_comm_unique_id(uint8_t id[RTG_COMM_ID_BYTES]) {
 
 int32_t rtg_comm_init_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
                            rtg_comm** out) {
+    return rtg_comm_init_rank_timeout(id, nranks, rank, device, 0, out);
+}
+
+int32_t rtg_comm_init_rank_timeout(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
+                                   int32_t timeout_ms, rtg_comm** out) {
     return guarded([&]() -> int32_t {
         if (!id || !out) return set_error(RTG_ERR_INVALID, "null argument");
         *out = nullptr;
@@ -478,11 +570,29 @@ int32_t rtg_comm_init_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, 
         if (hipSetDevice(device) != hipSuccess) return set_error(RTG_ERR_NO_DEVICE, "hipSetDevice");
         ncclUniqueId u;
         memcpy(&u, id, sizeof u);
-        ncclComm_t c = nullptr;
-        const ncclResult_t e = R->CommInitRank(&c, nranks, u, rank);
-        if (e != ncclSuccess) return nccl_fail(*R, e, "ncclCommInitRank");
         rtg_comm* k = new rtg_comm();
-        k->R = R; k->comm = c; k->rank = rank; k->nranks = nranks; k->device = device;
+        k->R = R; k->rank = rank; k->nranks = nranks; k->device = device;
+        k->timeout_ms = timeout_ms > 0 ? timeout_ms : 120000;
+        k->nonblocking = R->CommInitRankConfig && R->CommGetAsyncError && R->CommAbort;
+        const auto deadline = Clock::now() + std::chrono::milliseconds(k->timeout_ms);
+        ncclResult_t e;
+        if (k->nonblocking) {
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            e = R->CommInitRankConfig(&k->comm, nranks, u, rank, &cfg);
+            if (e == ncclInProgress) e = ncclSuccess;
+        } else {
+            e = R->CommInitRank(&k->comm, nranks, u, rank);
+        }
+        if (e != ncclSuccess) {
+            if (k->comm) (void)(R->CommAbort ? R->CommAbort(k->comm) : R->CommDestroy(k->comm));
+            delete k;
+            return nccl_fail(*R, e, "ncclCommInitRank");
+        }
+        if (int rc2 = comm_settle(k, deadline, "ncclCommInitRank")) {
+            delete k;                            // aborted by comm_settle
+            return rc2;
+        }
         *out = k;
         return RTG_OK;
     });
@@ -490,7 +600,7 @@ int32_t rtg_comm_init_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, 
 
 int32_t rtg_comm_destroy(rtg_comm* c) {
     if (!c) return RTG_OK;
-    if (c->comm) (void)c->R->CommDestroy(c->comm);
+    if (c->comm && !c->dead) (void)c->R->CommDestroy(c->comm);   // an aborted communicator is freed already
     c->part.release();
     c->recv.release();
     c->flag.release();
@@ -502,6 +612,7 @@ int32_t rtg_render_ranked(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
                           float* frame_device, void* stream) {
     return guarded([&]() -> int32_t {
         if (!c) return set_error(RTG_ERR_INVALID, "null communicator");
+        if (c->dead) return set_error(RTG_ERR_INVALID, "communicator was aborted after a timeout: destroy it");
         // The one early return that skips the failure agreement: without its device this rank
         // cannot take part in any collective, so its peers can still block in the agreement
         // until the job's own timeout (or the caller aborts the communicator).
@@ -545,16 +656,21 @@ int32_t rtg_render_ranked(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
         }
         const std::string local_err = rc == RTG_OK ? std::string() : std::string(rtg_last_error());
         const auto t1 = std::chrono::steady_clock::now();
+        // the agreement and the gather share one deadline, counted from the shard's end
+        const auto deadline = t1 + std::chrono::milliseconds(c->timeout_ms);
         std::string why;
-        const int failed = agree_failures(c, rc != RTG_OK, st, why);
+        const int failed = agree_failures(c, rc != RTG_OK, st, deadline, why);
         if (failed < 0) return set_error(RTG_ERR_HIP, "rank status agreement: " + why +
                                                          (rc != RTG_OK ? " (after: " + local_err + ")" : ""));
         if (rc != RTG_OK) return set_error(rc, local_err);
         if (failed > 0)
             return set_error(RTG_ERR_HIP, std::to_string(failed) + " other rank(s) failed before the gather");
-        if ((rc = gather_rows(*c->R, c->comm, c->rank, n, nx, ny, block, c->part.f(), c->recv.f(), frame_device, st)))
+        std::function<int()> settle;
+        if (c->nonblocking) settle = [&] { return comm_settle(c, deadline, "RCCL gather (enqueue)"); };
+        if ((rc = gather_rows(*c->R, c->comm, c->rank, n, nx, ny, block, c->part.f(), c->recv.f(), frame_device, st,
+                              settle)))
             return rc;
-        if (hipStreamSynchronize(st) != hipSuccess) return set_error(RTG_ERR_HIP, "gather sync");
+        if ((rc = comm_stream_wait(c, st, deadline, "RCCL gather"))) return rc;
         rtg_render_stats t = scene_stats(s);
         t.render_ms = ms_since(t0);
         t.gather_ms = ms_since(t1);             // failure agreement + gather, after the shard finished

@@ -128,16 +128,37 @@ constexpr int kMaxLen = 58;                 // longest code length a 6-bit lengt
 // at the first length whose code range holds the bits read so far (the code-range decoder
 // of canonical prefix codes).
 
-// Reads `n` (<= 57) bits MSB first from a byte string of `nbits` valid bits.
+// Reads bits MSB first from a byte string of `nbits` valid bits (codes are at most 58 bits long:
+// the decoder takes the shortest length first, then one bit at a time).
 struct MsbBits {
     const unsigned char* data;
     uint64_t nbits;
     uint64_t at = 0;
-    bool take(int n, uint32_t& v) {
+    // the next n (1..57) bits without consuming them; bits past the end read as 0
+    uint64_t peek(int n) const {
+        const uint64_t byte = at >> 3, nbytes = (nbits + 7) >> 3;
+        uint64_t w = 0;
+        for (int k = 0; k < 8; k++) w = (w << 8) | (byte + k < nbytes ? data[byte + k] : 0u);
+        uint64_t v = (w << (at & 7)) >> (64 - n);
+        const uint64_t left = nbits > at ? nbits - at : 0;
+        if (left < (uint64_t)n) v &= ~((1ull << (n - left)) - 1);
+        return v;
+    }
+    bool take(int n, uint64_t& v) {      // n <= 64
         if (at + (uint64_t)n > nbits) return false;
-        uint32_t r = 0;
-        for (int k = 0; k < n; k++, at++) r = (r << 1) | ((data[at >> 3] >> (7 - (at & 7))) & 1u);
-        v = r;
+        v = 0;
+        for (int k = n; k > 0;) {           // peek covers 57 bits: at most 32 per step
+            const int m = k < 32 ? k : 32;
+            v = (v << m) | peek(m);
+            at += (uint64_t)m;
+            k -= m;
+        }
+        return true;
+    }
+    bool take(int n, uint32_t& v) {      // n <= 32
+        uint64_t w;
+        if (!take(n, w)) return false;
+        v = (uint32_t)w;
         return true;
     }
 };
@@ -148,7 +169,10 @@ struct CanonicalCode {
     uint32_t start[kMaxLen + 2] = {};   // position of the length's first symbol in `by_code`
     std::vector<int> by_code;           // symbols sorted by (length, code)
     int shortest = 0, longest = 0;
+    // direct lookup of the codes of at most kLut bits: entry = symbol << 8 | length (0: none)
+    std::vector<uint32_t> lut;
 };
+constexpr int kLut = 12;
 
 // Length table -> canonical code; false with `err` set if the lengths do not form a prefix
 // code (a code that does not fit its length, or a shorter code equal to a longer one's prefix).
@@ -184,6 +208,14 @@ bool build_canonical(const std::vector<uint8_t>& len, int lo, CanonicalCode& cc,
     std::vector<uint32_t> fill(cc.start, cc.start + kMaxLen + 1);
     for (size_t i = 0; i < len.size(); i++)          // ascending symbols -> ascending codes
         if (len[i]) cc.by_code[fill[len[i]]++] = lo + (int)i;
+    // every kLut-bit window that starts with a code of length L <= kLut (prefix-free: at most one)
+    cc.lut.assign((size_t)1 << kLut, 0u);
+    for (int L = 1; L <= kLut; L++)
+        for (uint32_t k = 0; k < cc.count[L]; k++) {
+            const uint64_t code = cc.first[L] + k;
+            const uint32_t e = (uint32_t)cc.by_code[cc.start[L] + k] << 8 | (uint32_t)L;
+            for (uint64_t j = 0; j < (1ull << (kLut - L)); j++) cc.lut[(size_t)(code << (kLut - L) | j)] = e;
+        }
     return true;
 }
 
@@ -235,12 +267,17 @@ bool huf_decode(const unsigned char* in, size_t n_in, uint16_t* out, size_t n_ou
     const int repeat_symbol = hi;
     size_t written = 0;
     while (pb.at < pb.nbits) {
-        uint32_t bits;
-        if (!pb.take(cc.shortest, bits)) { err = "PIZ: truncated code"; return false; }
-        uint64_t v = bits;
-        int L = cc.shortest;
         int sym = -1;
-        for (;;) {
+        // short codes: one table lookup (a window past the end reads zeros, so the length is checked)
+        const uint32_t e = cc.lut[(size_t)pb.peek(kLut)];
+        if (e && pb.at + (e & 0xFFu) <= pb.nbits) {
+            sym = (int)(e >> 8);
+            pb.at += e & 0xFFu;
+        }
+        uint64_t v = 0;
+        int L = cc.shortest;
+        if (sym < 0 && !pb.take(cc.shortest, v)) { err = "PIZ: truncated code"; return false; }
+        for (; sym < 0;) {
             if (cc.count[L] && v >= cc.first[L] && v - cc.first[L] < cc.count[L]) {
                 sym = cc.by_code[cc.start[L] + (uint32_t)(v - cc.first[L])];
                 break;

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 7
+RTG_ABI_VERSION = 8
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -108,7 +108,8 @@ class RenderOpts(C.Structure):
                 ("traversal", C.c_int32), ("max_batch_rays", C.c_int32), ("collect_stats", C.c_int32),
                 ("collect_timing", C.c_int32), ("streams", C.c_int32), ("row_block", C.c_int32),
                 ("compact_rows", C.c_int32), ("num_devices", C.c_int32), ("devices", C.POINTER(C.c_int32)),
-                ("schedule", C.c_int32)]
+                ("schedule", C.c_int32), ("tile_band", C.c_int32), ("segment_pixels", C.c_int32),
+                ("segment_nodes", C.c_int32), ("pad_abi8", C.c_int32)]
 
 
 SCHEDULE_AUTO, SCHEDULE_PASSES, SCHEDULE_STREAM = 0, 1, 2
@@ -140,7 +141,8 @@ class Ray(C.Structure):
 
 
 class BuildOpts(C.Structure):
-    _fields_ = [("bvh_builder", C.c_int32), ("tlas", C.c_int32), ("traversal_tree", C.c_int32)]
+    _fields_ = [("bvh_builder", C.c_int32), ("tlas", C.c_int32), ("traversal_tree", C.c_int32),
+                ("uniform_walk", C.c_int32)]
 
 
 class BuildStats(C.Structure):
@@ -192,6 +194,8 @@ EXPORTS = {
     "rtg_scene_vertex_normals": (C.c_int32, [C.c_void_p, PF]),
     "rtg_comm_unique_id": (C.c_int32, [C.c_void_p]),
     "rtg_comm_init_rank": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "rtg_comm_init_rank_timeout": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                               C.POINTER(C.c_void_p)]),
     "rtg_comm_destroy": (C.c_int32, [C.c_void_p]),
     "rtg_render_ranked": (C.c_int32, [C.c_void_p, C.POINTER(CameraDesc), C.POINTER(RenderOpts), C.c_void_p,
                                       C.c_void_p, C.c_void_p]),

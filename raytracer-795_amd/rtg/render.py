@@ -25,12 +25,12 @@ DEFAULT_SEED = 0x5EED2026
 
 class Renderer:
     def __init__(self, scene: Scene, device: int = 0, bvh_builder: int = A.RTG_BVH_AUTO, tlas: int = 0,
-                 traversal_tree: int = 0):
+                 traversal_tree: int = 0, uniform_walk: int = 0):
         self.lib = A.load_library()
         self.scene = scene
         desc, self._keep = scene.to_desc()
         h = C.c_void_p()
-        bo = A.BuildOpts(bvh_builder, tlas, traversal_tree)
+        bo = A.BuildOpts(bvh_builder, tlas, traversal_tree, uniform_walk)
         A.check(self.lib.rtg_scene_create_ex(C.byref(desc), int(device), C.byref(bo), C.byref(h)), self.lib)
         self.handle = h
         self.device = device
@@ -54,9 +54,11 @@ class Renderer:
 
     @staticmethod
     def opts(seed=DEFAULT_SEED, row_offset=0, row_stride=1, traversal=0, max_batch_rays=0, collect_stats=0,
-             collect_timing=0, streams=0, row_block=1, compact_rows=0, num_devices=0, devices=None, schedule=0):
+             collect_timing=0, streams=0, row_block=1, compact_rows=0, num_devices=0, devices=None, schedule=0,
+             tile_band=0, segment_pixels=0, segment_nodes=0):
         o = A.RenderOpts()
         o.schedule = schedule
+        o.tile_band, o.segment_pixels, o.segment_nodes = tile_band, segment_pixels, segment_nodes
         o.seed = seed
         o.row_offset, o.row_stride, o.row_block = row_offset, row_stride, row_block
         o.traversal = traversal
@@ -262,13 +264,16 @@ class Comm:
         A.check(lib.rtg_comm_unique_id(buf), lib)
         return bytes(buf)
 
-    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int, timeout_ms: int = 0):
+        """timeout_ms bounds every wait of this rank (set-up, failure agreement, gather); 0 = the
+        library default (120 s).  A rank whose peers do not join returns an error instead of hanging."""
         self.lib = A.load_library()
         if len(uid) != A.RTG_COMM_ID_BYTES:
             raise ValueError("communicator id must be 128 bytes")
         buf = (C.c_uint8 * A.RTG_COMM_ID_BYTES).from_buffer_copy(uid)
         h = C.c_void_p()
-        A.check(self.lib.rtg_comm_init_rank(buf, int(nranks), int(rank), int(device), C.byref(h)), self.lib)
+        A.check(self.lib.rtg_comm_init_rank_timeout(buf, int(nranks), int(rank), int(device), int(timeout_ms),
+                                                    C.byref(h)), self.lib)
         self.handle = h
         self.rank, self.nranks, self.device = rank, nranks, device
 

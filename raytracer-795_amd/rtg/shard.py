@@ -74,6 +74,22 @@ def _row_index(ny, rank, world, block, device):
     return _ROW_INDEX[k]
 
 
+def exchange_comm_id(dist, rank: int, make_id, group=None) -> bytes:
+    """Rank 0's communicator id (make_id(): rtg.Comm.unique_id) to every rank -- the set-up of the
+    one-process-per-GPU path (bench.py N > 1).  Bounded: the broadcast runs on `group` (a gloo group;
+    default: the default group), whose timeout the caller sets at init_process_group / new_group, so a
+    peer that died or never joined makes every other rank raise RuntimeError instead of blocking.
+    The librtg side bounds its own waits (rtg.Comm(timeout_ms=...), rtg_comm_init_rank_timeout)."""
+    obj = [make_id() if rank == 0 else None]
+    try:
+        dist.broadcast_object_list(obj, src=0, group=group)
+    except Exception as e:          # gloo: peer closed / timed out
+        raise RuntimeError(f"rank {rank}: communicator id exchange failed (a peer did not join): {e}") from e
+    if not isinstance(obj[0], (bytes, bytearray)) or len(obj[0]) != 128:
+        raise RuntimeError(f"rank {rank}: bad communicator id from rank 0")
+    return bytes(obj[0])
+
+
 def max_shard_rows(ny: int, world: int, block: int = ROW_BLOCK) -> int:
     return max(len(owned_rows(ny, r, world, block)) for r in range(world))
 

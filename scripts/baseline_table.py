@@ -1,6 +1,6 @@
 """Markdown rows for BASELINE.md §3 / README from bench lines (one JSON line per file).
 
-usage: python scripts/baseline_table.py <bench.json> ...   (e.g. profiles/r3d_bench_final_*.json)
+usage: python scripts/baseline_table.py <bench.json> ...   (e.g. profiles/history/r3d_bench_final_*.json)
 Columns: workload, spp, ms/frame, Mray/s, primary Msamples/s, ms/frame incl. D2H, scene create ms,
 first frame incl. D2H ms, frame HBM GB/s (frac of 8 TB/s), parity (oracle rows, differing values).
 """

@@ -16,9 +16,9 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 timeout -k 10 600 python3 bench.py $BENCH_ARGS > $D/bench.json 2> $D/bench.err || { tail -20 $D/bench.err; exit 1; }
 cat $D/bench.json
-# kernel trace: passes serialised (RTG_STREAMS=1) so every launch is timed alone
-RTG_STREAMS=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/kt -o kt --output-format csv -- \
-    python3 bench.py --no-cpu $BENCH_ARGS > $D/bench_kt.json 2> $D/bench_kt.err || { tail -20 $D/bench_kt.err; exit 1; }
+# kernel trace: passes serialised (--streams 1) so every launch is timed alone
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/kt -o kt --output-format csv -- \
+    python3 bench.py --no-cpu --streams 1 $BENCH_ARGS > $D/bench_kt.json 2> $D/bench_kt.err || { tail -20 $D/bench_kt.err; exit 1; }
 echo "kernel trace done"
 # PMC passes (one counter set per run: at most 8 SQ, 4 TCC, 4 TCP, 2 GRBM counters)
 i=0
@@ -27,8 +27,8 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS S
            "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_WRITE_REQ_sum" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  RTG_STREAMS=1 timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace -d $D/p$i -o p$i --output-format csv -- \
-      python3 bench.py --steps 1 --warmup 0 --no-cpu $BENCH_ARGS > $D/p$i.out 2> $D/p$i.err \
+  timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace -d $D/p$i -o p$i --output-format csv -- \
+      python3 bench.py --steps 1 --warmup 0 --no-cpu --streams 1 $BENCH_ARGS > $D/p$i.out 2> $D/p$i.err \
       || { echo "pmc pass $i failed"; tail -5 $D/p$i.err; exit 1; }
   echo "pmc pass $i done"
 done

@@ -3,7 +3,7 @@
 usage: python scripts/pmc_counters.py <prof_dir> <out.csv> <out.json> [workload]
 
 Every counter pass (p1..pN) is a separate `rocprofv3 --pmc <set> --kernel-trace` run of
-`bench.py --steps 1 --warmup 0 --no-cpu` with RTG_STREAMS=1.  For each kernel and counter the
+`bench.py --steps 1 --warmup 0 --no-cpu --streams 1`.  For each kernel and counter the
 CSV holds the number of dispatches, the sum over them and the mean per dispatch; the JSON holds
 the per-dispatch means that bench.py divides by its live HIP-event launch times (the roofline
 ceilings of DESIGN.md §4).  FETCH_SIZE / WRITE_SIZE are in KB; the gfx950 correction
@@ -67,7 +67,7 @@ def main():
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
             m["hbm_bytes"] = 2.0 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024
     json.dump({"source": os.path.basename(os.path.normpath(d)), "workload": workload,
-               "command": "RTG_STREAMS=1 rocprofv3 --pmc <set> --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu",
+               "command": "rocprofv3 --pmc <set> --kernel-trace -- python3 bench.py --steps 1 --warmup 0 --no-cpu --streams 1",
                "kernels": summ}, open(out_json, "w"), indent=1, sort_keys=True)
 
 

@@ -1,6 +1,6 @@
 """Markdown per-kernel roofline table from one bench line's `roofline.kernels`.
 
-usage: python scripts/roofline_table.py profiles/r3f_<workload>_bench_final.json
+usage: python scripts/roofline_table.py profiles/history/r3f_<workload>_bench_final.json
 Columns: kernel, ms / frame (streams=1 roofline frame), launches, VALU frac (lane-adjusted), HBM GB/s
 (frac of 8 TB/s), HBM MB / launch, L2 hit, issuing / waiting on memory / dependency, lane efficiency.
 """

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Copy the judged evidence of a gpu_round.sh run into profiles/ (tracked):
 #   <tag>_bench.json            the bench.py line
-#   <tag>_kernel_stats.{csv,txt} rocprofv3 --kernel-trace --stats of bench.py (RTG_STREAMS=1)
+#   <tag>_kernel_stats.{csv,txt} rocprofv3 --kernel-trace --stats of bench.py --streams 1
 #   <tag>_counters.csv          per-kernel PMC counters (dispatches, sum, per-dispatch mean)
 #   counters_<workload>.json    the per-dispatch means bench.py's rooflines divide by live launch times
 #                               (counters_current.json: the same for the headline workload, dragon1m)

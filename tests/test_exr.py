@@ -211,3 +211,28 @@ def test_piz_rejects_invalid_code_lengths(tmp_path, monkeypatch, lengths, msg):
     X.write_exr(p, ch, X.PIZ, X.HALF)
     with pytest.raises(RtgError, match=msg):
         native.read_image(p)
+
+
+def test_piz_long_codes_round_trip_and_refuse_high_bits(tmp_path, monkeypatch):
+    """codes longer than 32 bits.  Every symbol gets a 40-bit code (an incomplete but
+    prefix-free table, values 0..n-1): the file round-trips exactly.  The same table with the
+    first symbol's payload code given a 1 in its top bit (value >= 2^39, past every code of that
+    length) is an invalid code and must be refused, not wrapped into a valid 32-bit value."""
+    ch = {"Y": np.arange(16, dtype=np.float32).reshape(4, 4)}
+    monkeypatch.setattr(X, "_huffman_lengths", lambda freq: {s: 40 for s in freq})
+    p = str(tmp_path / "long.exr")
+    X.write_exr(p, ch, X.PIZ, X.HALF)
+    np.testing.assert_array_equal(native.read_image(p), X.expected_rgba(ch, X.HALF)[..., :3])
+    canon = X._canonical
+
+    def high_bit(lengths):
+        codes = canon(lengths)
+        s0 = min(codes)
+        c, l = codes[s0]
+        codes[s0] = (c | (1 << (l - 1)), l)
+        return codes
+    monkeypatch.setattr(X, "_canonical", high_bit)
+    p2 = str(tmp_path / "bad_long.exr")
+    X.write_exr(p2, ch, X.PIZ, X.HALF)
+    with pytest.raises(RtgError, match="invalid code"):
+        native.read_image(p2)

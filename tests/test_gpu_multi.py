@@ -108,6 +108,17 @@ def test_ranked_rank_failure_is_agreed_not_hung(gpu, cornell):
         comm.close()
 
 
+def test_ranked_peer_that_never_joins_times_out(gpu):
+    """a two-rank communicator whose second rank never calls ncclCommInitRank.  The
+    first rank's set-up is non-blocking with a deadline (rtg_comm_init_rank_timeout): it aborts the
+    communicator and returns an error within the timeout instead of waiting forever."""
+    import time
+    t0 = time.monotonic()
+    with pytest.raises(rtg.RtgError, match="did not respond|timed out|aborted"):
+        rtg.Comm(rtg.Comm.unique_id(), 2, 0, 0, timeout_ms=2000)
+    assert time.monotonic() - t0 < 30.0
+
+
 def test_dragon_full_frame_two_shards(gpu):
     """The bench scene at 1080p (1 spp): the shard + gather path at full size."""
     sc = scenegen.dragon1m(1920, 1080, spp=1)

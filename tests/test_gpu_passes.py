@@ -36,13 +36,12 @@ def test_row_shards_with_small_passes_gather_to_the_frame(gpu):
             assert np.array_equal(_bits(img), _bits(ref))
 
 
-@pytest.mark.parametrize("tile_s", ["1", "3", "16", "4096"])
-def test_tile_order_does_not_change_the_frame(gpu, monkeypatch, tile_s):
+@pytest.mark.parametrize("tile_band", [1, 3, 16, 4096])
+def test_tile_order_does_not_change_the_frame(gpu, tile_band):
     sc = scenegen.cornell(70, 45, spp=3, level=1)
     with rtg.Renderer(sc, device=gpu) as r:
         ref = r.render(0)
-        monkeypatch.setenv("RTG_TILE_S", tile_s)
-        img = r.render(0, max_batch_rays=1000)
-        shard = r.render(0, num_devices=2, devices=[0, 0])
+        img = r.render(0, max_batch_rays=1000, tile_band=tile_band)
+        shard = r.render(0, num_devices=2, devices=[0, 0], tile_band=tile_band)
     assert np.array_equal(_bits(img), _bits(ref))
     assert np.array_equal(_bits(shard), _bits(ref))

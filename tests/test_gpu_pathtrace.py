@@ -165,12 +165,11 @@ def test_stream_schedule_equals_pass_schedule(gpu, flags, monkeypatch):
     rays: small steps (many regenerating steps per lane, levels mixed in every launch), one or
     three lanes, and segments of a few pixels (the radiance buffer reused)."""
     sc = scenegen.cornell_pt(37, 23, spp=7, flags=flags)
-    monkeypatch.setenv("RTG_STREAM_SEG_PIX", "97")
     with rtg.Renderer(sc, device=gpu) as r:
         ref = r.render(0, schedule=A.SCHEDULE_PASSES)
         st0 = r.stats()
         for batch, streams in ((0, 0), (500, 1), (1300, 3), (64, 2)):
-            img = r.render(0, schedule=A.SCHEDULE_STREAM, max_batch_rays=batch, streams=streams)
+            img = r.render(0, schedule=A.SCHEDULE_STREAM, max_batch_rays=batch, streams=streams, segment_pixels=97)
             st = r.stats()
             assert np.array_equal(img.view(np.int32), ref.view(np.int32)), (batch, streams)
             assert (st["primary_rays"], st["secondary_rays"], st["shadow_rays"]) == \

@@ -32,12 +32,12 @@ def _same(a, b):
 @pytest.mark.parametrize("name", sorted(SCENES))
 def test_stream_equals_passes_reference_integrator(gpu, name, monkeypatch):
     sc = SCENES[name]()
-    monkeypatch.setenv("RTG_STREAM_NODE_BUDGET", "200000")       # ~4 K nodes: several segments
     with rtg.Renderer(sc, device=gpu) as r:
         ref = r.render(0, schedule=A.SCHEDULE_PASSES)
         st0 = r.stats()
         for batch, streams in ((0, 0), (300, 1), (1000, 3), (64, 2)):
-            img = r.render(0, schedule=A.SCHEDULE_STREAM, max_batch_rays=batch, streams=streams)
+            img = r.render(0, schedule=A.SCHEDULE_STREAM, max_batch_rays=batch, streams=streams,
+                           segment_nodes=4200)       # ~4 K nodes: several segments
             st = r.stats()
             assert _same(img, ref), (name, batch, streams)
             assert (st["primary_rays"], st["secondary_rays"], st["shadow_rays"]) == \

@@ -4,7 +4,7 @@ uniform, scalar-cache loads, slots visited when any lane needs them), every lane
 its own window, test and reachability gate.  A lane then sees a superset of its own walk's candidates,
 each valid, so the winner -- the minimum of the total order (dist, -leaf_start, prim) that the
 reference's recursive walk returns (src/BVH.cpp:137-210) -- and every frame are unchanged.  Checked
-here bitwise against the per-lane walk (RTG_UNI_WALK=0 at scene creation) on both schedules and both
+here bitwise against the per-lane walk (rtg_build_opts.uniform_walk = 1) on both schedules and both
 integrators, and against the oracle."""
 import numpy as np
 import pytest
@@ -34,11 +34,9 @@ def _render_pair(sc, gpu, monkeypatch, **kw):
     with rtg.Renderer(sc, device=gpu) as r:
         uni = r.render(0, **kw)
         st_uni = r.stats()
-    monkeypatch.setenv("RTG_UNI_WALK", "0")
-    with rtg.Renderer(sc, device=gpu) as r:
+    with rtg.Renderer(sc, device=gpu, uniform_walk=1) as r:
         lane = r.render(0, **kw)
         st_lane = r.stats()
-    monkeypatch.delenv("RTG_UNI_WALK")
     return uni, lane, st_uni, st_lane
 
 

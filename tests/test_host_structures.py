@@ -73,3 +73,44 @@ def test_degenerate_centres_hit_depth_cap(lib):
     assert np.array_equal(p1, p2) and np.array_equal(n1, n2)
     leaves = n1[(n1[:, 0] < 0) & (n1[:, 1] < 0)]
     assert (leaves[:, 3] - leaves[:, 2]).max() == 40
+
+
+def test_parallel_root_box_keeps_the_reference_fold_with_nan(lib):
+    """the top levels of a >= 64K-triangle host build (construct_par) reduce their node
+    boxes in chunks.  The reference's fold (ComputeBoundingBox, src/BVH.cpp:268-283, min/maxOfTwo
+    as `a <= b ? a : b`) drops everything before the last NaN, which a merge of chunk results does
+    not; a mesh with a NaN vertex coordinate must get the sequential fold (the oracle's).  The NaN
+    sits in the third vertex's z of one triangle three quarters into the face list, so the
+    triangle's box z is NaN (minOfThree(a, b, NaN) = NaN): the reference's root box z then comes from
+    the triangles after it only, while a chunked merge would also take the earlier chunks'."""
+    sc = scenegen.dragon1m(8, 8, spp=1, nu=300, nv=150)     # 90,000 triangles in the mesh
+    mesh = len(sc.objects) - 1
+    faces = sc.objects[mesh].faces
+    f = faces[(3 * len(faces)) // 4]
+    sc.vertices = np.array(sc.vertices, np.float32, copy=True)
+    sc.vertices[f[2] - 1, 2] = np.nan
+    desc, keep = sc.to_desc()
+    h = C.c_void_p()
+    assert lib.rtg_scene_create(C.byref(desc), A.RTG_DEVICE_HOST_ONLY, C.byref(h)) == 0, lib.rtg_last_error()
+    o = pyoracle.Oracle(sc)
+    try:
+        p1, n1, b1 = _bvh(lib.rtg_scene_object_bvh, h, mesh)
+        p2, n2, b2 = o.bvh(mesh)
+        assert np.isnan(b2).any(), "the fixture must put a NaN into a node box"
+        # Nodes down to depth 2 (x, y splits: the NaN is only in a z coordinate, so these medians
+        # are well defined): same ranges and bit-identical boxes, found by their path from the root.
+        # Below, a z split over a NaN centroid depends on the sort algorithm (the reference's
+        # std::sort with NaN is unspecified), so the permutation is not compared there.
+        def walk(n, b, node, depth, path, out):
+            out[path] = (tuple(n[node][2:4]), bits(b[node]).tobytes())
+            if depth < 2:
+                for k, child in ((0, n[node][0]), (1, n[node][1])):
+                    if child >= 0:
+                        walk(n, b, child, depth + 1, path + "LR"[k], out)
+        a, r = {}, {}
+        walk(n1, b1, 0, 0, "", a)
+        walk(n2, b2, 0, 0, "", r)
+        assert a == r
+    finally:
+        lib.rtg_scene_destroy(h)
+        o.close()
