@@ -219,6 +219,14 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
                     "node_steps": st_stats[f"{pre}_steps"], "walk_lane_slots": slots}
             if "valu" in out[key]:
                 out[key]["valu"]["lane_adjusted_frac"] = round(out[key]["valu"]["frac"] * eff, 4)
+    # where the traversal's wave time goes: s_memtime cycles per top-level entry of the linear loop
+    # (collect_stats frame; entries >= 15 pooled in the last slot)
+    for key, pre in (("k_trace", "trace"), ("k_shadow", "shadow")):
+        cyc = list(st_stats.get(f"{pre}_entry_cycles", []))
+        while cyc and cyc[-1] == 0:
+            cyc.pop()
+        if key in out and cyc and sum(cyc) > 0:
+            out[key]["entry_cycles_frac"] = [round(c / sum(cyc), 4) for c in cyc]
     sq = st_stats.get("shadow_rays", 0)
     if "k_shadow" in out and sq > 0:
         b = st_stats["shadow_blocked"]

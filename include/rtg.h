@@ -322,6 +322,11 @@ typedef struct rtg_render_stats {
     /* ... and the same sum with each blocked query's steps before replaced by the fewest any blocked
        query of its wave took (what sharing the first blocker found in a wave could save at most) */
     uint64_t shadow_blocked_steps_before_wavemin;
+    /* ABI 8, collect_stats: wave cycles (shader clock, s_memtime, summed over waves) spent in each
+       top-level entry of the linear object loop (entry-box test, ray transform, walk), closest-hit
+       and shadow kernels; entries >= 15 share the last slot.  Where the traversal time goes per entry. */
+    uint64_t trace_entry_cycles[16];
+    uint64_t shadow_entry_cycles[16];
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */
@@ -380,7 +385,7 @@ typedef struct rtg_build_stats {
     int32_t bvh_gpu_objects; /* objects whose BVH was built on the GPU */
     int32_t num_objects;
     int32_t tlas_nodes;      /* nodes of the top-level BVH (0: linear object loop) */
-    int32_t pad0;
+    int32_t flat_group_entries;  /* ABI 8: entries in the flat group (closest_hit) */
     /* ABI 7: wall-time split of rtg_scene_create (ms), in build order.  Together they cover the
        whole call (total_ms); the reference does this work at the start of renderScene
        (src/Scene.cpp:296-323, BVH.cpp:53-62). */

@@ -182,10 +182,47 @@ DEV bool box_test(f3 o, f3 d, float mnx, float mny, float mnz, float mxx, float 
     float le = max3(txe, tye, tze);
     return !(sl < le);
 }
-// Out-of-line copy for the rare fallbacks inside the traversal loops (keeps the hot loop small).
-__device__ __attribute__((noinline)) bool box_test_slow(f3 o, f3 d, float mnx, float mny, float mnz, float mxx,
-                                                        float mxy, float mxz) {
-    return box_test(o, d, mnx, mny, mnz, mxx, mxy, mxz);
+// box_test decided pair by pair (round 5).  For quotients that are not NaN, !(min3(exits) <
+// max3(entries)) holds iff every slab exit is >= every slab entry; an axis's own pair always holds
+// (correctly rounded subtraction and division are monotone in the bound), so only the six cross-axis
+// pairs are compared -- each with the fast quotients (a, b: (bound - o) * rcp(d), within 3 ulp of
+// box_test's) and the 2^-20 band, and with box_test's two exact divisions only when a pair falls inside
+// the band.  The whole-box band test in box_hit is undecided whenever the line meets the box in one
+// point of parameter -- every line crossing a zero-thickness box (the root and gate boxes of the
+// axis-aligned walls and floors of flat meshes) -- where box_test would divide six times; here the
+// thin axis's pairs against the other axes' slabs are decided by the fast quotients unless the
+// crossing lies on the rectangle's edge.
+DEV bool box_pairs(f3 o, f3 d, float ax, float bx, float ay, float by, float az, float bz, float mnx, float mny,
+                   float mnz, float mxx, float mxy, float mxz) {
+    const float en[3] = {d.x > 0 ? ax : bx, d.y > 0 ? ay : by, d.z > 0 ? az : bz};
+    const float ex[3] = {d.x > 0 ? bx : ax, d.y > 0 ? by : ay, d.z > 0 ? bz : az};
+    const float dv[3] = {d.x, d.y, d.z}, ov[3] = {o.x, o.y, o.z};
+    const float lo[3] = {mnx, mny, mnz}, hi[3] = {mxx, mxy, mxz};
+    bool ok = true;
+    unsigned und = 0;
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            if (i == j) continue;
+            const float m = (fabsf(ex[i]) + fabsf(en[j])) * 9.5367431640625e-7f + 1e-37f;   // 2^-20
+            ok = ok && !(ex[i] < en[j] - m);
+            und |= (ex[i] >= en[j] + m ? 0u : 1u) << (3 * i + j);
+        }
+    // the open pairs (a crossing on the rectangle's edge), one division pair at a time
+    while (ok && und) {
+        const int b = __builtin_ctz(und);
+        und &= und - 1u;
+        const int i = b / 3, j = b - 3 * i;
+        const float di = i == 0 ? dv[0] : i == 1 ? dv[1] : dv[2], dj = j == 0 ? dv[0] : j == 1 ? dv[1] : dv[2];
+        const float oi = i == 0 ? ov[0] : i == 1 ? ov[1] : ov[2], oj = j == 0 ? ov[0] : j == 1 ? ov[1] : ov[2];
+        const float li = i == 0 ? lo[0] : i == 1 ? lo[1] : lo[2], lj = j == 0 ? lo[0] : j == 1 ? lo[1] : lo[2];
+        const float hi_ = i == 0 ? hi[0] : i == 1 ? hi[1] : hi[2], hj = j == 0 ? hi[0] : j == 1 ? hi[1] : hi[2];
+        const float exi = ((di > 0) ? hi_ - oi : li - oi) / di;
+        const float enj = ((dj > 0) ? lj - oj : hj - oj) / dj;
+        ok = exi >= enj;
+    }
+    return ok;
 }
 // Same predicate, decided with reciprocal multiplies when that is provably safe.
 // q = fl(fl(b-o) * fl(1/d)) is within 3 ulp of the exact t = fl(fl(b-o)/d), so the min3/max3
@@ -202,6 +239,8 @@ DEV bool box_hit(f3 o, f3 d, f3 inv, bool fast_ok, float mnx, float mny, float m
         float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
         if (sl < le - e) return false;
         if (sl >= le + e) return true;
+        const float q = (ax + bx) + (ay + by) + (az + bz);
+        if (q == q) return box_pairs(o, d, ax, bx, ay, by, az, bz, mnx, mny, mnz, mxx, mxy, mxz);   // no NaN
     }
     return box_test(o, d, mnx, mny, mnz, mxx, mxy, mxz);
 }
@@ -247,9 +286,24 @@ struct Cand {           // Triangle::bvhIntersect acceptance + point (src/Shape.
     float beta, gamma, t;
     f3 p;
 };
+// Fast rejection of Triangle::bvhIntersect's acceptance (src/Shape.cpp:297-345): quotients formed with
+// v_rcp_f32 (1 ulp) lie within 2^-21 (relative) of the correctly rounded ones, so a quotient that misses
+// the acceptance bounds by more than 2^-20 of its magnitude is rejected by the exact test too.  Only
+// for fastq (det within [1e-30, 1e30]); a non-finite operand compares false (not rejected).
 // thi (the caller's parameter window, round 4's windowed test): a candidate whose t lies beyond it cannot
 // become the object's winner that matters -- the same bound the traversal's slot boxes are pruned
 // with (visit_object) -- so it may be rejected as well; INFINITY keeps every candidate.
+DEV bool tri_reject_t(float nt, float r, float eps, float thi) {
+    const float m = 9.5367431640625e-7f;   // 2^-20
+    const float tq = nt * r;
+    return tq < (-eps - fabsf(tq) * m) - 1e-37f || tq > (thi + fabsf(tq) * m) + 1e-37f;
+}
+DEV bool tri_reject_bary(float nb, float ng, float r, float eps) {
+    const float m = 9.5367431640625e-7f;
+    const float bq = nb * r, gq = ng * r;
+    return bq < (-eps - fabsf(bq) * m) - 1e-37f || gq < (-eps - fabsf(gq) * m) - 1e-37f ||
+           bq + gq > (1.0f + (fabsf(bq) + fabsf(gq)) * (2.0f * m)) + m;
+}
 DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps, float thi = INFINITY) {
     f3 a = mk(g.p0.x, g.p0.y, g.p0.z);
     f3 amb = mk(g.p0.w, g.p1.x, g.p1.y);
@@ -258,36 +312,24 @@ DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps, float thi = INFINITY)
     Cand c;
     float det = det3(amb, amc, d);
     float nt = det3(amb, amc, amo);
-    // Fast rejection: quotients formed with v_rcp_f32 (1 ulp) lie within 2^-21 (relative) of
-    // the correctly rounded ones, so a quotient that misses the acceptance bounds by more than
-    // 2^-20 of its magnitude is rejected by the exact test too.  Everything else (and any
-    // det outside [1e-30, 1e30] or non-finite operand, whose comparisons come out false)
-    // takes the exact divisions below.  The ray parameter is tested first, against
-    // [-eps, thi]: a candidate behind the origin or beyond the window costs two determinants,
-    // not four (round 4).
+    // The fast rejection (above) where det allows it, the exact divisions otherwise.  The ray
+    // parameter is tested first, against [-eps, thi]: a candidate behind the origin or beyond the
+    // window costs two determinants, not four (round 4).
     const float ad = fabsf(det);
     const bool fastq = ad >= 1e-30f && ad <= 1e30f;
     const float r = __builtin_amdgcn_rcpf(det);
-    const float m = 9.5367431640625e-7f;   // 2^-20
-    if (fastq) {
-        const float tq = nt * r;
-        if (tq < (-eps - fabsf(tq) * m) - 1e-37f || tq > (thi + fabsf(tq) * m) + 1e-37f) {
-            c.ok = false;
-            c.beta = c.gamma = c.t = 0.0f;
-            c.p = o;
-            return c;
-        }
+    if (fastq && tri_reject_t(nt, r, eps, thi)) {
+        c.ok = false;
+        c.beta = c.gamma = c.t = 0.0f;
+        c.p = o;
+        return c;
     }
     float nb = det3(amo, amc, d), ng = det3(amb, amo, d);
-    if (fastq) {
-        const float bq = nb * r, gq = ng * r;
-        if (bq < (-eps - fabsf(bq) * m) - 1e-37f || gq < (-eps - fabsf(gq) * m) - 1e-37f ||
-            bq + gq > (1.0f + (fabsf(bq) + fabsf(gq)) * (2.0f * m)) + m) {
-            c.ok = false;
-            c.beta = c.gamma = c.t = 0.0f;
-            c.p = o;
-            return c;
-        }
+    if (fastq && tri_reject_bary(nb, ng, r, eps)) {
+        c.ok = false;
+        c.beta = c.gamma = c.t = 0.0f;
+        c.p = o;
+        return c;
     }
     c.beta = nb / det;
     c.gamma = ng / det;
@@ -295,6 +337,19 @@ DEV Cand tri_test(const TriGeom& g, f3 o, f3 d, float eps, float thi = INFINITY)
     c.ok = (c.t >= -eps && (c.beta + c.gamma <= 1) && c.beta >= -eps && c.gamma >= -eps);
     c.p = o + d * c.t;
     return c;
+}
+// tri_test's fast rejection alone: false only when tri_test(g, o, d, eps, thi) would reject.
+DEV bool tri_maybe(const TriGeom& g, f3 o, f3 d, float eps, float thi) {
+    const f3 a = mk(g.p0.x, g.p0.y, g.p0.z);
+    const f3 amb = mk(g.p0.w, g.p1.x, g.p1.y);
+    const f3 amc = mk(g.p1.z, g.p1.w, g.p2.x);
+    const f3 amo = a - o;
+    const float det = det3(amb, amc, d);
+    const float ad = fabsf(det);
+    if (!(ad >= 1e-30f && ad <= 1e30f)) return true;
+    const float r = __builtin_amdgcn_rcpf(det);
+    if (tri_reject_t(det3(amb, amc, amo), r, eps, thi)) return false;
+    return !tri_reject_bary(det3(amo, amc, d), det3(amb, amo, d), r, eps);
 }
 // Sphere::bvhIntersect root selection (src/Shape.cpp:347-391)
 DEV bool sphere_test(f3 o, f3 d, f3 c, float R, float eps, f3& ip) {
@@ -412,10 +467,12 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         float boundD = FLT_MAX;
         const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
         const float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
+        // (bounds only: 1-ulp v_sqrt / v_rcp, inside the 1e-5 / 2e-5 margins)
+        const float dnorm = __builtin_amdgcn_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
         if (!EXHAUSTIVE && nearest < FLT_MAX) {
-            float dl = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+            const float dl = dnorm;
             if (da != 0.0f) {
-                float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) / fabsf(da)) * (1.0f + 1e-5f);
+                float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) * __builtin_amdgcn_rcpf(fabsf(da))) * (1.0f + 1e-5f);
                 boundD = tm * dl * (1.0f + 2e-5f) + 1e-30f;
                 if (!(boundD == boundD)) boundD = FLT_MAX;
             }
@@ -428,7 +485,6 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
         // skipped when its box, expanded by `pad`, meets the line only outside that window.
         const float padt = fast ? (pad * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z))) * 1.0001f : 0.0f;
         const float tlo = -(fabsf(eps) + 1e-6f);
-        const float dnorm = __builtin_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
         const float inv_dn = __builtin_amdgcn_rcpf(dnorm);   // 1 ulp: inside the 2e-5 margins of thi
         float thi = INFINITY;
         if (!EXHAUSTIVE && boundD < FLT_MAX) thi = boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
@@ -452,6 +508,47 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                     if (STATS) st.cand_step = st.steps;
                     if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
                 }
+            }
+        };
+        // a traversal-tree triangle (stris): its reference position and leaf in p2.y / p2.z; a gated one
+        // (p2.w) is accepted as the object's winner only if the reference walk reaches it (§4 "gate")
+        auto test_sah = [&](const TriGeom& tg) {
+            if (STATS) st.tris++;
+            Cand c = tri_test(tg, o2, d2, eps, thi);
+            if (!c.ok) return;
+            const float dist = norm(c.p - o2);
+            const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
+            if (!(dist < FLT_MAX &&
+                  (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))))
+                return;
+            if (__float_as_int(tg.p2.w)) {          // src/BVH.cpp:178 on the leaf's parent
+                const float* gb = sv.gates + 6 * (size_t)k;
+                if (!box_hit(o2, d2, inv, fast, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) return;
+            }
+            best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
+            if (STATS) st.cand_step = st.steps;
+            if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+        };
+        // Flat meshes (<= kFlatMaxPrims triangles tested without a node, round 3): the loop over them is
+        // wave-uniform, so a triangle's exact test (three correctly rounded divisions, the distance, the
+        // tie rule) ran whenever ANY lane of the wave needed it -- for bounce rays in a room, every
+        // triangle of every wall.  Round 5: first the fast rejection of every triangle for every lane
+        // (tri_maybe: straight-line, all lanes active), then each lane runs the full test on its own
+        // candidates only (usually the one triangle it hits).  The winner is the minimum of a total
+        // order, so testing a lane's candidates in index order with the window shrinking between them
+        // gives the same result as testing them all.  split < 0: the one-node traversal tree's records
+        // (stris); split >= 0: a reference root over two leaves (tris[first, split), [split, end)).
+        auto flat_mesh = [&](const TriGeom* recs, const int split) {
+            const int first = g.flat_first, count = g.flat_count;
+            unsigned cand = 0;
+            for (int j = 0; j < count; j++)
+                if (tri_maybe(recs[first + j], o2, d2, eps, thi)) cand |= 1u << j;
+            while (cand) {
+                const int j = __builtin_ctz(cand);
+                cand &= cand - 1;
+                const int k = first + j;
+                if (split < 0) test_sah(recs[k]);
+                else test_prim(recs[k], k, k < split ? first : split);
             }
         };
         // one child box: reachability (interior, exact predicate) + window pruning + entry key
@@ -539,23 +636,6 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             // walk; candidates already accepted stay valid (they are reachable).
             bool use2 = EXHAUSTIVE || !fast || g.sah_base < 0;
             if (!use2) {
-                auto test_sah = [&](const TriGeom& tg) {
-                    if (STATS) st.tris++;
-                    Cand c = tri_test(tg, o2, d2, eps, thi);
-                    if (!c.ok) return;
-                    const float dist = norm(c.p - o2);
-                    const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
-                    if (!(dist < FLT_MAX &&
-                          (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))))
-                        return;
-                    if (__float_as_int(tg.p2.w)) {          // src/BVH.cpp:178 on the leaf's parent
-                        const float* gb = sv.gates + 6 * (size_t)k;
-                        if (!box_hit(o2, d2, inv, fast, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) return;
-                    }
-                    best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
-                    if (STATS) st.cand_step = st.steps;
-                    if (!EXHAUSTIVE) thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
-                };
                 int sp = 0;
                 int cur = g.sah_base;
                 // a one-node tree of a few triangles: test them all instead of loading the node (the
@@ -563,7 +643,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
                 // have skipped changes nothing: they lie outside the window and lose either here or
                 // at the object-level t < nearest)
                 if (g.flat_count > 0) {             // (flat_split < 0 here: sah_base >= 0)
-                    for (int q = g.flat_first; q < g.flat_first + g.flat_count; q++) test_sah(sv.stris[q]);
+                    flat_mesh(sv.stris, -1);
                 } else if (UNI && uni) {
                     // Wave-uniform walk (coherent waves: a pixel's camera samples).  The wave visits a
                     // node when any of its lanes needs it; node, triangle and stack values are
@@ -713,8 +793,7 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
             }
             if (use2) {
                 if (!EXHAUSTIVE && g.flat_split >= 0) {     // root over two leaves: both, no node load
-                    for (int k = g.flat_first; k < g.flat_first + g.flat_count; k++)
-                        test_prim(sv.tris[k], k, k < g.flat_split ? g.flat_first : g.flat_split);
+                    flat_mesh(sv.tris, g.flat_split);
                 } else {
                     walk2();
                 }
@@ -731,9 +810,94 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
     }
 }
 
+// The flat group (SceneView::gents, round 5): the entries whose mesh is tested without a node and whose
+// transform (inverse matrix and blur) is bit-identical -- in practice the untransformed ones, whose glm
+// inverse is the identity with signed zeros -- for a finite ray whose object-space direction is fast,
+// all at once.  visit_object spends on every entry a prologue (transform, root
+// box, window, the direction's reciprocals and norms) that costs several triangle tests, and the
+// wave-uniform loop over a flat mesh's triangles runs a triangle's exact test whenever any lane needs
+// it; in a room (C4 / C5: walls, floor, ceiling, light quads) both happened for nearly every wave.
+// Here the direction set-up is done once, every group triangle gets tri_test's fast rejection (all
+// lanes), and then each entry with candidates runs its reference root test (box_hit, exact) and each
+// lane's own candidates through the exact test, in index order with the window shrinking -- the
+// object's winner is the minimum of the total order (dist, -leaf_start, prim) over its accepted,
+// reachable candidates either way (visit_object) -- followed by the top-level acceptance of
+// src/Helper.cpp:39-49, 64.  Visiting these entries before the others is harmless: an entry replaces
+// the winner iff t < nearest, or t == nearest and it comes earlier in the loop order.
+// Returns false (nothing done) for a ray whose object-space direction is not fast: its lane visits the
+// group's entries in the object loop.
+DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float time, float& nearest, HitRec& out) {
+    f3 o2, d2;
+    transform_ray(sv.tops[sv.gents[0].entry], o, d, time, o2, d2, true);   // the members' common transform
+    const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
+    if (!(adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f))
+        return false;
+    const float eps = sv.int_eps;
+    const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
+    const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
+    const float oa = d2.x != 0.0f ? o2.x : (d2.y != 0.0f ? o2.y : o2.z);
+    const float dnorm = __builtin_amdgcn_sqrtf(d2.x * d2.x + d2.y * d2.y + d2.z * d2.z);
+    const float inv_dn = __builtin_amdgcn_rcpf(dnorm);
+    // visit_object's parameter window for an object visited now (bounds: 1-ulp v_rcp / v_sqrt)
+    auto window = [&]() -> float {
+        if (!(nearest < FLT_MAX) || da == 0.0f) return INFINITY;
+        const float tm = (nearest + 4.0f * 5.96e-8f * fabsf(oa) * __builtin_amdgcn_rcpf(fabsf(da))) * (1.0f + 1e-5f);
+        const float boundD = tm * dnorm * (1.0f + 2e-5f) + 1e-30f;
+        if (!(boundD < FLT_MAX)) return INFINITY;
+        return boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
+    };
+    const float thi1 = window();
+    unsigned cand = 0;
+    for (int j = 0; j < sv.num_gtris; j++)
+        if (tri_maybe(sv.gtris[j], o2, d2, eps, thi1)) cand |= 1u << j;
+    for (int e = 0; e < sv.num_gents; e++) {
+        const GroupEnt& G = sv.gents[e];
+        unsigned m = (cand >> G.first) & ((1u << G.count) - 1u);
+        if (__ballot(m != 0u) == 0ull) continue;
+        if (m == 0u) continue;
+        if (G.root_box && !box_hit(o2, d2, inv, true, G.root_min[0], G.root_min[1], G.root_min[2], G.root_max[0],
+                                   G.root_max[1], G.root_max[2]))
+            continue;
+        const float thi0 = window();
+        float thi = thi0, best_d = FLT_MAX;
+        int best_leaf = -1, bprim = -1;
+        bool found = false;
+        f3 bp = mk(0, 0, 0);
+        while (m) {
+            const int j = __builtin_ctz(m);
+            m &= m - 1u;
+            const TriGeom tg = sv.gtris[G.first + j];
+            const Cand c = tri_test(tg, o2, d2, eps, thi);
+            if (!c.ok) continue;
+            const float dist = norm(c.p - o2);
+            const int k = __float_as_int(tg.p2.y), start = __float_as_int(tg.p2.z);
+            if (!(dist < FLT_MAX &&
+                  (dist < best_d || (dist == best_d && (start > best_leaf || (start == best_leaf && k < bprim))))))
+                continue;
+            if (__float_as_int(tg.p2.w)) {           // src/BVH.cpp:178 on the leaf's parent
+                const float* gb = sv.gates + 6 * (size_t)k;
+                if (!box_hit(o2, d2, inv, true, gb[0], gb[1], gb[2], gb[3], gb[4], gb[5])) continue;
+            }
+            best_d = dist; best_leaf = start; bprim = k; found = true; bp = c.p;
+            thi = fminf(thi0, best_d * inv_dn * (1.0f + 2e-5f) + 1e-30f);
+        }
+        if (found) {
+            const float t = gett(o2, d2, bp);
+            const int i = G.entry;
+            if (t > 0 && (t < nearest || (t == nearest && i < out.obj))) {   // src/Helper.cpp:43, 64
+                nearest = t;
+                out.obj = i; out.prim = bprim; out.t = t;
+            }
+        }
+    }
+    return true;
+}
+
+// ecyc (STATS): per-entry wave-cycle accumulators in LDS (the kernel flushes them to Counters); the
+// flat group's cycles are charged to slot 15
 template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool UNI = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
-                       short* tstack = nullptr, bool uni = false) {
+                       short* tstack = nullptr, bool uni = false, unsigned long long* ecyc = nullptr) {
     HitRec out;
     out.obj = -1; out.prim = -1; out.t = 0.0f; out.pad = 0;
     if (isnan3(o) || isnan3(d)) return out;
@@ -751,9 +915,20 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
     // the ray transform (times outside [0, 1] leave the blur sweep: no skip)
     const bool tin = time >= 0.0f && time <= 1.0f;
     if (!TLAS || EXHAUSTIVE || sv.tlas_root < 0 || !wfast) {   // wfast is per lane: the others walk on
+        // the flat group first (finite rays, fast in object space; the other lanes visit its entries in
+        // the loop)
+        bool grouped = false;
+        if (!EXHAUSTIVE && sv.num_gents > 0 && __ballot(fin) != 0ull) {
+            const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
+            if (fin) grouped = flat_group(sv, o, d, time, nearest, out);
+            if (STATS && ecyc && (__ballot(1) & __lanemask_lt()) == 0ull)
+                atomicAdd(ecyc + 15, __builtin_amdgcn_s_memtime() - c0);
+        }
         for (int i = 0; i < sv.num_tops; i++) {
             if (STATS) st.considered++;
-            if (!EXHAUSTIVE && sv.tops[i].wbox && wfast && tin) {
+            const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
+            bool skip = grouped && sv.tops[i].grouped;
+            if (!skip && !EXHAUSTIVE && sv.tops[i].wbox && wfast && tin) {
                 const TopObject& T = sv.tops[i];
                 const f3 wi = mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
                 const float ax = (T.wlo[0] - o.x) * wi.x, bx = (T.whi[0] - o.x) * wi.x;
@@ -762,10 +937,15 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 const float sl = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
                 const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
                 const float e = (fabsf(sl) + fabsf(le)) * 3.814697265625e-6f + 1e-30f;   // 2^-18
-                if (sl + e < le - e) continue;
+                skip = sl + e < le - e;
             }
-            if (STATS) st.entries++;
-            visit(i);
+            if (!skip) {
+                if (STATS) st.entries++;
+                visit(i);
+            }
+            // STATS: the entry's wave cycles, charged once per wave after the lanes reconverge
+            if (STATS && ecyc && (__ballot(1) & __lanemask_lt()) == 0ull)
+                atomicAdd(ecyc + (i < 15 ? i : 15), __builtin_amdgcn_s_memtime() - c0);
         }
         return out;
     }
@@ -1557,6 +1737,9 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
                                                        bool compact, int nq, int gbase) {
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
+    __shared__ unsigned long long s_ecyc[STATS ? 16 : 1];
+    if (STATS && threadIdx.x < 16) s_ecyc[threadIdx.x] = 0ull;
+    if (STATS) __syncthreads();
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     Stats st = {0, 0, 0, 0, 0, 0, 0};
     if (i < n) {
@@ -1573,7 +1756,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
         constexpr bool KUNI = GEN && !TLAS && !EXHAUSTIVE;
         const bool uni = KUNI && sv.uni_walk && (int)(blockIdx.x * blockDim.x) >= nq;
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KUNI>(sv, o, d, time, tmax, s_stack + threadIdx.x, kTraceBlock, st,
-                                                             s_tstack + (TLAS ? threadIdx.x : 0), uni);
+                                                             s_tstack + (TLAS ? threadIdx.x : 0), uni,
+                                                             STATS ? s_ecyc : nullptr);
         if (compact) {
             hit_planes(hits, n).id[i] = make_int2(h.obj, h.prim);
         } else {
@@ -1591,6 +1775,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
             mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
             mc = max(mc, (unsigned)__shfl_xor((int)mc, off));
         }
+        __syncthreads();
+        if (threadIdx.x < 16 && s_ecyc[threadIdx.x]) atomicAdd(&ctr->trace_entry_cycles[threadIdx.x], s_ecyc[threadIdx.x]);
         if ((threadIdx.x & 63) == 0) {
             atomicAdd(&ctr->node_visits, nv);
             atomicAdd(&ctr->tri_tests, nt);
@@ -2192,6 +2378,9 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                                        int uni_from) {
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
+    __shared__ unsigned long long s_ecyc[STATS ? 16 : 1];
+    if (STATS && threadIdx.x < 16) s_ecyc[threadIdx.x] = 0ull;
+    if (STATS) __syncthreads();
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
     Stats st = {0, 0, 0, 0, 0, 0, 0};
@@ -2243,7 +2432,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         const bool uni = KUNI && sv.uni_walk && __ballot(i < uni_from) == 0ull;
         HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KUNI>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax,
                                                              s_stack + threadIdx.x, kTraceBlock, st,
-                                                             s_tstack + (TLAS ? threadIdx.x : 0), uni);
+                                                             s_tstack + (TLAS ? threadIdx.x : 0), uni,
+                                                             STATS ? s_ecyc : nullptr);
         const float mode = query_mode();
         bool blocked;
         if (mode == 1.0f || mode == 3.0f) {
@@ -2332,6 +2522,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             wm += __shfl_down(wm, off);
             mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
         }
+        __syncthreads();
+        if (threadIdx.x < 16 && s_ecyc[threadIdx.x]) atomicAdd(&ctr->shadow_entry_cycles[threadIdx.x], s_ecyc[threadIdx.x]);
         if ((threadIdx.x & 63) == 0) {
             atomicAdd(&ctr->shadow_node_visits, nv);
             atomicAdd(&ctr->shadow_tri_tests, nt);
@@ -2368,9 +2560,11 @@ DEV f3 nan_check(f3 c) { return isnan3(c) ? mk(0, 0, 0) : c; }   // Scene::NanCh
 
 // Bottom-up combination of RecursiveShading (src/Scene.cpp:148-219): the colour of one node
 // from its basic shading and its children's (already resolved) colours.
-// Node i of `self` (colour record nc) against its children in `child`.  A missed refracted
-// child's point is (0,0,0) (src/Helper.cpp:21): the child's point plane is read only for hits.
-DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& self, const NodePlanes& child) {
+// Node i of `self` (colour record nc); child_col(c) / child_pnt(c): child c's resolved colour (w: its
+// kind bits) and its point.  A missed refracted child's point is (0,0,0) (src/Helper.cpp:21): the
+// child's point plane is read only for hits.
+template <class CC, class CP>
+DEV f3 resolve_with(const SceneView& sv, float4 nc, int i, const NodePlanes& self, CC&& child_col, CP&& child_pnt) {
     const int kind = __float_as_int(nc.w) & 0xFF;
     f3 basic = mk(nc.x, nc.y, nc.z);
     if (kind == NK_FINAL) return basic;
@@ -2385,15 +2579,15 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
     const bool p_far = !(fabsf(p.x) < 1e18f && fabsf(p.y) < 1e18f && fabsf(p.z) < 1e18f);
     f3 c0 = mk(0, 0, 0), c1 = mk(0, 0, 0), q0 = mk(0, 0, 0);
     if (lk.x >= 0) {
-        const float4 a = child.col[lk.x];
+        const float4 a = child_col(lk.x);
         c0 = mk(a.x, a.y, a.z);
         const int ck = __float_as_int(a.w);
         if ((ck & kNodeHit) && (absorbs || p_far || (ck & kNodeFar))) {
-            const float4 ap = child.pnt[lk.x];
+            const float4 ap = child_pnt(lk.x);
             q0 = mk(ap.x, ap.y, ap.z);
         }
     }
-    if (lk.y >= 0) { const float4 b = child.col[lk.y]; c1 = mk(b.x, b.y, b.z); }
+    if (lk.y >= 0) { const float4 b = child_col(lk.y); c1 = mk(b.x, b.y, b.z); }
     const struct { float F; } nd = {pf.w};
     f3 res;
     if (kind == NK_MIRROR) {
@@ -2423,6 +2617,38 @@ DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
     return res;
 }
 
+// Node i of `self` against its children in `child`, whose colours are already resolved.
+DEV f3 resolve_node(const SceneView& sv, float4 nc, int i, const NodePlanes& self, const NodePlanes& child) {
+    return resolve_with(sv, nc, i, self, [&](int c) { return child.col[c]; }, [&](int c) { return child.pnt[c]; });
+}
+// Node i of `self` together with its children in `child` (round 5): each non-final child is resolved
+// here against its own children in `grand` (already resolved), with the same arithmetic, and its
+// colour is never stored -- a child is read by its one parent only (ray trees), so the bottom-up pass
+// skips writing and re-reading every other level.
+DEV f3 resolve_node2(const SceneView& sv, float4 nc, int i, const NodePlanes& self, const NodePlanes& child,
+                     const NodePlanes& grand) {
+    return resolve_with(
+        sv, nc, i, self,
+        [&](int c) {
+            const float4 a = child.col[c];
+            if ((__float_as_int(a.w) & 0xFF) == NK_FINAL) return a;
+            const f3 r = resolve_node(sv, a, c, child, grand);
+            return make_float4(r.x, r.y, r.z, a.w);
+        },
+        [&](int c) { return child.pnt[c]; });
+}
+
+// Two levels of the bottom-up pass in one launch: the nodes of `self` and, inline, their children.
+__global__ void __launch_bounds__(256) k_resolve2(const SceneView sv, const NodePlanes self, const NodePlanes child,
+                                                  const NodePlanes grand, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 nc = self.col[i];
+    if ((__float_as_int(nc.w) & 0xFF) == NK_FINAL) return;
+    const f3 res = resolve_node2(sv, nc, i, self, child, grand);
+    self.col[i] = make_float4(res.x, res.y, res.z, nc.w);
+}
+
 // One level of the bottom-up pass (levels >= 1; level 0 is resolved inside k_accumulate).
 // One thread per node of the level; final nodes only read their colour's kind word.
 __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodePlanes nodes, const NodePlanes child,
@@ -2443,9 +2669,12 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodeP
 constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
 // Colours are read from the level-0 NodePlanes colour plane; `resolve` (Whitted only) evaluates
 // non-final level-0 nodes against level 1 first.
+// DEEP (round 5): level 1 is resolved inline too (resolve_node2, against the resolved level 2).
+template <bool DEEP = false>
 __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv,
                                                     const NodePlanes level0, const NodePlanes level1, bool resolve,
-                                                    float* __restrict__ acc, const PassDev ps, int nx, int mode) {
+                                                    float* __restrict__ acc, const PassDev ps, int nx, int mode,
+                                                    const NodePlanes level2) {
     __shared__ float sr[kAccPix * kAccStride], sg[kAccPix * kAccStride], sb[kAccPix * kAccStride];
     const int p0 = blockIdx.x * kAccPix;
     const int np = min(kAccPix, ps.npass - p0);
@@ -2467,7 +2696,8 @@ __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv,
             f3 c;
             const float4 nc = level0.col[slot];
             if (resolve && (__float_as_int(nc.w) & 0xFF) != NK_FINAL)   // level 0 of the bottom-up pass
-                c = resolve_node(sv, nc, (int)slot, level0, level1);
+                c = DEEP ? resolve_node2(sv, nc, (int)slot, level0, level1, level2)
+                         : resolve_node(sv, nc, (int)slot, level0, level1);
             else
                 c = mk(nc.x, nc.y, nc.z);
             sr[q * kAccStride + s] = c.x;
@@ -2656,6 +2886,13 @@ void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRe
                        shadow_planes(const_cast<ShadowRec*>(shadows), (long long)n * (nL > 1 ? nL : 1)), nL,
                        node_planes(rad, n_rad), nq, n);
 }
+void launch_resolve2(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, const NodeRec* grand_nodes, int n,
+                     int n_child, int n_grand, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_resolve2, dim3(nblk(n, 256)), dim3(256), 0, st, sv, node_planes(nodes, n),
+                       node_planes(const_cast<NodeRec*>(child_nodes), n_child),
+                       node_planes(const_cast<NodeRec*>(grand_nodes), n_grand), n);
+}
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
                     hipStream_t st) {
     if (n <= 0) return;
@@ -2670,17 +2907,24 @@ void launch_resolve_planes(const SceneView& sv, const NodePlanes& self, const No
 void launch_accumulate_planes(const SceneView& sv, const NodePlanes& level0, const NodePlanes& level1, bool resolve,
                               float* acc, const PassDev& ps, int nx, int mode, hipStream_t st) {
     if (ps.npass <= 0) return;
-    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, level0, level1, resolve, acc,
-                       ps, nx, mode);
+    hipLaunchKernelGGL(k_accumulate<false>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, level0, level1, resolve,
+                       acc, ps, nx, mode, NodePlanes{});
 }
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
-                       const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1) {
+                       const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1,
+                       const NodeRec* level2, int n2) {
     if (ps.npass <= 0) return;
     NodeRec* l0 = const_cast<NodeRec*>(level0);
     const NodePlanes p0 = node_planes(l0, n0);
     const NodePlanes p1 = (whitted && level1) ? node_planes(const_cast<NodeRec*>(level1), n1) : NodePlanes{};
-    hipLaunchKernelGGL(k_accumulate, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, p0, p1,
-                       resolve && whitted, acc, ps, nx, mode);
+    if (whitted && resolve && level1 && level2) {
+        const NodePlanes p2 = node_planes(const_cast<NodeRec*>(level2), n2);
+        hipLaunchKernelGGL(k_accumulate<true>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, p0, p1, true, acc, ps,
+                           nx, mode, p2);
+    } else {
+        hipLaunchKernelGGL(k_accumulate<false>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, p0, p1,
+                           resolve && whitted, acc, ps, nx, mode, NodePlanes{});
+    }
 }
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block,
                      int total, hipStream_t st) {

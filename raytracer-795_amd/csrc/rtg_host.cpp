@@ -1108,7 +1108,9 @@ struct rtg_scene {
     std::vector<int> orig_prim;              // absolute BVH position -> original prim index
     SceneView sv{};
     DBuf d_tops, d_geoms, d_nodes, d_nodes4, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
-        d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf, d_tlas, d_tlasidx, d_stris, d_gates;
+        d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf, d_tlas, d_tlasidx, d_stris, d_gates, d_gtris,
+        d_gents;
+    int num_gtris = 0, num_gents = 0;
     int blas_mode = 0;                       // rtg_build_opts.traversal_tree
     int tlas_mode = 0;                       // rtg_build_opts.tlas
     int tlas_root = -1;                      // top-level BVH root node (-1: linear object loop)
@@ -1221,7 +1223,8 @@ static int validate(const rtg_scene_desc* d) {
 static std::vector<DBuf*> scene_buffers(rtg_scene* s) {
     return {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices,
             &s->d_vnormals, &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights,
-            &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_tlas, &s->d_tlasidx, &s->d_stris,
+            &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_tlas, &s->d_tlasidx, &s->d_stris, &s->d_gtris,
+            &s->d_gents,
             &s->d_gates};
 }
 
@@ -1248,6 +1251,8 @@ static void bind_view(rtg_scene* s) {
     sv.emit_cdf = s->d_ecdf.as<float>();
     sv.tlas = s->d_tlas.as<Node>();
     sv.tlas_idx = s->d_tlasidx.as<int>();
+    sv.gtris = s->d_gtris.as<TriGeom>();
+    sv.gents = s->d_gents.as<GroupEnt>();
 }
 
 static void scene_free(rtg_scene* s) {
@@ -1428,6 +1433,9 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     hvec<TriGeom> stris;                     // their triangles, SAH leaf order (p2 = ref position / leaf / gated)
     hvec<float> gates;                       // per reference position: its leaf's parent box
     hvec<TriGeom> tris;
+    std::vector<int> pos_leaf;               // per reference position: first position of its leaf ...
+    std::vector<char> pos_gated;             // ... and whether its leaf's parent (gates[]) is not the root
+    std::vector<char> geom_finite(d->num_objects, 0);   // every primitive box coordinate finite
     hvec<int4> primidx;
     bool early_upload = false;               // dnodes / gates / tris / primidx / orig_prim / vnormals already uploaded
     s->orig_prim.clear();
@@ -1462,6 +1470,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         });
         bool all_finite = true;
         for (char f : fin_chunk) all_finite = all_finite && f;
+        geom_finite[i] = all_finite;
         // traversal tree (SAH, 4-wide; below) of a triangle object with finite primitives: its
         // binned-SAH recursion runs on its own threads, over the triangles in parse order, while the
         // reference's median tree is built (on the GPU for large meshes); its leaves are mapped to
@@ -1702,6 +1711,11 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             }
           }
         });
+        if (np <= kFlatMaxPrims) {                  // small meshes: kept for the flat group
+            pos_leaf.resize(std::max(pos_leaf.size(), (size_t)(g.prim_base + np)), 0);
+            pos_gated.resize(std::max(pos_gated.size(), (size_t)(g.prim_base + np)), 0);
+            for (int k = 0; k < np; k++) { pos_leaf[g.prim_base + k] = leaf_start[k]; pos_gated[g.prim_base + k] = gated[k]; }
+        }
         // traversal tree (SAH, 4-wide) of a triangle object with an interior reference root and
         // finite primitives (its boxes must bound every candidate; NaN / inf objects keep the
         // reference-tree walk)
@@ -1900,6 +1914,50 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         s->tlas_count = s->tlas_root >= 0 ? (int)tlas_nodes.size() : 0;
     }
 
+    // the flat group (GroupEnt, closest_hit), linear-loop scenes only.  (An untransformed object's glm
+    // inverse is the identity with signed zeros, so TopObject::ident -- +0 entries only -- is rarely set;
+    // the group asks only that its members share one transform.)
+    std::vector<TriGeom> gtris;
+    std::vector<GroupEnt> gents;
+    for (int i = 0; i < ntops && s->tlas_root < 0; i++) {
+        TopObject& T = tops[i];
+        const Geometry& g = geoms[T.geom];
+        if (g.type == RTG_OBJ_SPHERE) continue;
+        // one transform for the whole group: the first member's inverse and blur, bit for bit
+        if (!gents.empty() && (memcmp(T.inv, tops[gents[0].entry].inv, sizeof T.inv) != 0 ||
+                               memcmp(T.blur, tops[gents[0].entry].blur, sizeof T.blur) != 0))
+            continue;
+        GroupEnt G;
+        memset(&G, 0, sizeof G);
+        G.entry = i;
+        G.first = (int)gtris.size();
+        // a small mesh (<= kFlatMaxPrims triangles, any reference-tree shape): its triangles in
+        // reference order, each with its leaf (tie order) and gate -- the reference walk reaches a
+        // candidate iff the root box and its leaf's parent box pass the exact slab test (visit_object)
+        const ObjBVH& ob = s->bvh[T.geom];
+        // (finite only: the gate argument needs every reference box to contain its descendants')
+        if (ob.root < 0 || !geom_finite[T.geom] || g.nprims > kFlatMaxPrims ||
+            g.prim_base + g.nprims > (int)pos_leaf.size())
+            continue;
+        std::vector<TriGeom> recs;
+        for (int k = g.prim_base; k < g.prim_base + g.nprims; k++) {
+            TriGeom r = tris[k];
+            const int w[3] = {k, pos_leaf[k], (int)pos_gated[k]};
+            memcpy(&r.p2.y, &w[0], 4); memcpy(&r.p2.z, &w[1], 4); memcpy(&r.p2.w, &w[2], 4);
+            recs.push_back(r);
+        }
+        G.root_box = g.node_base >= 0;              // an interior root: its box is tested (a root leaf: none)
+        if ((int)(gtris.size() + recs.size()) > kGroupMaxTris || (int)gents.size() >= kGroupMaxEnts) continue;
+        for (int z = 0; z < 3; z++) { G.root_min[z] = g.root_min[z]; G.root_max[z] = g.root_max[z]; }
+        G.count = (int)recs.size();
+        gtris.insert(gtris.end(), recs.begin(), recs.end());
+        gents.push_back(G);
+        T.grouped = 1;
+    }
+    s->num_gtris = (int)gtris.size();
+    s->num_gents = (int)gents.size();
+    bs.flat_group_entries = s->num_gents;
+
     // materials, textures, lights
     std::vector<MaterialDev> mats(d->num_materials);
     for (int i = 0; i < d->num_materials; i++) {
@@ -2014,7 +2072,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         (rc = upload(s->d_materials, mats)) || (rc = upload(s->d_textures, texs)) || (rc = upload(s->d_texels, texels)) ||
         (rc = upload(s->d_lights, lights)) ||
         (rc = upload(s->d_topemit, top_emit)) || (rc = upload(s->d_etris, etris)) || (rc = upload(s->d_ecdf, ecdf)) ||
-        (rc = upload(s->d_tlas, tlas_nodes)) || (rc = upload(s->d_tlasidx, tlas_idx)))
+        (rc = upload(s->d_tlas, tlas_nodes)) || (rc = upload(s->d_tlasidx, tlas_idx)) ||
+        (rc = upload(s->d_gtris, gtris)) || (rc = upload(s->d_gents, gents)))
         return rc;
     bs.upload_bytes = 0;
     for (DBuf* b : scene_buffers(s)) bs.upload_bytes += b->used;
@@ -2029,6 +2088,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.num_lights = d->num_lights;
     sv.num_emit = s->num_emit;
     sv.tlas_root = s->tlas_root;
+    sv.num_gtris = s->num_gtris;
+    sv.num_gents = s->num_gents;
     for (int z = 0; z < 3; z++) sv.tlas_k[z] = s->tlas_k[z];
     sv.pt_flags = 0;
     sv.max_depth = d->max_recursion_depth;
@@ -2427,18 +2488,28 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const int level = ln.level;
         stt.max_level = std::max(stt.max_level, level);
         int rc2;
-        // bottom-up: levels level-1 .. 1 here, level 0 inside the accumulation
-        for (int l = level - 1; l >= 1 && !pt; l--)
+        // bottom-up (round 5): levels level-1 .. 2 two at a time (k_resolve2: a level and, inline, its
+        // children, which no one else reads), the odd one alone, and levels 1 and 0 inside the
+        // accumulation -- every resolved level is stored only where its parents are not resolved
+        // in the same launch.  The nodes of `level` itself are final.
+        auto N = [&](int l) { return ln.levels[l].nodes.as<NodeRec>(); };
+        int l = level - 1;
+        for (; l >= 3 && !pt; l -= 2)
             if ((rc2 = timed_launch(ln, [&] {
-                     launch_resolve(sv, ln.levels[l].nodes.as<NodeRec>(), ln.levels[l + 1].nodes.as<NodeRec>(),
-                                    ln.counts[l], ln.counts[l + 1], ln.st);
+                     launch_resolve2(sv, N(l - 1), N(l), N(l + 1), ln.counts[l - 1], ln.counts[l], ln.counts[l + 1], ln.st);
                  }, stt.resolve_ms, stt.resolve_launches)))
                 return rc2;
+        if (l == 2 && !pt &&
+            (rc2 = timed_launch(ln, [&] { launch_resolve(sv, N(2), N(3), ln.counts[2], ln.counts[3], ln.st); },
+                                stt.resolve_ms, stt.resolve_launches)))
+            return rc2;
         const int mode = (total == 1) ? 2 : (ps.s0 == 0 ? 1 : 0);
-        const NodeRec* level1 = level >= 1 ? ln.levels[1].nodes.as<NodeRec>() : nullptr;
+        const NodeRec* level1 = level >= 1 ? N(1) : nullptr;
+        const NodeRec* level2 = level >= 2 ? N(2) : nullptr;
         if ((rc2 = timed_launch(ln, [&] {
-                 launch_accumulate(sv, ln.levels[0].nodes.as<NodeRec>(), level1, !pt && level >= 1, s->d_acc.as<float>(),
-                                   ps, cam->nx, mode, ln.st, !pt, ln.counts[0], level >= 1 ? ln.counts[1] : 0);
+                 launch_accumulate(sv, N(0), level1, !pt && level >= 1, s->d_acc.as<float>(), ps, cam->nx, mode, ln.st, !pt,
+                                   ln.counts[0], level >= 1 ? ln.counts[1] : 0, pt ? nullptr : level2,
+                                   level >= 2 ? ln.counts[2] : 0);
              }, stt.accumulate_ms, stt.accumulate_launches)))
             return rc2;
         stt.passes++;
@@ -2814,6 +2885,10 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     }
     stt.shadow_blocked_steps_before = ctr.shadow_blocked_steps_before;
     stt.shadow_blocked_steps_before_wavemin = ctr.shadow_blocked_steps_before_wavemin;
+    for (int b = 0; b < 16; b++) {
+        stt.trace_entry_cycles[b] = ctr.trace_entry_cycles[b];
+        stt.shadow_entry_cycles[b] = ctr.shadow_entry_cycles[b];
+    }
     stt.devices = 1;
     s->stats = stt;
     return RTG_OK;

@@ -41,6 +41,21 @@ struct TopObject {
     int ident;              // inv is exactly the identity (+0 off-diagonal) and blur is +0
     int wbox;               // wlo / whi valid: a transformed entry's world box (root box + eps overhang
     float wlo[3], whi[3];   // through the model matrix, blur sweep for times in [0, 1], margins)
+    int grouped;            // a member of the flat group (SceneView::gents): fast rays test it there
+};
+
+// The flat group (round 5, closest_hit): the identity-transform entries whose mesh is tested without a
+// node -- a root leaf, a reference root over two leaves, or a one-node traversal tree (<= kFlatMaxPrims
+// triangles each) -- with their triangles in one array in the traversal-record format (p2.y reference
+// position, p2.z first position of its reference leaf, p2.w gate flag).  Fast rays filter all of them
+// at once and run the exact test on their own candidates only.
+constexpr int kGroupMaxTris = 32;   // candidate bits of a lane
+constexpr int kGroupMaxEnts = 16;
+struct GroupEnt {
+    int entry;              // top-level index
+    int first, count;       // range in SceneView::gtris (= bits of the candidate mask)
+    int root_box;           // 1: the reference root is interior (its box decides reachability)
+    float root_min[3], root_max[3];
 };
 
 // Per geometry (one per object; instances share their base mesh's geometry).
@@ -189,6 +204,10 @@ struct SceneView {
     const int* tlas_idx;
     int tlas_root;
     float tlas_k[3];               // gett() error scale of the axis-aligned entries (closest_hit)
+    // the flat group (GroupEnt); num_gents 0: none (top-level BVH scenes never group)
+    const TriGeom* gtris;
+    const GroupEnt* gents;
+    int num_gtris, num_gents;
 };
 
 // Path state of one path-tracing ray (per level, next to the RayQ planes / RayMeta).
@@ -338,6 +357,9 @@ struct Counters {
     // taken before the blocker was accepted and after it, and the summed steps before
     unsigned long long shadow_hist_before[8], shadow_hist_after[8], shadow_blocked_steps_before;
     unsigned long long shadow_blocked_steps_before_wavemin;
+    // wave cycles (s_memtime) spent per top-level entry of the linear object loop (entries >= 15 pooled
+    // in the last slot), closest-hit and shadow kernels: where the traversal's time goes
+    unsigned long long trace_entry_cycles[16], shadow_entry_cycles[16];
 };
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
@@ -373,10 +395,15 @@ void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRe
                       long long n_rad, int nq, int n, hipStream_t st);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
                     hipStream_t st);
+// levels p (nodes) and p + 1 (child_nodes, resolved inline, not stored) against the resolved level p + 2
+void launch_resolve2(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, const NodeRec* grand_nodes, int n,
+                     int n_child, int n_grand, hipStream_t st);
 // mode: 0 = continue the running sum, 1 = start from (0,0,0), 2 = assign (single-sample camera)
 // level0 / level1 hold NodePlanes over n0 / n1 nodes; whitted: resolve level 0 against level 1
+// level2 (optional): level 1 is resolved inline against it (the bottom-up pass left level 1 unresolved)
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
-                       const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1);
+                       const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1,
+                       const NodeRec* level2 = nullptr, int n2 = 0);
 void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offset, int row_stride, int row_block, int total,
                      hipStream_t st);
 void launch_hit_details(const SceneView& sv, const RayQ rays, const HitRec* hits, struct ::rtg_hit* out,

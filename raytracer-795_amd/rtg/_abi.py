@@ -131,7 +131,8 @@ class RenderStats(C.Structure):
                 ("shadow_entry_visits", C.c_uint64), ("shadow_entry_slots", C.c_uint64),
                 ("shadow_hist_before", C.c_uint64 * 8), ("shadow_hist_after", C.c_uint64 * 8),
                 ("shadow_blocked_steps_before", C.c_uint64),
-                ("shadow_blocked_steps_before_wavemin", C.c_uint64)]
+                ("shadow_blocked_steps_before_wavemin", C.c_uint64),
+                ("trace_entry_cycles", C.c_uint64 * 16), ("shadow_entry_cycles", C.c_uint64 * 16)]
 
 RTG_COMM_ID_BYTES = 128
 
@@ -147,7 +148,7 @@ class BuildOpts(C.Structure):
 
 class BuildStats(C.Structure):
     _fields_ = [("bvh_build_ms", C.c_double), ("bvh_gpu_objects", C.c_int32), ("num_objects", C.c_int32),
-                ("tlas_nodes", C.c_int32), ("pad0", C.c_int32),
+                ("tlas_nodes", C.c_int32), ("flat_group_entries", C.c_int32),
                 ("validate_ms", C.c_double), ("prep_ms", C.c_double), ("median_tree_ms", C.c_double),
                 ("records_ms", C.c_double), ("traversal_tree_ms", C.c_double), ("top_level_ms", C.c_double),
                 ("upload_ms", C.c_double), ("total_ms", C.c_double), ("upload_bytes", C.c_uint64)]

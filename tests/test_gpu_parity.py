@@ -139,6 +139,49 @@ def test_trace_from_surface_points_matches_oracle(gpu, name):
             assert np.array_equal(h["point"][m].view(np.int32), ref["point"][m].view(np.int32))
 
 
+@pytest.mark.parametrize("name", ["cornell", "dragon"])
+def test_trace_at_flat_box_edges_matches_oracle(gpu, name):
+    """Round 5's pairwise slab decision (box_pairs): a line crossing a zero-thickness box -- the root
+    and gate boxes of axis-aligned walls and floors -- meets it at one parameter, so the whole-box
+    band test is always undecided; the six cross-axis exit/entry pairs decide it instead.  Rays aimed
+    at the boxes' edges and corners (exactly, and a few ulp inside / outside), from inside and
+    outside the scene, where a pair falls inside the band and the exact divisions must decide:
+    every field bitwise against the literal oracle, pruned and exhaustive."""
+    sc = SCENES[name]()
+    rng = np.random.default_rng(41)
+    V = np.asarray(sc.vertices, np.float32)
+    pts = []
+    for ob in sc.objects:
+        if ob.faces is None or len(ob.faces) > 8:
+            continue
+        P = V[np.asarray(ob.faces).reshape(-1) - 1]
+        lo, hi = P.min(0), P.max(0)
+        for _ in range(400):
+            q = rng.uniform(lo, hi).astype(np.float32)
+            k = rng.integers(0, 3)
+            q[k] = (lo if rng.random() < 0.5 else hi)[k]              # an edge / corner plane
+            q = np.nextafter(q, rng.choice([-np.inf, np.inf], 3).astype(np.float32)) if rng.random() < 0.5 else q
+            pts.append(q)
+    pts = np.asarray(pts, np.float32)
+    n = len(pts)
+    c = V.mean(0)
+    o = (c + rng.normal(0, 1, (n, 3)) * (V.max(0) - V.min(0)) * 0.4).astype(np.float32)
+    d = (pts - o).astype(np.float64)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d = d.astype(np.float32)
+    t = rng.random(n).astype(np.float32)
+    ref = pyoracle.Oracle(sc).trace(o, d, t)
+    with rtg.Renderer(sc, device=gpu) as r:
+        for trav in (0, 1):
+            h = r.trace(o, d, t, traversal=trav)
+            assert np.array_equal(h["full"], ref["full"])
+            assert np.array_equal(h["object"], ref["object"])
+            assert np.array_equal(h["prim"], ref["prim"])
+            m = ref["full"] == 1
+            assert np.array_equal(h["t"][m].view(np.int32), ref["t"][m].view(np.int32))
+            assert np.array_equal(h["point"][m].view(np.int32), ref["point"][m].view(np.int32))
+
+
 def test_trace_transformed_entries_any_time_matches_oracle(gpu):
     """cornell_dynamic's transformed entries (scaled / rotated instances, the motion-blurred sphere
     and instance) are skipped before their ray transform when the ray line misses their world box
