@@ -227,6 +227,10 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
             cyc.pop()
         if key in out and cyc and sum(cyc) > 0:
             out[key]["entry_cycles_frac"] = [round(c / sum(cyc), 4) for c in cyc]
+    pc = list(st_stats.get("pt_shade_cycles", []))
+    if pt and "k_pt_shade" in out and sum(pc) > 0:
+        out["k_pt_shade"]["phase_cycles_frac"] = dict(zip(("hit_setup", "nee", "continuation", "compaction_stores"),
+                                                          [round(c / sum(pc), 4) for c in pc]))
     sq = st_stats.get("shadow_rays", 0)
     if "k_shadow" in out and sq > 0:
         b = st_stats["shadow_blocked"]

@@ -327,6 +327,10 @@ typedef struct rtg_render_stats {
        and shadow kernels; entries >= 15 share the last slot.  Where the traversal time goes per entry. */
     uint64_t trace_entry_cycles[16];
     uint64_t shadow_entry_cycles[16];
+    /* ABI 8, collect_stats: path-tracer shading (k_pt_shade) wave cycles by phase -- hit set-up
+       (ray, hit record), next-event estimation (light samples + BRDF), continuation sampling,
+       compaction + record stores */
+    uint64_t pt_shade_cycles[4];
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */

@@ -182,48 +182,6 @@ DEV bool box_test(f3 o, f3 d, float mnx, float mny, float mnz, float mxx, float 
     float le = max3(txe, tye, tze);
     return !(sl < le);
 }
-// box_test decided pair by pair (round 5).  For quotients that are not NaN, !(min3(exits) <
-// max3(entries)) holds iff every slab exit is >= every slab entry; an axis's own pair always holds
-// (correctly rounded subtraction and division are monotone in the bound), so only the six cross-axis
-// pairs are compared -- each with the fast quotients (a, b: (bound - o) * rcp(d), within 3 ulp of
-// box_test's) and the 2^-20 band, and with box_test's two exact divisions only when a pair falls inside
-// the band.  The whole-box band test in box_hit is undecided whenever the line meets the box in one
-// point of parameter -- every line crossing a zero-thickness box (the root and gate boxes of the
-// axis-aligned walls and floors of flat meshes) -- where box_test would divide six times; here the
-// thin axis's pairs against the other axes' slabs are decided by the fast quotients unless the
-// crossing lies on the rectangle's edge.
-DEV bool box_pairs(f3 o, f3 d, float ax, float bx, float ay, float by, float az, float bz, float mnx, float mny,
-                   float mnz, float mxx, float mxy, float mxz) {
-    const float en[3] = {d.x > 0 ? ax : bx, d.y > 0 ? ay : by, d.z > 0 ? az : bz};
-    const float ex[3] = {d.x > 0 ? bx : ax, d.y > 0 ? by : ay, d.z > 0 ? bz : az};
-    const float dv[3] = {d.x, d.y, d.z}, ov[3] = {o.x, o.y, o.z};
-    const float lo[3] = {mnx, mny, mnz}, hi[3] = {mxx, mxy, mxz};
-    bool ok = true;
-    unsigned und = 0;
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            if (i == j) continue;
-            const float m = (fabsf(ex[i]) + fabsf(en[j])) * 9.5367431640625e-7f + 1e-37f;   // 2^-20
-            ok = ok && !(ex[i] < en[j] - m);
-            und |= (ex[i] >= en[j] + m ? 0u : 1u) << (3 * i + j);
-        }
-    // the open pairs (a crossing on the rectangle's edge), one division pair at a time
-    while (ok && und) {
-        const int b = __builtin_ctz(und);
-        und &= und - 1u;
-        const int i = b / 3, j = b - 3 * i;
-        const float di = i == 0 ? dv[0] : i == 1 ? dv[1] : dv[2], dj = j == 0 ? dv[0] : j == 1 ? dv[1] : dv[2];
-        const float oi = i == 0 ? ov[0] : i == 1 ? ov[1] : ov[2], oj = j == 0 ? ov[0] : j == 1 ? ov[1] : ov[2];
-        const float li = i == 0 ? lo[0] : i == 1 ? lo[1] : lo[2], lj = j == 0 ? lo[0] : j == 1 ? lo[1] : lo[2];
-        const float hi_ = i == 0 ? hi[0] : i == 1 ? hi[1] : hi[2], hj = j == 0 ? hi[0] : j == 1 ? hi[1] : hi[2];
-        const float exi = ((di > 0) ? hi_ - oi : li - oi) / di;
-        const float enj = ((dj > 0) ? lj - oj : hj - oj) / dj;
-        ok = exi >= enj;
-    }
-    return ok;
-}
 // Same predicate, decided with reciprocal multiplies when that is provably safe.
 // q = fl(fl(b-o) * fl(1/d)) is within 3 ulp of the exact t = fl(fl(b-o)/d), so the min3/max3
 // of either set differ by < 2^-21 (|sl|+|le|); outside that band the fast answer equals the
@@ -239,8 +197,6 @@ DEV bool box_hit(f3 o, f3 d, f3 inv, bool fast_ok, float mnx, float mny, float m
         float e = (fabsf(sl) + fabsf(le)) * 9.5367431640625e-7f;   // 2^-20
         if (sl < le - e) return false;
         if (sl >= le + e) return true;
-        const float q = (ax + bx) + (ay + by) + (az + bz);
-        if (q == q) return box_pairs(o, d, ax, bx, ay, by, az, bz, mnx, mny, mnz, mxx, mxy, mxz);   // no NaN
     }
     return box_test(o, d, mnx, mny, mnz, mxx, mxy, mxz);
 }
@@ -847,9 +803,18 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
         return boundD * inv_dn * (1.0f + 2e-5f) + 1e-30f;
     };
     const float thi1 = window();
+    const float tlo = -(fabsf(eps) + 1e-6f);
     unsigned cand = 0;
-    for (int j = 0; j < sv.num_gtris; j++)
-        if (tri_maybe(sv.gtris[j], o2, d2, eps, thi1)) cand |= 1u << j;
+    for (int e = 0; e < sv.num_gents; e++) {
+        const GroupEnt& G = sv.gents[e];
+        // the entry's root box widened by the eps overhang against the parameter window (visit_object):
+        // a coherent wave (a pixel's samples) skips the walls it does not face
+        const bool need = !G.win || window_meets(o2, inv, G.win_min[0], G.win_min[1], G.win_min[2], G.win_max[0],
+                                                 G.win_max[1], G.win_max[2], tlo, thi1);
+        if (__ballot(need) == 0ull) continue;
+        for (int j = G.first; j < G.first + G.count; j++)
+            if (need && tri_maybe(sv.gtris[j], o2, d2, eps, thi1)) cand |= 1u << j;
+    }
     for (int e = 0; e < sv.num_gents; e++) {
         const GroupEnt& G = sv.gents[e];
         unsigned m = (cand >> G.first) & ((1u << G.count) - 1u);
@@ -2127,9 +2092,18 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                                                   const RayQ next_rays, RayMeta* __restrict__ next_meta,
                                                   PathRec* __restrict__ next_paths, unsigned long long* qcount, int n,
                                                   int nq, int gbase, const unsigned char* __restrict__ lv_in,
-                                                  unsigned char* __restrict__ lv_out) {
+                                                  unsigned char* __restrict__ lv_out, Counters* ctr) {
     constexpr int BLOCK = kPtBlock;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    // collect_stats (ctr): wave cycles by phase (Counters::pt_shade_cycles), charged by each wave's
+    // first active lane at the end of the phase
+    __shared__ unsigned long long s_cyc[4];
+    if (ctr && threadIdx.x < 4) s_cyc[threadIdx.x] = 0ull;
+    if (ctr) __syncthreads();
+    const unsigned long long t_start = ctr ? __builtin_amdgcn_s_memtime() : 0ull;
+    auto charge = [&](int r, unsigned long long t0) {
+        if (ctr && (__ballot(1) & __lanemask_lt()) == 0ull) atomicAdd(&s_cyc[r], __builtin_amdgcn_s_memtime() - t0);
+    };
     bool has = false;
     QRay cr;
     RayMeta cm;
@@ -2223,6 +2197,8 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                 DielSplit ds;
                 ds.entering = true; ds.tir = false; ds.F = 0.0f;
                 if (m.type == RTG_MAT_DIELECTRIC) ds = dielectric_split(sv, d, ret, m);
+                charge(0, t_start);
+                const unsigned long long t_nee = ctr ? __builtin_amdgcn_s_memtime() : 0ull;
                 if (ds.entering) {                                     // BasicShading + NEE
                     kind |= kContrib | 0x100;
                     const f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
@@ -2238,6 +2214,8 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
                     }
                 }
+                charge(1, t_nee);
+                const unsigned long long t_cont = ctr ? __builtin_amdgcn_s_memtime() : 0ull;
                 const bool cont = (flags & RTG_PT_RUSSIAN_ROULETTE) ? (level + 1 < RTG_PT_MAX_BOUNCES) : (mt.depth > 0);
                 if (cont) {
                     float xi[4];
@@ -2282,11 +2260,13 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                         }
                     }
                 }
+                charge(2, t_cont);
             }
         }
         nd.kind = kind;
         Tg = T;
     }
+    const unsigned long long t_store = ctr ? __builtin_amdgcn_s_memtime() : 0ull;
     // compaction: one continuation per lane, shadow list light-major per wave (as k_shade)
     __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64];
     __shared__ unsigned long long s_base;
@@ -2326,6 +2306,10 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
         const unsigned long long m = __ballot(need);
         if (need) slist[sb + __popcll(m & lt)] = i * sv.num_lights + li;
         sb += __popcll(m);
+    }    if (ctr) {
+        charge(3, t_store);
+        __syncthreads();
+        if (threadIdx.x < 4 && s_cyc[threadIdx.x]) atomicAdd(&ctr->pt_shade_cycles[threadIdx.x], s_cyc[threadIdx.x]);
     }
 }
 
@@ -2853,14 +2837,14 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
                      const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st, bool gen, int nq, int gbase,
-                     const unsigned char* lv_in, unsigned char* lv_out) {
+                     const unsigned char* lv_in, unsigned char* lv_out, Counters* ctr) {
     if (n <= 0) return;
     dim3 g(nblk(n, kPtBlock)), b(kPtBlock);
 #define RTG_PT_LAUNCH1(F, S, B, G)                                                                                \
     hipLaunchKernelGGL((k_pt_shade<F, S, B, G>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, \
                        node_planes(nodes, n), \
                        shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1)), slist, next_rays, next_meta, next_paths, qcount, n, \
-                       nq, gbase, lv_in, lv_out)
+                       nq, gbase, lv_in, lv_out, ctr)
 #define RTG_PT_LAUNCH(F, S, B)                                                                                    \
     do {                                                                                                          \
         if (gen) RTG_PT_LAUNCH1(F, S, B, true);                                                                   \

@@ -1855,7 +1855,10 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     }
 
     // world boxes of the transformed entries: the object loop skips such an entry, before its ray
-    // transform, for a wave whose ray lines all miss the box (closest_hit, RTG_ENTRY_BOX)
+    // transform, for a lane whose ray line misses the box (closest_hit).  (Round 5 measured every entry
+    // with a world box and, for axis-aligned ones, the top-level BVH's distance pruning -- behind the
+    // origin / beyond the winner so far -- in the object loop: dragon 30.1 -> 31.5, cornell_pt 300 ->
+    // 311 ms per frame; not kept.)
     for (int i = 0; i < d->num_objects + d->num_instances; i++) {
         TopObject& T = tops[i];
         T.wbox = 0;
@@ -1948,7 +1951,11 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         }
         G.root_box = g.node_base >= 0;              // an interior root: its box is tested (a root leaf: none)
         if ((int)(gtris.size() + recs.size()) > kGroupMaxTris || (int)gents.size() >= kGroupMaxEnts) continue;
-        for (int z = 0; z < 3; z++) { G.root_min[z] = g.root_min[z]; G.root_max[z] = g.root_max[z]; }
+        for (int z = 0; z < 3; z++) {
+            G.root_min[z] = g.root_min[z]; G.root_max[z] = g.root_max[z];
+            G.win_min[z] = g.win_min[z]; G.win_max[z] = g.win_max[z];
+        }
+        G.win = g.node_base >= 0 && g.win;
         G.count = (int)recs.size();
         gtris.insert(gtris.end(), recs.begin(), recs.end());
         gents.push_back(G);
@@ -2428,7 +2435,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                             gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                             Lc.paths.as<PathRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                             next_q, Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st,
-                            gen, gen ? 0 : n, 0, nullptr, nullptr);
+                            gen, gen ? 0 : n, 0, nullptr, nullptr, sctr);
         else
             launch_shade(sv, cd, level, ps, o.seed, cur_q,
                          gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
@@ -2646,7 +2653,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                 launch_pt_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), W.hits.as<HitRec>(), A.paths.as<PathRec>(),
                                 nodes->as<NodeRec>(), W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q,
                                 B.meta.as<RayMeta>(), B.paths.as<PathRec>(), qc, n, ln.st, g > 0, m, gbase,
-                                A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
+                                A.lv.as<unsigned char>(), B.lv.as<unsigned char>(), sctr);
             else
                 launch_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), W.hits.as<HitRec>(), nodes->as<NodeRec>(),
                              W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q, B.meta.as<RayMeta>(), qc, n, ln.st, g > 0 ? 1 : 0, m, gbase, A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
@@ -2885,6 +2892,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     }
     stt.shadow_blocked_steps_before = ctr.shadow_blocked_steps_before;
     stt.shadow_blocked_steps_before_wavemin = ctr.shadow_blocked_steps_before_wavemin;
+    for (int b = 0; b < 4; b++) stt.pt_shade_cycles[b] = ctr.pt_shade_cycles[b];
     for (int b = 0; b < 16; b++) {
         stt.trace_entry_cycles[b] = ctr.trace_entry_cycles[b];
         stt.shadow_entry_cycles[b] = ctr.shadow_entry_cycles[b];

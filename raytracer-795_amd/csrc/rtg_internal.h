@@ -56,6 +56,8 @@ struct GroupEnt {
     int first, count;       // range in SceneView::gtris (= bits of the candidate mask)
     int root_box;           // 1: the reference root is interior (its box decides reachability)
     float root_min[3], root_max[3];
+    int win;                // win_min / win_max valid (Geometry::win): a lane whose parameter window misses
+    float win_min[3], win_max[3];   // this box has no candidate here, and a wave with no such lane skips the entry
 };
 
 // Per geometry (one per object; instances share their base mesh's geometry).
@@ -360,6 +362,8 @@ struct Counters {
     // wave cycles (s_memtime) spent per top-level entry of the linear object loop (entries >= 15 pooled
     // in the last slot), closest-hit and shadow kernels: where the traversal's time goes
     unsigned long long trace_entry_cycles[16], shadow_entry_cycles[16];
+    // k_pt_shade wave cycles by phase: hit set-up, next-event estimation, continuation, compaction + stores
+    unsigned long long pt_shade_cycles[4];
 };
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
@@ -388,7 +392,7 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
                      const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st, bool gen, int nq, int gbase,
-                     const unsigned char* lv_in, unsigned char* lv_out);
+                     const unsigned char* lv_in, unsigned char* lv_out, Counters* ctr = nullptr);
 // rad: NodePlanes over n_rad sample slots (its colour plane is the samples' radiance); vertices
 // i >= nq start their slot's sum (level 0)
 void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* rad,

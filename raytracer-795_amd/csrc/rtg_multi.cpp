@@ -220,6 +220,7 @@ void add_stats(rtg_render_stats& a, const rtg_render_stats& b) {
     }
     a.shadow_blocked_steps_before += b.shadow_blocked_steps_before;
     a.shadow_blocked_steps_before_wavemin += b.shadow_blocked_steps_before_wavemin;
+    for (int k = 0; k < 4; k++) a.pt_shade_cycles[k] += b.pt_shade_cycles[k];
     for (int k = 0; k < 16; k++) {
         a.trace_entry_cycles[k] += b.trace_entry_cycles[k];
         a.shadow_entry_cycles[k] += b.shadow_entry_cycles[k];

@@ -132,7 +132,8 @@ class RenderStats(C.Structure):
                 ("shadow_hist_before", C.c_uint64 * 8), ("shadow_hist_after", C.c_uint64 * 8),
                 ("shadow_blocked_steps_before", C.c_uint64),
                 ("shadow_blocked_steps_before_wavemin", C.c_uint64),
-                ("trace_entry_cycles", C.c_uint64 * 16), ("shadow_entry_cycles", C.c_uint64 * 16)]
+                ("trace_entry_cycles", C.c_uint64 * 16), ("shadow_entry_cycles", C.c_uint64 * 16),
+                ("pt_shade_cycles", C.c_uint64 * 4)]
 
 RTG_COMM_ID_BYTES = 128
 
