@@ -8,16 +8,18 @@ from rtg import scenegen
 w = sys.argv[1] if len(sys.argv) > 1 else "dragon1m"
 fn, spp = {"bunny": ("bunny5k", 1), "cornell_pt": ("cornell_pt", 256)}.get(w, (w, 64))   # bench.py's workloads
 sc = getattr(scenegen, fn)(1920, 1080, spp=spp)
+# AB_OPTS "key=int,key=int": render options of this variant (e.g. tile_band=8)
+kw = {k: int(v) for k, v in (p.split("=") for p in os.environ.get("AB_OPTS", "").split(",") if p)}
 r = rtg.Renderer(sc, 0)
-r.render(0)
+r.render(0, **kw)
 ms = []
 for _ in range(int(os.environ.get("AB_FRAMES", "5"))):
-    r.render(0)
+    r.render(0, **kw)
     ms.append(r.stats()["render_ms"])
-r.render(0, collect_stats=1)
+r.render(0, collect_stats=1, **kw)
 ss = r.stats()
-r.render(0, collect_timing=1, streams=1)
-r.render(0, collect_timing=1, streams=1)
+r.render(0, collect_timing=1, streams=1, **kw)
+r.render(0, collect_timing=1, streams=1, **kw)
 st = r.stats()
 print(json.dumps({"lib": os.environ.get("AB_TAG", os.environ.get("RTG_LIBRARY", "librtg")), "workload": w, "frame_ms": round(statistics.median(ms), 2),
                   "frames": [round(x, 2) for x in ms], "trace_ms": round(st["trace_ms"], 2),
