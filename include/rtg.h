@@ -364,7 +364,8 @@ int32_t rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene**
 /* BVH builder selection for rtg_scene_create_ex.  All builders produce the reference's tree
    (src/BVH.cpp:64-135) bit for bit; they differ only in where the work runs. */
 typedef enum rtg_bvh_builder {
-    RTG_BVH_AUTO = 0,   /* GPU for meshes of >= 4096 finite triangles on a device scene, else host */
+    RTG_BVH_AUTO = 0,   /* GPU for meshes of >= 4096 finite triangles on a device scene, else host
+                           (the SAH traversal tree: GPU from 65536 triangles) */
     RTG_BVH_HOST = 1,   /* recursive host build */
     RTG_BVH_GPU = 2     /* level-synchronous GPU build (falls back to host for non-finite input) */
 } rtg_bvh_builder;
@@ -402,6 +403,14 @@ typedef struct rtg_build_stats {
     double upload_ms;        /* host -> device copies of every scene buffer */
     double total_ms;         /* the whole rtg_scene_create call */
     uint64_t upload_bytes;   /* bytes copied to the device */
+    /* ABI 8: traversal trees (SAH) built on the GPU (rtg_bvh_builder applies to both trees), their
+       binary nodes before the 4-wide collapse, and an order-independent hash of those nodes (box and
+       triangle count of every node): the host and GPU builds of a mesh give the same hash unless a
+       range with all centroids equal was halved by count */
+    int32_t sah_gpu_objects;
+    int32_t pad_abi8;
+    uint64_t traversal_nodes;
+    uint64_t traversal_hash;
 } rtg_build_stats;
 int32_t rtg_scene_build_stats(const rtg_scene* scene, rtg_build_stats* out);
 int32_t rtg_scene_destroy(rtg_scene* scene);

@@ -438,15 +438,9 @@ int construct_par(BuildCtx& B, int start, int end, int splitType, int depth, int
 // so that one box decides the whole ancestor chain), and ties keep the reference's order
 // (distance, rightmost reference leaf, lowest position).
 struct SahBox { float lo[3], hi[3]; };
-struct SahNode2 {
-    float lo[3], hi[3];
-    int left, right;          // children (-1 for a leaf)
-    int start, count;         // leaf range in the SAH primitive order
-};
-
-constexpr int kSahBins = 16;
-constexpr int kSahMaxLeaf = 4;
+// (SahNode2, SahRec, kSahBins, kSahMaxLeaf: rtg_internal.h, shared with the GPU build)
 constexpr int kWinMinPrims = 1;    // Geometry::win threshold (64: dragon 34.7 -> 35.2 ms, r3_ab_window.jsonl)
+constexpr int kSahGpuMin = 1 << 16;  // RTG_BVH_AUTO: traversal trees of meshes from this size on the GPU
 constexpr int kFlatMaxPrims = 8;   // Geometry::flat_count: meshes tested without a node (incl. a reference
                                    // root over two leaves)
 
@@ -455,13 +449,9 @@ inline double sah_area(const float lo[3], const float hi[3]) {
     return dx * dy + dy * dz + dz * dx;
 }
 
-// One triangle of the binned-SAH build: its box and face index, partitioned in place (32 B,
-// so the passes over a range stream through memory instead of gathering through an index array;
-// 1 M-triangle dragon: the tree's build went from 86 ms to ...).  The centroid is the box centre.
-struct SahRec {
-    float lo[3], hi[3];
-    int idx, pad_;
-};
+// One triangle of the binned-SAH build (SahRec): its box and face index, partitioned in place (32 B,
+// so the passes over a range stream through memory instead of gathering through an index array).
+// The centroid is the box centre.
 inline float sah_ctr(const SahRec& r, int z) { return 0.5f * (r.lo[z] + r.hi[z]); }
 
 // Node box and split of the SAH-ordered range [s, e) (partitions r[s, e)); returns the split
@@ -729,6 +719,32 @@ int sah_rec_par(SahRec* r, SahRec* tmp, int s, int e, std::vector<SahNode2>& out
     return me;
 }
 
+// Node count and an order-independent hash of a BVH2 (reachable nodes from `root`: the GPU build's
+// array may hold unused reserved slots): the sum over nodes of a mix of the box (-0 as +0) and the
+// triangle count, so two builds that chose the same splits hash alike whatever their node order.
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return x;
+}
+void sah_tree_stats(const SahNode2* bn, int root, uint64_t& count, uint64_t& hash) {
+    count = 0; hash = 0;
+    std::vector<int> stack{root};
+    while (!stack.empty()) {
+        const SahNode2& nd = bn[stack.back()];
+        stack.pop_back();
+        uint64_t h = (uint64_t)(uint32_t)nd.count * 0x9E3779B97F4A7C15ULL;
+        for (int z = 0; z < 3; z++) {
+            const float a = nd.lo[z] + 0.0f, b = nd.hi[z] + 0.0f;
+            uint32_t ua, ub;
+            memcpy(&ua, &a, 4); memcpy(&ub, &b, 4);
+            h = mix64(h ^ ((uint64_t)ua << 32 | ub) ^ (uint64_t)(z + 1));
+        }
+        hash += h;
+        count++;
+        if (nd.left >= 0) { stack.push_back(nd.left); stack.push_back(nd.right); }
+    }
+}
+
 // Collapse the SAH BVH2 into 4-wide nodes: each node's slots are its children, the interior
 // slot with the largest surface area replaced by its own two children while slots are free.
 // Slot info: < 0 empty, 0 interior (ref = Node4 index), > 0 leaf of `info` triangles at ref
@@ -743,7 +759,7 @@ struct Collapsed {
     float lo[3][4], hi[3][4];
     int ref[4], info[4];
 };
-Collapsed collapse_node(const std::vector<SahNode2>& bn, int n, int tri_base, float pad) {
+Collapsed collapse_node(const SahNode2* bn, int n, int tri_base, float pad) {
     Collapsed C;
     int* slot = C.slot;
     slot[0] = bn[n].left; slot[1] = bn[n].right; slot[2] = slot[3] = -1;
@@ -799,7 +815,7 @@ Node4 node4_of(const Collapsed& C) {
     return nd;
 }
 template <class V>
-int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad, V& out) {
+int sah_collapse(const SahNode2* bn, int n, int tri_base, float pad, V& out) {
     const int me = (int)out.size();
     out.emplace_back();
     Collapsed C = collapse_node(bn, n, tri_base, pad);
@@ -812,7 +828,7 @@ int sah_collapse(const std::vector<SahNode2>& bn, int n, int tri_base, float pad
 // triangles) collapsed on their own threads into their own arrays and appended with their interior
 // refs shifted.
 template <class V>
-int sah_collapse_par(const std::vector<SahNode2>& bn, int n, int tri_base, float pad, V& out, int depth) {
+int sah_collapse_par(const SahNode2* bn, int n, int tri_base, float pad, V& out, int depth) {
     if (depth <= 0 || bn[n].count < (1 << 16)) return sah_collapse(bn, n, tri_base, pad, out);
     const int me = (int)out.size();
     out.emplace_back();
@@ -1437,7 +1453,13 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     std::vector<char> pos_gated;             // ... and whether its leaf's parent (gates[]) is not the root
     std::vector<char> geom_finite(d->num_objects, 0);   // every primitive box coordinate finite
     hvec<int4> primidx;
-    bool early_upload = false;               // dnodes / gates / tris / primidx / orig_prim / vnormals already uploaded
+    bool early_upload = false;               // dnodes / gates / tris / primidx / orig_prim / vnormals uploaded by early_thread
+    std::thread early_thread;
+    int early_rc = RTG_OK;
+    struct EarlyJoin {                       // joined on every return path (the thread reads this frame's arrays)
+        std::thread& t;
+        ~EarlyJoin() { if (t.joinable()) t.join(); }
+    } early_join{early_thread};
     s->orig_prim.clear();
     s->bvh.assign(d->num_objects, ObjBVH());
     const float ieps = d->intersection_test_eps;
@@ -1497,7 +1519,13 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         }
         hvec<SahRec> sah_rec_buf, sah_tmp;
         hvec<int> sah_idx;
-        std::vector<SahNode2> sah_bn;
+        std::vector<SahNode2> sah_bn;            // host build (the GPU build collapses on the device)
+        bool sah_root_interior = false;
+        uint64_t sah_hash = 0, sah_bnodes = 0;
+        // the traversal tree on the GPU: large meshes of a device scene (the host recursion was the
+        // long pole of scene creation, ~75-85 ms for the dragon on its thread)
+        const bool sah_gpu = s->device >= 0 && (s->bvh_builder == RTG_BVH_GPU ||
+                                                (s->bvh_builder == RTG_BVH_AUTO && np >= kSahGpuMin));
         // the SAH thread also collapses its tree to 4-wide nodes (leaf refs from tri_base0, the
         // object's first traversal-order triangle) and forms the triangles' records in that order
         // (p2.yzw, which need the reference tree, are filled after the join)
@@ -1512,7 +1540,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         } sah_join{sah_thread};
         if (sah_try) {
             sah_rec_buf.resize(np);
-            sah_tmp.resize(np);
+            if (!sah_gpu) sah_tmp.resize(np);
             sah_idx.resize(np);
             parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
                 for (size_t f = k0; f < k1; f++) {
@@ -1522,19 +1550,35 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                     q.pad_ = 0;
                 }
             });
-            sah_bn.reserve(2 * (size_t)np / kSahMaxLeaf + 16);
+            if (!sah_gpu) sah_bn.reserve(2 * (size_t)np / kSahMaxLeaf + 16);
             sah_thread = std::thread([&] {
                 try {
                     PhaseClock tc;
-                    sah_rec_par(sah_rec_buf.data(), sah_tmp.data(), 0, np, sah_bn, sah_depth());
-                    parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
-                        for (size_t k = k0; k < k1; k++) sah_idx[k] = sah_rec_buf[k].idx;
-                    });
-                    tc.lap(" sah_tree (thread)");
-                    if (sah_bn[0].left >= 0) {
-                        sah_nodes.reserve((size_t)np / 2 + 16);
-                        sah_collapse_par(sah_bn, 0, tri_base0, obj_pad, sah_nodes, 3);
-                        tc.lap(" sah_collapse (thread)");
+                    if (sah_gpu) {                   // tree, collapse and hash on the device
+                        std::string e;
+                        if (hipSetDevice(s->device) != hipSuccess)
+                            throw std::runtime_error("GPU SAH build: hipSetDevice failed");
+                        auto alloc4 = [&](size_t c) { sah_nodes.resize(c); return sah_nodes.data(); };
+                        if (gpu_build_sah(sah_rec_buf.data(), np, tri_base0, obj_pad, alloc4, sah_idx.data(), sah_bnodes,
+                                          sah_hash, e))
+                            throw std::runtime_error("GPU SAH build: " + e);
+                        sah_root_interior = !sah_nodes.empty();
+                        tc.lap(" sah_tree+collapse gpu (thread)");
+                    } else {
+                        sah_rec_par(sah_rec_buf.data(), sah_tmp.data(), 0, np, sah_bn, sah_depth());
+                        parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
+                            for (size_t k = k0; k < k1; k++) sah_idx[k] = sah_rec_buf[k].idx;
+                        });
+                        tc.lap(" sah_tree (thread)");
+                        sah_tree_stats(sah_bn.data(), 0, sah_bnodes, sah_hash);
+                        sah_root_interior = sah_bn[0].left >= 0;
+                        if (sah_root_interior) {
+                            sah_nodes.reserve((size_t)np / 2 + 16);
+                            sah_collapse_par(sah_bn.data(), 0, tri_base0, obj_pad, sah_nodes, 3);
+                            tc.lap(" sah_collapse (thread)");
+                        }
+                    }
+                    if (sah_root_interior) {
                         sah_tris.resize(np);
                         parallel_chunks((size_t)np, 1 << 14, [&](int, size_t k0, size_t k1) {
                             for (size_t k = k0; k < k1; k++) sah_tris[k] = tri_geom(verts, pv, (size_t)sah_idx[k]);
@@ -1723,24 +1767,29 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         const bool sah_ok = sah_try && ob.root >= 0 && (hn[ob.root].left >= 0 || hn[ob.root].right >= 0);
         bs.records_ms += pc.lap("records");
         PhaseClock sub;
-        // The last object's reference-tree records are final now: while the SAH thread finishes,
-        // this thread uploads them (the rest goes up after the top level).  Dragon1m: the wait for
-        // the SAH thread was 30-45 ms, these uploads ~10 ms of it.
+        // The last object's reference-tree records are final now: a helper thread uploads them while
+        // this one finishes the traversal tree and the top level (joined before the remaining uploads;
+        // nothing below writes these arrays).  Dragon1m: ~7-10 ms of host-to-device copies.
         if (s->device >= 0 && i == d->num_objects - 1 && sah_thread.joinable()) {
-            int rc2;
-            if ((rc2 = upload(s->d_nodes, dnodes)) || (rc2 = upload(s->d_gates, gates)) || (rc2 = upload(s->d_tris, tris)) ||
-                (rc2 = upload(s->d_primidx, primidx)) || (rc2 = upload(s->d_origprim, s->orig_prim)) ||
-                (rc2 = upload(s->d_vnormals, s->vnormals)))
-                return rc2;
+            early_thread = std::thread([&, dev = s->device] {
+                if (hipSetDevice(dev) != hipSuccess) { early_rc = RTG_ERR_HIP; return; }
+                int rc2;
+                if ((rc2 = upload(s->d_nodes, dnodes)) || (rc2 = upload(s->d_gates, gates)) || (rc2 = upload(s->d_tris, tris)) ||
+                    (rc2 = upload(s->d_primidx, primidx)) || (rc2 = upload(s->d_origprim, s->orig_prim)) ||
+                    (rc2 = upload(s->d_vnormals, s->vnormals)))
+                    early_rc = rc2;
+            });
             early_upload = true;
-            sub.lap(" early_upload");
+            sub.lap(" early_upload start");
         }
         if (sah_thread.joinable()) sah_thread.join();
         if (sah_err) std::rethrow_exception(sah_err);
         sub.lap(" sah_join_wait");
         if (sah_ok) {
-            const std::vector<SahNode2>& bn = sah_bn;
-            if (bn[0].left >= 0) {
+            bs.traversal_nodes += sah_bnodes;
+            bs.traversal_hash += sah_hash;
+            if (sah_gpu) bs.sah_gpu_objects++;
+            if (sah_root_interior) {
                 // SAH leaf order: face index -> reference position (inverse of the median tree's
                 // perm); the thread's records get their reference position, leaf and gate flag
                 std::vector<int> pos_of(np);
@@ -2068,6 +2117,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     std::vector<float> tcflat;
     if (d->num_texcoords > 0) tcflat.assign(d->texcoords, d->texcoords + 2 * (size_t)d->num_texcoords);
     int rc;
+    if (early_thread.joinable()) early_thread.join();
+    if (early_rc != RTG_OK) return fail(early_rc, "scene upload (reference-tree records)");
     if (!early_upload &&
         ((rc = upload(s->d_nodes, dnodes)) || (rc = upload(s->d_gates, gates)) || (rc = upload(s->d_tris, tris)) ||
          (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_origprim, s->orig_prim)) ||

@@ -5,6 +5,7 @@
 #include <climits>
 #include <stdint.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -413,6 +414,20 @@ void launch_finalize(const float* acc, float* out, int nx, int ny, int row_offse
 void launch_hit_details(const SceneView& sv, const RayQ rays, const HitRec* hits, struct ::rtg_hit* out,
                         const int* orig_prim, int n, hipStream_t st);
 
+// Traversal-tree build records (rtg_host.cpp sah_split, rtg_sah_gpu.hip): one triangle's box and face
+// index (32 B; the centroid is the box centre), and the binned-SAH BVH2 node over a range of them.
+constexpr int kSahBins = 16;
+constexpr int kSahMaxLeaf = 4;
+struct SahRec {
+    float lo[3], hi[3];
+    int idx, pad_;
+};
+struct SahNode2 {
+    float lo[3], hi[3];
+    int left, right;          // children (-1 for a leaf)
+    int start, count;         // range in the SAH primitive order (interior nodes too)
+};
+
 // Multi-GPU rows gather: shard r's compact rows start at row prefix[r] of `recv`; every frame
 // row y is copied from its owning shard ((y / block) % nranks).  nranks <= kMaxRanks.
 constexpr int kMaxRanks = 64;
@@ -479,6 +494,14 @@ struct GpuBvh {
 };
 int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, int n, GpuBvh& out, std::string& err,
                   hipStream_t st);
+// GPU binned-SAH build of one mesh's traversal tree (rtg_sah_gpu.hip), collapsed to 4-wide nodes on the
+// device as rtg_host.cpp collapse_node does (slot boxes widened by `pad`, leaf refs from tri_base, interior
+// refs 0-based within the mesh, breadth-first): alloc4(count) returns host memory for the Node4 records
+// (count 0: the root is a leaf); the face index of every SAH position into order_host[n]; the binary
+// tree's node count and order-independent hash (sah_tree_stats).  Runs on its own non-blocking stream of
+// the calling thread's current device.
+int gpu_build_sah(const SahRec* recs_host, int n, int tri_base, float pad, const std::function<Node4*(size_t)>& alloc4,
+                  int* order_host, uint64_t& bvh2_nodes, uint64_t& hash, std::string& err);
 // Empty launches that load the GPU build's / the render kernels' code objects (scene-create warm-up).
 void gpu_bvh_warm(hipStream_t st);
 void device_warm(hipStream_t st);

@@ -152,7 +152,9 @@ class BuildStats(C.Structure):
                 ("tlas_nodes", C.c_int32), ("flat_group_entries", C.c_int32),
                 ("validate_ms", C.c_double), ("prep_ms", C.c_double), ("median_tree_ms", C.c_double),
                 ("records_ms", C.c_double), ("traversal_tree_ms", C.c_double), ("top_level_ms", C.c_double),
-                ("upload_ms", C.c_double), ("total_ms", C.c_double), ("upload_bytes", C.c_uint64)]
+                ("upload_ms", C.c_double), ("total_ms", C.c_double), ("upload_bytes", C.c_uint64),
+                ("sah_gpu_objects", C.c_int32), ("pad_abi8", C.c_int32), ("traversal_nodes", C.c_uint64),
+                ("traversal_hash", C.c_uint64)]
 
 
 RTG_BVH_AUTO, RTG_BVH_HOST, RTG_BVH_GPU = 0, 1, 2

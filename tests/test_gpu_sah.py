@@ -67,3 +67,78 @@ def test_sah_random_rays_match_oracle(gpu, name):
         m = ref["full"] == 1
         for key in ("t", "point", "normal"):
             assert np.array_equal(h[key][m].view(np.int32), ref[key][m].view(np.int32)), (tree, key)
+
+
+# ---------------------------------------------------------------- GPU-built traversal tree (round 5)
+HOST_B, GPU_B = 1, 2   # rtg_bvh_builder: RTG_BVH_HOST, RTG_BVH_GPU
+
+
+def _soup(n, seed, nx=40, ny=30):
+    """n random triangles (no two with the same centroid) in the unit cube, camera and a point light."""
+    from rtg import _abi as A
+    from rtg.scene import Light, Material, Object, Scene
+    rng = np.random.default_rng(seed)
+    sc = Scene(max_depth=2, background=(10, 10, 20), ambient=(20, 20, 20))
+    sc.cameras.append(scenegen._cam((0.5, 0.5, 3.0), (0, 0, -1), (0, 1, 0), nx, ny, fov_deg=40))
+    sc.materials.append(Material(ambient=(1, 1, 1), diffuse=(0.7, 0.6, 0.5), specular=(0.3, 0.3, 0.3), phong_exp=20))
+    c = rng.uniform(0, 1, (n, 1, 3))
+    v = (c + rng.normal(0, 0.02, (n, 3, 3))).astype(np.float32).reshape(-1, 3)
+    b = scenegen._add_vertices(sc, v)
+    faces = (np.arange(3 * n, dtype=np.int32).reshape(n, 3) + b).astype(np.int32)
+    sc.objects.append(Object(type=A.OBJ_MESH, id=1, material=1, faces=faces))
+    sc.lights.append(Light(type=A.LIGHT_POINT, position=(0.5, 3, 3), intensity=(800, 800, 800)))
+    return sc
+
+
+def _tree(sc, builder):
+    with rtg.Renderer(sc, device=0, bvh_builder=builder) as r:
+        bs = r.build_stats()
+        img = r.render(0)
+    return bs, img
+
+
+@pytest.mark.parametrize("n", [2, 5, 300, 2048, 2049, 5000, 70000])
+def test_gpu_sah_tree_equals_host_tree(gpu, n):
+    """The GPU binned-SAH build applies the host's split rule to the same record sets, so both trees
+    have the same nodes (box + triangle count; order-independent hash) and every frame is identical.
+    Sizes around the one-wave subtree limit (2048) and the level phase (70000)."""
+    sc = _soup(n, seed=n)
+    bh, ih = _tree(sc, HOST_B)
+    bg, ig = _tree(sc, GPU_B)
+    assert bh["sah_gpu_objects"] == 0 and bg["sah_gpu_objects"] == 1
+    assert bg["traversal_nodes"] == bh["traversal_nodes"] > 0
+    assert bg["traversal_hash"] == bh["traversal_hash"]
+    assert np.array_equal(_bits(ig), _bits(ih))
+
+
+def test_gpu_sah_dragon_tree_and_frames(gpu):
+    """The C3 mesh at 160 K triangles: the level phase, then subtrees; same tree as the host's, frames
+    and random hit records bit-identical to the oracle."""
+    sc = scenegen.dragon1m(48, 27, spp=2, nu=400, nv=200)
+    bh, ih = _tree(sc, HOST_B)
+    bg, ig = _tree(sc, GPU_B)
+    assert bg["sah_gpu_objects"] >= 1
+    assert bg["traversal_hash"] == bh["traversal_hash"] and bg["traversal_nodes"] == bh["traversal_nodes"]
+    ref = pyoracle.Oracle(sc).render(0)[0]
+    assert np.array_equal(_bits(ig), _bits(ref))
+
+
+def test_gpu_sah_duplicate_centroids_match_oracle(gpu):
+    """Ranges whose centroids are all equal are halved by count; the two builders may then put
+    different members in each half (trees may differ), but every result stays the oracle's."""
+    sc = _soup(3000, seed=7)
+    v = np.asarray(sc.vertices, np.float32).copy()
+    v[-3 * 600:] = np.tile(v[-3:], (600, 1))                   # 600 copies of one triangle
+    sc.vertices = v
+    _, ig = _tree(sc, GPU_B)
+    ref = pyoracle.Oracle(sc).render(0)[0]
+    assert np.array_equal(_bits(ig), _bits(ref))
+    rng = np.random.default_rng(3)
+    o = rng.uniform(-0.5, 1.5, (20000, 3)).astype(np.float32)
+    d = rng.standard_normal((20000, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    with rtg.Renderer(sc, device=0, bvh_builder=GPU_B) as r:
+        h = r.trace(o, d)
+    hr = pyoracle.Oracle(sc).trace(o, d)
+    for key in ("full", "object", "prim"):
+        assert np.array_equal(h[key], hr[key]), key
