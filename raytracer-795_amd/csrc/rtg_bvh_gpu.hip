@@ -16,7 +16,10 @@
 //     position).  lessPrefix(j) < j, so the chains are resolved by pointer jumping.
 //   * boxes: min / max of the primitive boxes over the node's range in the order the reference
 //     sees it; ties between equal values (+0 / -0) keep the earliest element, as the reference's
-//     `a <= b ? a : b` fold does.  Non-finite inputs are rejected (the host builder handles them).
+//     `a <= b ? a : b` fold does -- per level, as (value, position) keys reduced with 64-bit atomics
+//     over runs of positions (round 5; the one-block-per-node reduction it replaced ran a handful of
+//     blocks at the top levels, ~8 ms of a 1 M-triangle build).  Non-finite inputs are rejected (the
+//     host builder handles them).
 //   * leaves: one primitive, or depth 30 (possibly empty); empty ranges below depth 30 are null.
 //
 // Node numbering here is breadth-first; the host converts to the reference's pre-order.
@@ -37,7 +40,6 @@ namespace rtg {
 namespace {
 
 constexpr int kMaxDepth = 30;      // src/BVH.cpp:67
-constexpr int kBigNode = 512;      // box reduction: one block per node from this length on
 
 __device__ __forceinline__ uint32_t ord_bits(float f) {
     const uint32_t u = __float_as_uint(f);
@@ -164,8 +166,7 @@ __global__ void k_child_count(const Seg* __restrict__ segs, int S, int depth1, c
 }
 __global__ void k_child_emit(const Seg* __restrict__ segs, int S, int depth1, const int* __restrict__ G,
                              const int* __restrict__ node_off, const int* __restrict__ int_off, int node_base,
-                             int4* __restrict__ nodes, Seg* __restrict__ next, int* __restrict__ big,
-                             int* __restrict__ nbig) {
+                             int4* __restrict__ nodes, Seg* __restrict__ next) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
     const Seg g = segs[s];
@@ -179,7 +180,6 @@ __global__ void k_child_emit(const Seg* __restrict__ segs, int S, int depth1, co
         if (kind == 0) continue;
         child[q] = id;
         nodes[id] = make_int4(-1, -1, r0[q], r1[q]);
-        if (len >= kBigNode) big[atomicAdd(nbig, 1)] = id;
         if (kind == 2) { Seg c; c.start = r0[q]; c.end = r1[q]; c.node = id; c.off = 0; next[nx++] = c; }
         id++;
     }
@@ -197,80 +197,80 @@ __global__ void k_seg_off(Seg* __restrict__ segs, int S, const int* __restrict__
     if (s < S) segs[s].off = off[s];
 }
 
-// ComputeBoundingBox (src/BVH.cpp:268-303): min/max with ties -> earliest element.
-struct MinMax {
-    float v[6];     // min xyz, max xyz
-    int at[6];      // position that supplied the value (-1: the FLT_MAX / -FLT_MAX start)
-};
-__device__ __forceinline__ void mm_init(MinMax& m) {
-    for (int z = 0; z < 3; z++) { m.v[z] = FLT_MAX; m.v[3 + z] = -FLT_MAX; m.at[z] = m.at[3 + z] = -1; }
+// ComputeBoundingBox (src/BVH.cpp:268-303): min / max over the node's range in the order the reference
+// sees it when it creates the node (after its parent's partition), ties between equal values (+0 / -0)
+// to the earliest element (the fold `if (!(m <= v)) m = v`).  Per level, right after the partition:
+// every position of a split range adds its box to its child's keys -- 64-bit (value, position) keys
+// with -0 folded into +0, so atomicMin picks the least value and, among equal ones, the earliest
+// position; the box then takes that element's own value (its sign of zero).  Runs of 16 positions per
+// lane, wave-merged when the whole wave feeds one node (the top levels), one atomic per key otherwise.
+__device__ __forceinline__ unsigned long long kmin_of(float v, int pos) {
+    return ((unsigned long long)ord_bits(v + 0.0f) << 32) | (unsigned)pos;
 }
-__device__ __forceinline__ void mm_push(MinMax& m, int pos, const float* lo, const float* hi) {   // in order
-    for (int z = 0; z < 3; z++) {
-        if (!(m.v[z] <= lo[z])) { m.v[z] = lo[z]; m.at[z] = pos; }
-        if (!(m.v[3 + z] >= hi[z])) { m.v[3 + z] = hi[z]; m.at[3 + z] = pos; }
+__device__ __forceinline__ unsigned long long kmax_of(float v, int pos) {
+    return ((unsigned long long)ord_bits(v + 0.0f) << 32) | (0xFFFFFFFFu - (unsigned)pos);
+}
+constexpr int kRun = 16;
+__global__ void __launch_bounds__(256) k_box_keys(int n, bool root, const int* __restrict__ segid, int S,
+                                                  const Seg* __restrict__ segs, const int* __restrict__ G,
+                                                  const int4* __restrict__ nodes, const int* __restrict__ perm,
+                                                  const float* __restrict__ lo3, const float* __restrict__ hi3,
+                                                  unsigned long long* __restrict__ kmin,
+                                                  unsigned long long* __restrict__ kmax) {
+    const int p0 = (blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+    int cur = -1;
+    unsigned long long a[3], b[3];
+    auto flush = [&]() {
+        for (int z = 0; z < 3; z++) {
+            atomicMin(&kmin[3 * (size_t)cur + z], a[z]);
+            atomicMax(&kmax[3 * (size_t)cur + z], b[z]);
+        }
+    };
+    for (int p = p0; p < min(n, p0 + kRun); p++) {
+        int o = 0;
+        if (!root) {
+            const int sid = segid[p];
+            if (sid >= S) continue;
+            const Seg g = segs[sid];
+            const int k = G[g.end] - G[g.start];
+            const int4 pn = nodes[g.node];
+            o = p < g.start + k ? pn.x : pn.y;
+        }
+        if (o != cur) {
+            if (cur >= 0) flush();
+            cur = o;
+            for (int z = 0; z < 3; z++) { a[z] = ~0ull; b[z] = 0ull; }
+        }
+        const int f = perm[p];
+        for (int z = 0; z < 3; z++) {
+            a[z] = min(a[z], kmin_of(lo3[3 * f + z], p));
+            b[z] = max(b[z], kmax_of(hi3[3 * f + z], p));
+        }
+    }
+    // the last run's partial: merged over the wave when every lane holds one for the same node
+    const int c0 = __shfl(cur, 0);
+    if (__ballot(cur != c0) == 0ull && c0 >= 0) {
+        for (int off = 32; off > 0; off >>= 1)
+            for (int z = 0; z < 3; z++) {
+                a[z] = min(a[z], (unsigned long long)__shfl_xor((long long)a[z], off));
+                b[z] = max(b[z], (unsigned long long)__shfl_xor((long long)b[z], off));
+            }
+        if ((threadIdx.x & 63) == 0) flush();
+    } else if (cur >= 0) {
+        flush();
     }
 }
-__device__ __forceinline__ void mm_merge(MinMax& a, const MinMax& b) {   // order-independent (value, position)
-    for (int z = 0; z < 6; z++) {
-        const bool take = (z < 3) ? (b.v[z] < a.v[z] || (b.v[z] == a.v[z] && b.at[z] < a.at[z]))
-                                  : (b.v[z] > a.v[z] || (b.v[z] == a.v[z] && b.at[z] < a.at[z]));
-        if (take) { a.v[z] = b.v[z]; a.at[z] = b.at[z]; }
-    }
-}
-__global__ void k_box_small(const int4* __restrict__ nodes, int first, int count, const int* __restrict__ perm,
-                            const float* __restrict__ lo3, const float* __restrict__ hi3, float* __restrict__ box) {
+__global__ void k_box_final(int first, int count, const int* __restrict__ perm, const float* __restrict__ lo3,
+                            const float* __restrict__ hi3, const unsigned long long* __restrict__ kmin,
+                            const unsigned long long* __restrict__ kmax, float* __restrict__ box) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
-    const int id = first + t;
-    const int4 nd = nodes[id];
-    if (nd.w - nd.z >= kBigNode) return;
-    MinMax m;
-    mm_init(m);
-    for (int p = nd.z; p < nd.w; p++) {
-        const int f = perm[p];
-        mm_push(m, p, lo3 + 3 * f, hi3 + 3 * f);
-    }
-    for (int z = 0; z < 6; z++) box[6 * (size_t)id + z] = m.v[z];
-}
-__global__ void __launch_bounds__(256) k_box_big(const int* __restrict__ big, const int* __restrict__ nbig,
-                                                 const int4* __restrict__ nodes,
-                                                 const int* __restrict__ perm, const float* __restrict__ lo3,
-                                                 const float* __restrict__ hi3, float* __restrict__ box) {
-    __shared__ MinMax sm[256];
-    if ((int)blockIdx.x >= *nbig) return;       // grid sized by an upper bound
-    const int id = big[blockIdx.x];
-    const int4 nd = nodes[id];
-    const int len = nd.w - nd.z;
-    const int per = (len + 255) / 256;
-    const int a = nd.z + threadIdx.x * per, b = min(nd.w, a + per);   // contiguous chunk per thread
-    MinMax m;
-    mm_init(m);
-    for (int p = a; p < b; p++) {
-        const int f = perm[p];
-        mm_push(m, p, lo3 + 3 * f, hi3 + 3 * f);
-    }
-    // the chunk's start values carry at = -1 only if the chunk is empty; make them lose ties
-    for (int z = 0; z < 6; z++) if (m.at[z] < 0) m.at[z] = INT_MAX;
-    sm[threadIdx.x] = m;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) {
-            MinMax x = sm[threadIdx.x];
-            mm_merge(x, sm[threadIdx.x + w]);
-            sm[threadIdx.x] = x;
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        MinMax r;
-        mm_init(r);              // the fold starts from FLT_MAX / -FLT_MAX (earliest of all)
-        MinMax x = sm[0];
-        for (int z = 0; z < 6; z++) {
-            const bool take = (z < 3) ? (x.v[z] < r.v[z]) : (x.v[z] > r.v[z]);
-            if (take) r.v[z] = x.v[z];
-        }
-        for (int z = 0; z < 6; z++) box[6 * (size_t)id + z] = r.v[z];
+    const size_t id = (size_t)first + t;
+    for (int z = 0; z < 3; z++) {
+        const unsigned long long a = kmin[3 * id + z], b = kmax[3 * id + z];
+        // an empty leaf (depth 30) keeps the fold's start values
+        box[6 * id + z] = a == ~0ull ? FLT_MAX : lo3[3 * perm[(unsigned)a] + z];
+        box[6 * id + 3 + z] = b == 0ull ? -FLT_MAX : hi3[3 * perm[0xFFFFFFFFu - (unsigned)b] + z];
     }
 }
 
@@ -279,20 +279,24 @@ __global__ void k_iota(int n, int* p) {
     if (i < n) p[i] = i;
 }
 
+// Scratch arrays allocated and freed in stream order (hipMallocAsync / hipFreeAsync): hipFree waits for
+// the whole device, and the median-tree and traversal-tree builds run side by side on two streams.
 template <class T>
 struct DevArr {
     T* p = nullptr;
     size_t cap = 0;
+    hipStream_t st = nullptr;
+    explicit DevArr(hipStream_t s = nullptr) : st(s) {}
     hipError_t grow(size_t n) {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFreeAsync(p, st);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipMalloc(&p, sizeof(T) * (n + 16));
+        hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&p), sizeof(T) * (n + 16), st);
         if (e == hipSuccess) cap = n + 16;
         return e;
     }
-    ~DevArr() { if (p) (void)hipFree(p); }
+    ~DevArr() { if (p) (void)hipFreeAsync(p, st); }
 };
 
 inline int nb(long long n, int b) { return (int)((n + b - 1) / b); }
@@ -325,20 +329,19 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
         fprintf(stderr, "[rtg] gpu bvh %-10s %7.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
         t_last = t;
     };
-    DevArr<float> c3, lo3, hi3, box;
-    DevArr<int> perm, perm2, segid, less, G, ptr, lens, offs, nn, ni, nnoff, nioff, big, cnt;
-    DevArr<int4> nodes;
-    DevArr<unsigned long long> keys, sorted;
-    DevArr<Seg> segs, next;
-    DevArr<float> split;
-    DevArr<unsigned char> tmp;
+    DevArr<float> c3(st), lo3(st), hi3(st), box(st);
+    DevArr<int> perm(st), perm2(st), segid(st), less(st), G(st), ptr(st), lens(st), offs(st), nn(st), ni(st), nnoff(st), nioff(st);
+    DevArr<int4> nodes(st);
+    DevArr<unsigned long long> keys(st), sorted(st);
+    DevArr<Seg> segs(st), next(st);
+    DevArr<float> split(st);
+    DevArr<unsigned char> tmp(st);
     BVH_TRY(c3.grow(3 * (size_t)n)); BVH_TRY(lo3.grow(3 * (size_t)n)); BVH_TRY(hi3.grow(3 * (size_t)n));
     BVH_TRY(hipMemcpyAsync(c3.p, centers, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
     BVH_TRY(hipMemcpyAsync(lo3.p, bmin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
     BVH_TRY(hipMemcpyAsync(hi3.p, bmax, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
     BVH_TRY(perm.grow(n)); BVH_TRY(perm2.grow(n)); BVH_TRY(segid.grow(n)); BVH_TRY(less.grow(n + 1));
     BVH_TRY(G.grow(n + 1)); BVH_TRY(ptr.grow(n)); BVH_TRY(keys.grow(n)); BVH_TRY(sorted.grow(n));
-    BVH_TRY(big.grow(2 * (size_t)n + 64)); BVH_TRY(cnt.grow(4));
     // per-segment arrays: a level has at most n / 2 interior segments
     const size_t scap = (size_t)n / 2 + 2;
     BVH_TRY(split.grow(scap)); BVH_TRY(lens.grow(scap)); BVH_TRY(offs.grow(scap)); BVH_TRY(nn.grow(scap));
@@ -354,13 +357,13 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
     int num_nodes = 1;
     const int4 root = make_int4(-1, -1, 0, n);
     BVH_TRY(hipMemcpyAsync(nodes.p, &root, sizeof(int4), hipMemcpyHostToDevice, st));
-    {
-        const int rb[2] = {0, 1};     // big list {root}, count 1
-        BVH_TRY(hipMemcpyAsync(big.p, &rb[0], sizeof(int), hipMemcpyHostToDevice, st));
-        BVH_TRY(hipMemcpyAsync(cnt.p, &rb[1], sizeof(int), hipMemcpyHostToDevice, st));
-        if (n >= kBigNode) hipLaunchKernelGGL(k_box_big, dim3(1), dim3(256), 0, st, big.p, cnt.p, nodes.p, perm.p, lo3.p, hi3.p, box.p);
-        else hipLaunchKernelGGL(k_box_small, dim3(1), dim3(64), 0, st, nodes.p, 0, 1, perm.p, lo3.p, hi3.p, box.p);
-    }
+    DevArr<unsigned long long> kmin(st), kmax(st);       // (value, position) box keys per node
+    BVH_TRY(kmin.grow(3 * node_cap)); BVH_TRY(kmax.grow(3 * node_cap));
+    BVH_TRY(hipMemsetAsync(kmin.p, 0xFF, sizeof(unsigned long long) * 3, st));
+    BVH_TRY(hipMemsetAsync(kmax.p, 0, sizeof(unsigned long long) * 3, st));
+    hipLaunchKernelGGL(k_box_keys, dim3(nb(nb(n, kRun), 256)), dim3(256), 0, st, n, true, segid.p, 0, segs.p, G.p, nodes.p,
+                       perm.p, lo3.p, hi3.p, kmin.p, kmax.p);
+    hipLaunchKernelGGL(k_box_final, dim3(1), dim3(64), 0, st, 0, 1, perm.p, lo3.p, hi3.p, kmin.p, kmax.p, box.p);
     int S = 0;
     if (n >= 2) {
         Seg s0; s0.start = 0; s0.end = n; s0.node = 0; s0.off = 0;
@@ -414,29 +417,25 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
         if ((size_t)(num_nodes + new_nodes) > node_cap) {       // grow the node arrays, keeping contents
             size_t cap2 = std::max(node_cap * 2, (size_t)(num_nodes + new_nodes) + 64);
             int4* n2 = nullptr; float* b2 = nullptr;
-            BVH_TRY(hipMalloc(&n2, sizeof(int4) * cap2));
-            BVH_TRY(hipMalloc(&b2, sizeof(float) * 6 * cap2));
+            BVH_TRY(hipMallocAsync(reinterpret_cast<void**>(&n2), sizeof(int4) * cap2, st));
+            BVH_TRY(hipMallocAsync(reinterpret_cast<void**>(&b2), sizeof(float) * 6 * cap2, st));
             BVH_TRY(hipMemcpyAsync(n2, nodes.p, sizeof(int4) * num_nodes, hipMemcpyDeviceToDevice, st));
             BVH_TRY(hipMemcpyAsync(b2, box.p, sizeof(float) * 6 * num_nodes, hipMemcpyDeviceToDevice, st));
-            BVH_TRY(hipStreamSynchronize(st));
-            (void)hipFree(nodes.p); (void)hipFree(box.p);
+            (void)hipFreeAsync(nodes.p, st); (void)hipFreeAsync(box.p, st);
             nodes.p = n2; nodes.cap = cap2; box.p = b2; box.cap = 6 * cap2;
             node_cap = cap2;
-            BVH_TRY(big.grow(cap2));
         }
-        int zero = 0;
-        BVH_TRY(hipMemcpyAsync(cnt.p, &zero, sizeof(int), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_child_emit, dim3(nb(S, 256)), dim3(256), 0, st, segs.p, S, depth + 1, G.p, nnoff.p, nioff.p,
-                           num_nodes, nodes.p, next.p, big.p, cnt.p);
-        // boxes of the new nodes over their ranges in the partitioned order (big ones: one block
-        // each; their count is bounded by n / kBigNode, the exact count stays on the device)
+                           num_nodes, nodes.p, next.p);
+        // the new nodes' boxes over their ranges in the order just formed
         if (new_nodes > 0) {
-            hipLaunchKernelGGL(k_box_small, dim3(nb(new_nodes, 256)), dim3(256), 0, st, nodes.p, num_nodes, new_nodes,
-                               perm.p, lo3.p, hi3.p, box.p);
-            const int max_big = std::min(new_nodes, n / kBigNode + 2);
-            if (n >= kBigNode)
-                hipLaunchKernelGGL(k_box_big, dim3(max_big), dim3(256), 0, st, big.p, cnt.p, nodes.p, perm.p, lo3.p, hi3.p,
-                                   box.p);
+            BVH_TRY(kmin.grow(3 * node_cap)); BVH_TRY(kmax.grow(3 * node_cap));
+            BVH_TRY(hipMemsetAsync(kmin.p + 3 * (size_t)num_nodes, 0xFF, sizeof(unsigned long long) * 3 * new_nodes, st));
+            BVH_TRY(hipMemsetAsync(kmax.p + 3 * (size_t)num_nodes, 0, sizeof(unsigned long long) * 3 * new_nodes, st));
+            hipLaunchKernelGGL(k_box_keys, dim3(nb(nb(n, kRun), 256)), dim3(256), 0, st, n, false, segid.p, S, segs.p, G.p,
+                               nodes.p, perm.p, lo3.p, hi3.p, kmin.p, kmax.p);
+            hipLaunchKernelGGL(k_box_final, dim3(nb(new_nodes, 256)), dim3(256), 0, st, num_nodes, new_nodes, perm.p,
+                               lo3.p, hi3.p, kmin.p, kmax.p, box.p);
         }
         BVH_TRY(hipGetLastError());
         num_nodes += new_nodes;

@@ -40,7 +40,7 @@ namespace {
 
 constexpr int kBins = kSahBins;
 constexpr int kLeaf = kSahMaxLeaf;
-constexpr int kSmall = 2048;       // ranges of at most this many records: one wave per subtree
+constexpr int kSmall = 512;        // ranges of at most this many records: one wave per subtree
 constexpr int kChunk = 4096;       // records per workgroup in the level passes
 constexpr int kStack = 24;         // subtree stack (the larger child is pushed: depth <= log2(kSmall) + 1)
 
@@ -507,20 +507,24 @@ __global__ void k_hash(const SahNode2* __restrict__ bn, int nn, unsigned long lo
     if ((threadIdx.x & 63) == 0 && c) { atomicAdd(out, h); atomicAdd(out + 1, c); }
 }
 
+// Scratch arrays allocated and freed in stream order (hipMallocAsync / hipFreeAsync): hipFree waits for
+// the whole device, and the median-tree and traversal-tree builds run side by side on two streams.
 template <class T>
 struct DevArr {
     T* p = nullptr;
     size_t cap = 0;
+    hipStream_t st = nullptr;
+    explicit DevArr(hipStream_t s = nullptr) : st(s) {}
     hipError_t grow(size_t n) {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFreeAsync(p, st);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipMalloc(&p, sizeof(T) * (n + 16));
+        hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&p), sizeof(T) * (n + 16), st);
         if (e == hipSuccess) cap = n + 16;
         return e;
     }
-    ~DevArr() { if (p) (void)hipFree(p); }
+    ~DevArr() { if (p) (void)hipFreeAsync(p, st); }
 };
 
 }  // namespace
@@ -552,15 +556,15 @@ int gpu_build_sah(const SahRec* recs_host, int n, int tri_base, float pad, const
         fprintf(stderr, "[rtg] gpu sah %-10s %7.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
         t_last = t;
     };
-    DevArr<SahRec> A, B;
-    DevArr<SahNode2> nodes;
-    DevArr<int> flags, G, order, ncount;
-    DevArr<unsigned> acc, bins;
-    DevArr<LSeg> dsegs;
-    DevArr<Decision> ddec;
-    DevArr<SSeg> dsmall;
-    DevArr<int2> dlinks;
-    DevArr<unsigned char> tmp;
+    DevArr<SahRec> A(st), B(st);
+    DevArr<SahNode2> nodes(st);
+    DevArr<int> flags(st), G(st), order(st), ncount(st);
+    DevArr<unsigned> acc(st), bins(st);
+    DevArr<LSeg> dsegs(st);
+    DevArr<Decision> ddec(st);
+    DevArr<SSeg> dsmall(st);
+    DevArr<int2> dlinks(st);
+    DevArr<unsigned char> tmp(st);
     const size_t node_cap = 2 * (size_t)n + 2;
     SAH_TRY(A.grow(n)); SAH_TRY(B.grow(n)); SAH_TRY(nodes.grow(node_cap));
     SAH_TRY(hipMemsetAsync(nodes.p, 0xFF, sizeof(SahNode2) * node_cap, st));   // count -1: never written
@@ -642,7 +646,7 @@ int gpu_build_sah(const SahRec* recs_host, int n, int tri_base, float pad, const
     hipLaunchKernelGGL(k_order, dim3((n + 255) / 256), dim3(256), 0, st, A.p, n, order.p);
     SAH_TRY(hipMemcpyAsync(order_host, order.p, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost, st));
     // hash + count of the binary nodes
-    DevArr<unsigned long long> hc;
+    DevArr<unsigned long long> hc(st);
     SAH_TRY(hc.grow(2));
     SAH_TRY(hipMemsetAsync(hc.p, 0, 2 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_hash, dim3((num_nodes + 255) / 256), dim3(256), 0, st, nodes.p, num_nodes, hc.p);
@@ -656,8 +660,8 @@ int gpu_build_sah(const SahRec* recs_host, int n, int tri_base, float pad, const
     bvh2_nodes = hch[1];
     lap("order+hash");
     if (root.left < 0) { alloc4(0); return 0; }
-    DevArr<Node4> n4;
-    DevArr<int> Q, Qn, cnt, off;
+    DevArr<Node4> n4(st);
+    DevArr<int> Q(st), Qn(st), cnt(st), off(st);
     const size_t cap4 = (size_t)num_nodes;        // at most one Node4 per binary node
     SAH_TRY(n4.grow(cap4)); SAH_TRY(Q.grow(cap4)); SAH_TRY(Qn.grow(cap4)); SAH_TRY(cnt.grow(cap4 + 1)); SAH_TRY(off.grow(cap4 + 1));
     const int zero = 0;

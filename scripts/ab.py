@@ -10,7 +10,9 @@ fn, spp = {"bunny": ("bunny5k", 1), "cornell_pt": ("cornell_pt", 256)}.get(w, (w
 sc = getattr(scenegen, fn)(1920, 1080, spp=spp)
 # AB_OPTS "key=int,key=int": render options of this variant (e.g. tile_band=8)
 kw = {k: int(v) for k, v in (p.split("=") for p in os.environ.get("AB_OPTS", "").split(",") if p)}
-r = rtg.Renderer(sc, 0)
+# AB_BUILD "key=int,...": build options (e.g. bvh_builder=1)
+bkw = {k: int(v) for k, v in (p.split("=") for p in os.environ.get("AB_BUILD", "").split(",") if p)}
+r = rtg.Renderer(sc, 0, **bkw)
 r.render(0, **kw)
 ms = []
 for _ in range(int(os.environ.get("AB_FRAMES", "5"))):

@@ -15,7 +15,8 @@ import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 print(f"{'kernel':48s} {'calls':>6s} {'total_ms':>10s} {'avg_us':>9s} {'pct':>6s}")
 for r in rows:
-    print(f"{r['Name'].split('(')[0].replace('void ', '')[:48]:48s} {r['Calls']:>6s} "
+    nm = r['Name'].replace('(anonymous namespace)::', '').replace('void ', '').split('(')[0]
+    print(f"{nm[:48]:48s} {r['Calls']:>6s} "
           f"{float(r['TotalDurationNs'])/1e6:10.2f} {float(r['AverageNs'])/1e3:9.1f} {float(r['Percentage']):6.2f}")
 # combined closest-hit line (GEN=true level-0 + GEN=false secondary launches): the kernel whose
 # average bench.py's roofline.avg_launch_ms measures
