@@ -27,8 +27,10 @@
 #include <limits.h>
 
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <mutex>
 #include <cstdlib>
 
 #include <string>
@@ -274,6 +276,18 @@ __global__ void k_box_final(int first, int count, const int* __restrict__ perm, 
     }
 }
 
+struct NodeRec40 { int c[4]; float b[6]; };   // = rtg_host.cpp HNode (4-byte aligned: 40 B, no padding)
+static_assert(sizeof(NodeRec40) == 40, "40-byte node record");
+__global__ void k_node40(const int4* __restrict__ nodes, const float* __restrict__ box, int nn, NodeRec40* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nn) return;
+    NodeRec40 r;
+    const int4 c = nodes[i];
+    r.c[0] = c.x; r.c[1] = c.y; r.c[2] = c.z; r.c[3] = c.w;
+    for (int z = 0; z < 6; z++) r.b[z] = box[6 * (size_t)i + z];
+    out[i] = r;
+}
+
 __global__ void k_iota(int n, int* p) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = i;
@@ -317,8 +331,9 @@ void gpu_bvh_warm(hipStream_t st) { hipLaunchKernelGGL(k_iota, dim3(1), dim3(64)
 
 int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, int n, GpuBvh& out, std::string& err,
                   hipStream_t st) {
-    out = GpuBvh();
-    if (n <= 0) { out.root = -1; return 0; }
+    out.num_nodes = 0;
+    out.root = -1;
+    if (n <= 0) return 0;
     // RTG_BUILD_TIMING: wall time of the build's stages on stderr (synchronising between them)
     const bool timing = getenv("RTG_BUILD_TIMING") != nullptr;
     auto t_last = std::chrono::steady_clock::now();
@@ -444,16 +459,49 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
         S = S_next;
     }
     lap("levels");
-    BVH_TRY(out.perm.alloc(n));
-    BVH_TRY(out.nodes.alloc(num_nodes));
-    BVH_TRY(out.box.alloc(6 * (size_t)num_nodes));
+    // the host's node layout on the device (one 40-byte record per node), then both arrays into pooled
+    // page-locked staging
+    DevArr<NodeRec40> rec(st);
+    BVH_TRY(rec.grow(num_nodes));
+    hipLaunchKernelGGL(k_node40, dim3(nb(num_nodes, 256)), dim3(256), 0, st, nodes.p, box.p, num_nodes, rec.p);
+    if (!out.perm.get(sizeof(int) * (size_t)n) || !out.nodes.get(sizeof(NodeRec40) * (size_t)num_nodes)) {
+        err = "page-locked staging allocation failed";
+        return -1;
+    }
     BVH_TRY(hipMemcpyAsync(out.perm.p, perm.p, sizeof(int) * n, hipMemcpyDeviceToHost, st));
-    BVH_TRY(hipMemcpyAsync(out.nodes.p, nodes.p, sizeof(int4) * num_nodes, hipMemcpyDeviceToHost, st));
-    BVH_TRY(hipMemcpyAsync(out.box.p, box.p, sizeof(float) * 6 * num_nodes, hipMemcpyDeviceToHost, st));
+    BVH_TRY(hipMemcpyAsync(out.nodes.p, rec.p, sizeof(NodeRec40) * num_nodes, hipMemcpyDeviceToHost, st));
     BVH_TRY(hipStreamSynchronize(st));
+    out.num_nodes = num_nodes;
     lap("d2h");
     out.root = 0;
     return 0;
+}
+
+// Process-wide pool of page-locked staging buffers (first fit, kept for the process's lifetime).
+namespace {
+std::mutex g_pool_mu;
+std::vector<std::pair<void*, size_t>> g_pool;
+}
+void* pinned_pool_get(size_t bytes) {
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        size_t best = g_pool.size();
+        for (size_t k = 0; k < g_pool.size(); k++)
+            if (g_pool[k].second >= bytes && (best == g_pool.size() || g_pool[k].second < g_pool[best].second)) best = k;
+        if (best < g_pool.size()) {
+            void* p = g_pool[best].first;
+            g_pool.erase(g_pool.begin() + best);
+            return p;
+        }
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+void pinned_pool_put(void* p, size_t bytes) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.emplace_back(p, bytes);
 }
 
 }  // namespace rtg

@@ -1646,21 +1646,17 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             sub.lap(" gpu_build");
             ob.perm.resize(np);
             parallel_chunks((size_t)np, 1 << 16, [&](int, size_t k0, size_t k1) {
-                std::copy(gb.perm.p + k0, gb.perm.p + k1, ob.perm.data() + k0);
+                memcpy(ob.perm.data() + k0, gb.perm.as<int>() + k0, sizeof(int) * (k1 - k0));
             });
             // the nodes stay in the build's breadth-first order: the device records below number
             // the interior nodes in any order (they follow child links), and only the introspection
-            // call needs the reference's pre-order (rtg_scene_object_bvh converts)
-            const int nn = (int)gb.nodes.size();
+            // call needs the reference's pre-order (rtg_scene_object_bvh converts).  The build hands
+            // them over in HNode's layout.
+            static_assert(sizeof(HNode) == 40, "HNode = the GPU build's 40-byte node record");
+            const int nn = gb.num_nodes;
             ob.nodes.resize(nn);
             parallel_chunks((size_t)nn, 1 << 15, [&](int, size_t k0, size_t k1) {
-                for (size_t id = k0; id < k1; id++) {
-                    const int4 c = gb.nodes[id];
-                    HNode h;
-                    h.left = c.x; h.right = c.y; h.start = c.z; h.end = c.w;
-                    for (int z = 0; z < 3; z++) { h.mn[z] = gb.box[6 * id + z]; h.mx[z] = gb.box[6 * id + 3 + z]; }
-                    ob.nodes[id] = h;
-                }
+                memcpy(ob.nodes.data() + k0, gb.nodes.as<HNode>() + k0, sizeof(HNode) * (k1 - k0));
             });
             ob.bfs = true;
             ob.root = nn > 0 ? 0 : -1;

@@ -484,12 +484,27 @@ struct PinnedBuf {
     const T& operator[](size_t i) const { return p[i]; }
 };
 
-// The GPU median-split build's result: nodes in breadth-first order (children after their parent),
-// {left, right, start, end} and the boxes (6 floats) per node, and the primitive permutation.
+// Page-locked staging from a process-wide pool: hipHostMalloc of the ~80 MB a 1 M-triangle build
+// returns costs milliseconds per scene creation, so the buffers are kept and reused.
+void* pinned_pool_get(size_t bytes);
+void pinned_pool_put(void* p, size_t bytes);
+struct PooledPinned {
+    void* p = nullptr;
+    size_t bytes = 0;
+    PooledPinned() = default;
+    PooledPinned(const PooledPinned&) = delete;
+    PooledPinned& operator=(const PooledPinned&) = delete;
+    ~PooledPinned() { if (p) pinned_pool_put(p, bytes); }
+    bool get(size_t b) { if (p) pinned_pool_put(p, bytes); bytes = b; p = pinned_pool_get(b); return p != nullptr; }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+// The GPU median-split build's result: nodes in breadth-first order (children after their parent) as
+// 40-byte records {left, right, start, end, min xyz, max xyz} (the host's HNode layout), and the
+// primitive permutation.
 struct GpuBvh {
-    PinnedBuf<int> perm;
-    PinnedBuf<int4> nodes;
-    PinnedBuf<float> box;
+    PooledPinned perm;       // int[n]
+    PooledPinned nodes;      // 40 B per node
+    int num_nodes = 0;
     int root = -1;
 };
 int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, int n, GpuBvh& out, std::string& err,

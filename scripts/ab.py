@@ -20,8 +20,9 @@ for _ in range(int(os.environ.get("AB_FRAMES", "5"))):
     ms.append(r.stats()["render_ms"])
 r.render(0, collect_stats=1, **kw)
 ss = r.stats()
-r.render(0, collect_timing=1, streams=1, **kw)
-r.render(0, collect_timing=1, streams=1, **kw)
+kw1 = {k: v for k, v in kw.items() if k != "streams"}
+r.render(0, collect_timing=1, streams=1, **kw1)
+r.render(0, collect_timing=1, streams=1, **kw1)
 st = r.stats()
 print(json.dumps({"lib": os.environ.get("AB_TAG", os.environ.get("RTG_LIBRARY", "librtg")), "workload": w, "frame_ms": round(statistics.median(ms), 2),
                   "frames": [round(x, 2) for x in ms], "trace_ms": round(st["trace_ms"], 2),
