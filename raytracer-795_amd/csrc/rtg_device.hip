@@ -2646,19 +2646,24 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodeP
 }
 
 // Scene::SingleSample / MultiSample (src/Scene.cpp:365-411): color += sample_s in sample order.
-// A block takes 64 pixels: their samples' colours are staged through LDS with coalesced loads
-// (the slots of a pixel are adjacent; one lane per slot), then one lane per pixel sums them in
-// order.  mode 2: the single sample itself; 1: first chunk (start from 0); 0: continue the
-// running sum in `acc`.
-constexpr int kAccPix = 64, kAccChunk = 64, kAccStride = kAccChunk + 1;
+// A block takes PIX pixels: their samples' colours are staged through LDS with coalesced loads
+// (the slots of a pixel are adjacent; one lane per slot), CHUNK samples per pixel at a time, then one
+// lane per pixel sums them in order.  mode 2: the single sample itself; 1: first chunk (start from 0);
+// 0: continue the running sum in `acc`.  64 pixels x 64 samples where level 0 is resolved here (the
+// Whitted passes); 256 x 16 otherwise -- the path tracer's radiance and passes of few samples, which
+// left most of a 64-pixel block idle (round 5, `profiles/r6_ab_accumulate256.jsonl`: bunny 1 spp
+// 0.10 -> 0.04 ms, cornell_pt 2.30 -> 2.11 ms; with the resolve, dragon 1.45 -> 2.0 ms: not used there).
+constexpr int kAccPix = 64, kAccChunk = 64;
+constexpr int kAccPixWide = 256, kAccChunkWide = 16;
 // Colours are read from the level-0 NodePlanes colour plane; `resolve` (Whitted only) evaluates
 // non-final level-0 nodes against level 1 first.
 // DEEP (round 5): level 1 is resolved inline too (resolve_node2, against the resolved level 2).
-template <bool DEEP = false>
+template <bool DEEP = false, int PIX = kAccPix, int CHUNK = kAccChunk>
 __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv,
                                                     const NodePlanes level0, const NodePlanes level1, bool resolve,
                                                     float* __restrict__ acc, const PassDev ps, int nx, int mode,
                                                     const NodePlanes level2) {
+    constexpr int kAccPix = PIX, kAccChunk = CHUNK, kAccStride = CHUNK + 1;
     __shared__ float sr[kAccPix * kAccStride], sg[kAccPix * kAccStride], sb[kAccPix * kAccStride];
     const int p0 = blockIdx.x * kAccPix;
     const int np = min(kAccPix, ps.npass - p0);
@@ -2891,8 +2896,12 @@ void launch_resolve_planes(const SceneView& sv, const NodePlanes& self, const No
 void launch_accumulate_planes(const SceneView& sv, const NodePlanes& level0, const NodePlanes& level1, bool resolve,
                               float* acc, const PassDev& ps, int nx, int mode, hipStream_t st) {
     if (ps.npass <= 0) return;
-    hipLaunchKernelGGL(k_accumulate<false>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, level0, level1, resolve,
-                       acc, ps, nx, mode, NodePlanes{});
+    if (!resolve || ps.ns <= kAccChunkWide)
+        hipLaunchKernelGGL((k_accumulate<false, kAccPixWide, kAccChunkWide>), dim3(nblk(ps.npass, kAccPixWide)), dim3(256),
+                           0, st, sv, level0, level1, resolve, acc, ps, nx, mode, NodePlanes{});
+    else
+        hipLaunchKernelGGL(k_accumulate<false>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, level0, level1,
+                           resolve, acc, ps, nx, mode, NodePlanes{});
 }
 void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec* level1, bool resolve, float* acc,
                        const PassDev& ps, int nx, int mode, hipStream_t st, bool whitted, int n0, int n1,
@@ -2903,8 +2912,15 @@ void launch_accumulate(const SceneView& sv, const NodeRec* level0, const NodeRec
     const NodePlanes p1 = (whitted && level1) ? node_planes(const_cast<NodeRec*>(level1), n1) : NodePlanes{};
     if (whitted && resolve && level1 && level2) {
         const NodePlanes p2 = node_planes(const_cast<NodeRec*>(level2), n2);
-        hipLaunchKernelGGL(k_accumulate<true>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, p0, p1, true, acc, ps,
-                           nx, mode, p2);
+        if (ps.ns <= kAccChunkWide)
+            hipLaunchKernelGGL((k_accumulate<true, kAccPixWide, kAccChunkWide>), dim3(nblk(ps.npass, kAccPixWide)), dim3(256),
+                               0, st, sv, p0, p1, true, acc, ps, nx, mode, p2);
+        else
+            hipLaunchKernelGGL(k_accumulate<true>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, p0, p1, true, acc,
+                               ps, nx, mode, p2);
+    } else if (!(resolve && whitted) || ps.ns <= kAccChunkWide) {
+        hipLaunchKernelGGL((k_accumulate<false, kAccPixWide, kAccChunkWide>), dim3(nblk(ps.npass, kAccPixWide)), dim3(256),
+                           0, st, sv, p0, p1, resolve && whitted, acc, ps, nx, mode, NodePlanes{});
     } else {
         hipLaunchKernelGGL(k_accumulate<false>, dim3(nblk(ps.npass, kAccPix)), dim3(256), 0, st, sv, p0, p1,
                            resolve && whitted, acc, ps, nx, mode, NodePlanes{});
