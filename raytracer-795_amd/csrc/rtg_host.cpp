@@ -2453,8 +2453,9 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         return fail(RTG_ERR_INVALID, "tile_band / segment_pixels / segment_nodes");
     // Round 5 (`profiles/r6_ab_schedule_sweep.jsonl`, `r6_ab_tile_band8.jsonl`, same box, interleaved): bands
     // of 8 tiles for the reference integrator -- dragon 30.16-30.47 -> 29.91-30.10 ms over four pairs,
-    // cornell_dynamic 14.92-15.18 -> 14.85-15.12 ms; the path tracer (stream schedule) keeps 16.
-    int tile_s = o.tile_band > 0 ? std::min(o.tile_band, 1 << 12) : (pt ? 16 : 8);
+    // cornell_dynamic 14.92-15.18 -> 14.85-15.12 ms; the path tracer (stream schedule) and row shards
+    // keep 16 (`profiles/r6_shard_band.txt`: 1/8 dragon shard 5.39 ms with 8, 4.40 with 16).
+    int tile_s = o.tile_band > 0 ? std::min(o.tile_band, 1 << 12) : (pt || stride > 1 ? 16 : 8);
     // tile_pixel (device) forms band * (tile_h * tile_s * nx) in 32-bit ints: keep one band of the
     // widest tiles (tile_h <= 8) below 2^31 pixels
     if ((long long)8 * cam->nx >= (1LL << 31)) return fail(RTG_ERR_UNSUPPORTED, "image wider than 2^28 pixels");
