@@ -9,7 +9,9 @@ set -e
 TAG=$1
 WL=${2:-dragon1m}
 D=gpurun_out/prof_$TAG
-cp $D/bench.json profiles/${TAG}_bench.json
+# the bench line re-run with the counters just measured (gpu_profile_all.sh), else the first one
+B=$D/bench_final.json; [ -s $B ] || B=$D/bench.json
+cp $B profiles/${TAG}_bench.json
 python3 - "$D/kt/kt_kernel_stats.csv" > profiles/${TAG}_kernel_stats.txt <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
