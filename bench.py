@@ -97,7 +97,10 @@ def kernel_roof(counters: dict, name: str, avg_ms: float, launches: int) -> dict
 
 def frame_hbm_bytes(counters: dict, shade_name: str, shade_per_frame: int) -> float | None:
     """Measured HBM bytes of one whole frame: every kernel's per-dispatch bytes x its dispatches in
-    the profiled run, over the frames of that run (k_shade dispatches / k_shade launches per frame)."""
+    the profiled run, over the frames of that run (k_shade dispatches / k_shade launches per frame).
+    The profiled run also creates the scene (twice): its build kernels (rocprim sorts, rtg::anon::
+    kernels of rtg_bvh_gpu / rtg_sah_gpu; "rtg::" in counter files written before the names kept
+    the namespace) are not frame traffic."""
     ks = counters.get("kernels", {})
     sh = ks.get(shade_name)
     if not sh or "dispatches_WRITE_SIZE" not in sh or shade_per_frame <= 0:
@@ -106,6 +109,8 @@ def frame_hbm_bytes(counters: dict, shade_name: str, shade_per_frame: int) -> fl
     tot = 0.0
     for k, c in ks.items():
         if k.endswith("*>") or "hbm_bytes" not in c:       # combined entries double-count
+            continue
+        if k == "rtg::" or k.startswith(("rocprim::", "rtg::anon::")):
             continue
         tot += c["hbm_bytes"] * min(c["dispatches_FETCH_SIZE"], c["dispatches_WRITE_SIZE"])
     return tot / frames

@@ -1792,6 +1792,9 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                    const RayQ& next_rays, RayMeta* __restrict__ next_meta, unsigned long long* qcount,
                    unsigned char* __restrict__ lv_out) {
     const HitRec& h = hin.h;
+    // (the point store below; decided here for the whole wave -- a superset -- so that neither the
+    // origin nor a per-lane flag is live across the shading)
+    const bool o_far = __ballot(!(fabsf(o.x) < 1e17f && fabsf(o.y) < 1e17f && fabsf(o.z) < 1e17f)) != 0ull;
     int nchild = 0;
     QRay c0r, c1r;
     RayMeta c0m, c1m;
@@ -1911,11 +1914,14 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
                             const size_t k = (size_t)i * sv.num_lights + li;
                             if (sv.lean_shadow && !sv.has_blur) {
-                                // 12-byte planes: the origin, and the node colour if the light is
-                                // not blocked (ambient + contribution, the sum k_shadow would form)
+                                // the 12-byte origin plane only: the node stores its lit colour
+                                // (ambient + contribution) and its material, and k_shadow puts the
+                                // ambient term back if the light is blocked
                                 reinterpret_cast<float3*>(shadows.o)[k] = make_float3(sr.o.x, sr.o.y, sr.o.z);
-                                reinterpret_cast<float3*>(shadows.c)[k] =
-                                    make_float3(nd.cr + sr.c.x, nd.cg + sr.c.y, nd.cb + sr.c.z);
+                                if (sr.c.w != 0.0f) {
+                                    nd.cr = nd.cr + sr.c.x; nd.cg = nd.cg + sr.c.y; nd.cb = nd.cb + sr.c.z;
+                                    nd.kind |= nd.material << kNodeMatShift;
+                                }
                             } else {
                                 // the origin (+ time) is the node's, whatever the light: one record
                                 // per node, at the node's index; direction and light point only
@@ -1973,7 +1979,16 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
         const bool far = hit && !(fabsf(nd.px) < 1e18f && fabsf(nd.py) < 1e18f && fabsf(nd.pz) < 1e18f);
         nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb,
                                    __int_as_float(nd.kind | (hit ? kNodeHit : 0) | (far ? kNodeFar : 0)));
-        if (hit) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
+        // the point plane's readers: k_shadow (a node with a query: on the lean path, the material
+        // bits of its kind word), this node's own resolve (conductor / dielectric: F and, for Beer's
+        // law, p) and a dielectric parent's Beer's law on its refracted child -- read only when the
+        // parent's material absorbs (sv.pnt_all) or a point is far: the child's own (kNodeFar) or
+        // the parent's, whose refracted ray then starts far from the origin too (|o| >= 1e18 - eps;
+        // SceneView::pnt_all also covers eps >= 1e17)
+        const int nk = nd.kind & 0xFF;
+        if (hit && (!sv.lean_shadow || sv.has_blur || sv.pnt_all || (nd.kind >> kNodeMatShift) != 0 || far ||
+                    o_far || (nk != NK_FINAL && nk != NK_MIRROR)))
+            nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);
         if ((nd.kind & 0xFF) != NK_FINAL) nodes.link[i] = make_int4(nd.child0, nd.child1, nd.material, 0);
     }
     unsigned sb = (unsigned)(s_base >> 32) + s_ws[w];
@@ -2457,11 +2472,14 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         }
         was_blocked = blocked;
         if (lean3) {
-            // lit: the colour k_shade prepared (xyz only; w keeps the node's kind bits);
-            // blocked: col + 0 == col (the ambient term is never -0), nothing to store
-            if (!blocked) {
-                const float* cq = reinterpret_cast<const float*>(shadows.c) + 3 * (size_t)idx;
-                *reinterpret_cast<float3*>(nodes.col + i) = make_float3(ld(cq), ld(cq + 1), ld(cq + 2));
+            // lit: k_shade stored the lit colour; blocked: the ambient term alone, recomputed as
+            // k_shade formed it (Scene.cpp:22-30: 0 + La * ka) from the material in the kind word
+            // (the light's term is 0 and col + 0 == col: the ambient term is never -0)
+            if (blocked) {
+                const int mi = (int)((unsigned)__float_as_int(nodes.col[i].w) >> kNodeMatShift);
+                const MaterialDev& m = sv.materials[mi - 1];
+                const f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
+                *reinterpret_cast<float3*>(nodes.col + i) = make_float3(amb.x, amb.y, amb.z);
             }
         } else if (sv.num_lights == 1) {
             const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
@@ -2553,7 +2571,8 @@ DEV f3 resolve_with(const SceneView& sv, float4 nc, int i, const NodePlanes& sel
     f3 basic = mk(nc.x, nc.y, nc.z);
     if (kind == NK_FINAL) return basic;
     const int4 lk = self.link[i];
-    const float4 pf = self.pnt[i];
+    // a mirror node needs neither its point nor F (k_shade may not have stored them)
+    const float4 pf = kind == NK_MIRROR ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : self.pnt[i];
     const MaterialDev& m = sv.materials[lk.z - 1];
     f3 p = mk(pf.x, pf.y, pf.z);
     // Beer's law with zero absorption is exp(-0 * bd) = 1 for every finite distance bd, so the

@@ -2222,9 +2222,16 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         if (o.type == RTG_OBJ_TRIANGLE || (o.type == RTG_OBJ_MESH && (o.smooth || o.num_textures > 0))) sv.bary = 1;
     }
     sv.uni_walk = s->uni_walk;
-    sv.lean_shadow = d->num_lights == 1 &&
+    sv.lean_shadow = d->num_lights == 1 && d->num_materials < kNodeMatMax &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);
+    sv.pnt_all = !(d->shadow_ray_eps < 1e17f);
+    for (int i = 0; i < d->num_materials; i++) {
+        const rtg_material_desc& m = d->materials[i];
+        if (m.type == RTG_MAT_DIELECTRIC &&
+            !(m.absorption_coeff[0] == 0.0f && m.absorption_coeff[1] == 0.0f && m.absorption_coeff[2] == 0.0f))
+            sv.pnt_all = 1;
+    }
     pc.lap("view");
     // The host copies of the uploaded records (~300 MB for a 1 M-triangle mesh) are freed by the
     // library's reaper thread (Reaper, above): unmapping them took 18-25 ms of rtg_scene_create on the

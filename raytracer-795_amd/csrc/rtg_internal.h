@@ -187,6 +187,8 @@ struct SceneView {
                                    // depth is max_depth - level, slot and path are unused)
     int lean_shadow;               // one point / spot / directional light: a Whitted shadow query
                                    // stores only origin + contribution (k_shadow rebuilds d, tmax, L)
+    int pnt_all;                   // k_shade stores every hit point: a dielectric material absorbs
+                                   // (Beer's law reads refracted children's points) or eps >= 1e17
     int has_blur;                  // some object / instance has a nonzero motion-blur vector: the
                                    // ray queues carry times (RayQ::t)
     int bary;                      // some triangle is smooth-shaded or textured: the render path's
@@ -321,6 +323,12 @@ struct NodePlanes {
 };
 constexpr int kNodeHit = 0x400;
 constexpr int kNodeFar = 0x800;    // hit point with a coordinate >= 1e18 or not finite (k_resolve)
+// Lean single-light Whitted path (round 5): a node whose shadow query is traced stores its lit colour
+// (ambient + the light's term) and its material index in the kind word's bits 12..30; k_shadow
+// rewrites the colour to the ambient term only for a blocked query.  Scenes with more materials use
+// the general shadow path (SceneView::lean_shadow = 0).
+constexpr int kNodeMatShift = 12;
+constexpr int kNodeMatMax = 1 << 19;
 inline NodePlanes node_planes(NodeRec* base, long long n) {
     float4* b = reinterpret_cast<float4*>(base);
     return NodePlanes{b, b + n, reinterpret_cast<int4*>(b + 2 * n)};

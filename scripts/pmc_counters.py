@@ -19,7 +19,9 @@ import sys
 
 
 def kname(k):
-    k = k.split("(")[0].replace("void ", "")
+    # the scene-build and tone-map kernels live in anonymous namespaces (rtg::anon::k_*); the frame's
+    # kernels (rtg_device.hip) in rtg:: itself
+    k = k.replace("(anonymous namespace)::", "anon::").split("(")[0].replace("void ", "")
     return k
 
 

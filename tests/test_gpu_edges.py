@@ -1,7 +1,8 @@
 """Edge cases of the render path on the GPU, each against the oracle bit for bit: empty and
 light-less scenes, degenerate image sizes, MaxRecursionDepth 0, many lights (the in-order
-light sum of Scene::RecursiveShading, src/Scene.cpp:148-219), every primary ray missing, and
-empty / NaN ray batches for rtg_trace_closest (src/Helper.cpp:28-30 returns {} on NaN)."""
+light sum of Scene::RecursiveShading, src/Scene.cpp:148-219), every primary ray missing,
+glass far from the origin (Beer's law on overflowing distances), and empty / NaN ray batches
+for rtg_trace_closest (src/Helper.cpp:28-30 returns {} on NaN)."""
 import numpy as np
 import pytest
 
@@ -9,7 +10,7 @@ import pyoracle
 import rtg
 from rtg import _abi as A
 from rtg import scenegen
-from rtg.scene import Light, Scene
+from rtg.scene import Light, Material, Object, Scene
 
 pytestmark = pytest.mark.gpu
 
@@ -68,6 +69,28 @@ def test_all_primary_rays_miss(gpu):
     sc.cameras[0].up = np.float32([0, 0, 1])
     img = _same(sc)
     assert np.all(img == 0)
+
+
+@pytest.mark.parametrize("scale", [1.0, 3e17, 1e18, 1e19])
+@pytest.mark.parametrize("intensity", [0.0, 500.0])
+def test_far_glass_beer_distance(gpu, scale, intensity):
+    """A non-absorbing glass sphere in front of a diffuse one, the scene scaled so hit points reach
+    1e18-1e19: Beer's law (src/Scene.cpp:110) then sees |q0 - p| overflow (exp(-0 * inf) = NaN) or
+    not, so the refracted child's hit point must reach the bottom-up pass even where the child is
+    a final diffuse node without a shadow query (light intensity 0: no queries at all)."""
+    S = scale
+    sc = Scene(max_depth=3, background=(10, 20, 30), ambient=(20, 20, 20))
+    sc.cameras.append(scenegen._cam((0, 0, 0), (0, 0, -1), (0, 1, 0), 24, 16, fov_deg=50, spp=2))
+    sc.materials += [
+        Material(type=A.MAT_DIELECTRIC, ambient=(0, 0, 0), diffuse=(0, 0, 0), specular=(0, 0, 0),
+                 refraction_index=1.5, absorption_coeff=(0, 0, 0)),
+        Material(ambient=(1, 1, 1), diffuse=(0.6, 0.4, 0.3), specular=(0.2, 0.2, 0.2), phong_exp=8),
+    ]
+    v = scenegen._add_vertices(sc, [(0.2 * S, 0.0, -3.0 * S), (-0.3 * S, 0.1 * S, -6.0 * S)])
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=1, material=1, center=v, radius=1.0 * S))
+    sc.objects.append(Object(type=A.OBJ_SPHERE, id=2, material=2, center=v + 1, radius=1.5 * S))
+    sc.lights.append(Light(type=A.LIGHT_POINT, position=(0, 4 * S, -1 * S), intensity=(intensity,) * 3))
+    _same(sc)
 
 
 def test_trace_empty_and_nan_batches(gpu):
