@@ -1914,21 +1914,28 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
                             const size_t k = (size_t)i * sv.num_lights + li;
                             if (sv.lean_shadow && !sv.has_blur) {
-                                // the 12-byte origin plane only: the node stores its lit colour
-                                // (ambient + contribution) and its material, and k_shadow puts the
-                                // ambient term back if the light is blocked
+                                // the 12-byte origin plane only (lit node, below)
                                 reinterpret_cast<float3*>(shadows.o)[k] = make_float3(sr.o.x, sr.o.y, sr.o.z);
-                                if (sr.c.w != 0.0f) {
-                                    nd.cr = nd.cr + sr.c.x; nd.cg = nd.cg + sr.c.y; nd.cb = nd.cb + sr.c.z;
-                                    nd.kind |= nd.material << kNodeMatShift;
-                                }
                             } else {
                                 // the origin (+ time) is the node's, whatever the light: one record
                                 // per node, at the node's index; direction and light point only
-                                // for a traced query (k_light_sum reads every contribution)
+                                // for a traced query (k_light_sum reads every contribution; one
+                                // light: no contribution plane, the query's mode in L.w)
                                 if (li == 0) shadows.o[i] = sr.o;
-                                shadows.c[k] = sr.c;
-                                if (!sv.lean_shadow && sr.c.w != 0.0f) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
+                                if (!sv.lit_nodes) shadows.c[k] = sr.c;
+                                if (!sv.lean_shadow && sr.c.w != 0.0f) {
+                                    shadows.d[k] = sr.d;
+                                    shadows.L[k] = sv.lit_nodes ? make_float4(sr.L.x, sr.L.y, sr.L.z, sr.c.w) : sr.L;
+                                } else if (sv.lit_nodes && sr.c.w != 0.0f) {
+                                    reinterpret_cast<float*>(shadows.L + k)[3] = sr.c.w;   // lean, blurred
+                                }
+                            }
+                            // one light (SceneView::lit_nodes): the node stores its lit colour
+                            // (ambient + contribution) and its material, and k_shadow puts the
+                            // ambient term back if the light is blocked
+                            if (sv.lit_nodes && sr.c.w != 0.0f) {
+                                nd.cr = nd.cr + sr.c.x; nd.cg = nd.cg + sr.c.y; nd.cb = nd.cb + sr.c.z;
+                                nd.kind |= nd.material << kNodeMatShift;
                             }
                         }
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
@@ -2420,6 +2427,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
         // the query's mode is re-read rather than kept live across the traversal
         // (register pressure: 128 VGPRs for 4 waves per SIMD)
+        // (lit: the host points `c` at the L plane, whose w holds the mode)
         auto query_mode = [&]() {
             return lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f)
                          : ld(reinterpret_cast<const float*>(shadows.c + idx) + 3);
@@ -2471,23 +2479,29 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             blocked = h.obj >= 0;               // directional / environment: any hit
         }
         was_blocked = blocked;
+        // lit node (one light, Whitted: SceneView::lit_nodes; its kind word carries the material):
+        // k_shade stored the lit colour; blocked: the ambient term alone, recomputed as k_shade
+        // formed it (Scene.cpp:22-30: 0 + La * ka; the light's term is 0 and col + 0 == col: the
+        // ambient term is never -0).  The path tracer's single-light nodes add the contribution.
+        auto restore_ambient = [&](int mi) {
+            const MaterialDev& m = sv.materials[mi - 1];
+            const f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
+            *reinterpret_cast<float3*>(nodes.col + i) = make_float3(amb.x, amb.y, amb.z);
+        };
         if (lean3) {
-            // lit: k_shade stored the lit colour; blocked: the ambient term alone, recomputed as
-            // k_shade formed it (Scene.cpp:22-30: 0 + La * ka) from the material in the kind word
-            // (the light's term is 0 and col + 0 == col: the ambient term is never -0)
-            if (blocked) {
-                const int mi = (int)((unsigned)__float_as_int(nodes.col[i].w) >> kNodeMatShift);
-                const MaterialDev& m = sv.materials[mi - 1];
-                const f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
-                *reinterpret_cast<float3*>(nodes.col + i) = make_float3(amb.x, amb.y, amb.z);
-            }
+            if (blocked) restore_ambient((int)((unsigned)__float_as_int(nodes.col[i].w) >> kNodeMatShift));
         } else if (sv.num_lights == 1) {
-            const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
-            f3 add = blocked ? mk(0, 0, 0) : mk(ld(scp), ld(scp + 1), ld(scp + 2));
             float* cp = reinterpret_cast<float*>(nodes.col + i);
-            cp[0] = cp[0] + add.x;
-            cp[1] = cp[1] + add.y;
-            cp[2] = cp[2] + add.z;
+            const int mi = (int)((unsigned)__float_as_int(cp[3]) >> kNodeMatShift);
+            if (mi != 0) {
+                if (blocked) restore_ambient(mi);
+            } else {
+                const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
+                f3 add = blocked ? mk(0, 0, 0) : mk(ld(scp), ld(scp + 1), ld(scp + 2));
+                cp[0] = cp[0] + add.x;
+                cp[1] = cp[1] + add.y;
+                cp[2] = cp[2] + add.z;
+            }
         } else {
             // blocked: the query's mode (c.w) becomes 0, so the light sum reads one plane only
             if (blocked) reinterpret_cast<float*>(shadows.c + idx)[3] = 0.0f;
@@ -2846,8 +2860,10 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
     const NodePlanes np = node_planes(nodes, n);
-    const ShadowPlanes sp = shadow_planes(shadows, cap);
+    ShadowPlanes sp = shadow_planes(shadows, cap);
     const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
+    const bool lit = whitted && sv.lit_nodes;     // (lean implies lit)
+    if (lit) sp.c = sp.L;                         // no contribution plane: the mode is L.w
     const bool tl = sv.tlas_root >= 0;
     if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
     else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);

@@ -2225,6 +2225,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     sv.lean_shadow = d->num_lights == 1 && d->num_materials < kNodeMatMax &&
                      (d->lights[0].type == RTG_LIGHT_POINT || d->lights[0].type == RTG_LIGHT_SPOT ||
                       d->lights[0].type == RTG_LIGHT_DIRECTIONAL);
+    sv.lit_nodes = d->num_lights == 1 && d->num_materials < kNodeMatMax;
     sv.pnt_all = !(d->shadow_ray_eps < 1e17f);
     for (int i = 0; i < d->num_materials; i++) {
         const rtg_material_desc& m = d->materials[i];

@@ -187,6 +187,8 @@ struct SceneView {
                                    // depth is max_depth - level, slot and path are unused)
     int lean_shadow;               // one point / spot / directional light: a Whitted shadow query
                                    // stores only origin + contribution (k_shadow rebuilds d, tmax, L)
+    int lit_nodes;                 // one light, < kNodeMatMax materials: Whitted nodes store their lit
+                                   // colour and k_shadow restores the ambient term if blocked
     int pnt_all;                   // k_shade stores every hit point: a dielectric material absorbs
                                    // (Beer's law reads refracted children's points) or eps >= 1e17
     int has_blur;                  // some object / instance has a nonzero motion-blur vector: the
@@ -323,10 +325,10 @@ struct NodePlanes {
 };
 constexpr int kNodeHit = 0x400;
 constexpr int kNodeFar = 0x800;    // hit point with a coordinate >= 1e18 or not finite (k_resolve)
-// Lean single-light Whitted path (round 5): a node whose shadow query is traced stores its lit colour
-// (ambient + the light's term) and its material index in the kind word's bits 12..30; k_shadow
-// rewrites the colour to the ambient term only for a blocked query.  Scenes with more materials use
-// the general shadow path (SceneView::lean_shadow = 0).
+// Single-light Whitted path (round 5, SceneView::lit_nodes): a node whose shadow query is traced
+// stores its lit colour (ambient + the light's term) and its material index in the kind word's bits
+// 12..30; k_shadow rewrites the colour to the ambient term only for a blocked query.  Scenes with more
+// materials keep the contribution plane (lit_nodes = lean_shadow = 0).
 constexpr int kNodeMatShift = 12;
 constexpr int kNodeMatMax = 1 << 19;
 inline NodePlanes node_planes(NodeRec* base, long long n) {
