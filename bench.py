@@ -95,25 +95,49 @@ def kernel_roof(counters: dict, name: str, avg_ms: float, launches: int) -> dict
     return out
 
 
+def _targs(k: str) -> list:
+    return [a.strip() for a in k[k.index("<") + 1:k.rindex(">")].split(",")] if "<" in k else []
+
+
 def frame_hbm_bytes(counters: dict, shade_name: str, shade_per_frame: int) -> float | None:
-    """Measured HBM bytes of one whole frame: every kernel's per-dispatch bytes x its dispatches in
+    """Measured HBM bytes of one rendered frame: every kernel's per-dispatch bytes x its dispatches in
     the profiled run, over the frames of that run (k_shade dispatches / k_shade launches per frame).
     The profiled run also creates the scene (twice): its build kernels (rocprim sorts, rtg::anon::
     kernels of rtg_bvh_gpu / rtg_sah_gpu; "rtg::" in counter files written before the names kept
-    the namespace) are not frame traffic."""
+    the namespace) are not frame traffic.  One of its frames is the collect_stats frame (the lane
+    efficiencies): its traversal kernels are the STATS instantiations (second template argument
+    true), which also write counters; they are left out and the plain traversal kernels divided by
+    the other frames (the stats frames counted from the camera-ray launches, GEN = true)."""
     ks = counters.get("kernels", {})
     sh = ks.get(shade_name)
     if not sh or "dispatches_WRITE_SIZE" not in sh or shade_per_frame <= 0:
         return None
     frames = sh["dispatches_WRITE_SIZE"] / shade_per_frame
+
+    def n_of(c):
+        return min(c["dispatches_FETCH_SIZE"], c["dispatches_WRITE_SIZE"])
+
+    def walk(k):
+        return k.startswith(("rtg::k_trace<", "rtg::k_shadow<"))
+    gen = {False: 0.0, True: 0.0}
+    for k, c in ks.items():
+        a = _targs(k)
+        if k.startswith("rtg::k_trace<") and len(a) >= 3 and a[2] == "true" and "dispatches_WRITE_SIZE" in c:
+            gen[a[1] == "true"] += n_of(c)
+    stats_frames = frames * gen[True] / (gen[True] + gen[False]) if gen[True] > 0 and gen[False] > 0 else 0.0
     tot = 0.0
     for k, c in ks.items():
         if k.endswith("*>") or "hbm_bytes" not in c:       # combined entries double-count
             continue
         if k == "rtg::" or k.startswith(("rocprim::", "rtg::anon::")):
             continue
-        tot += c["hbm_bytes"] * min(c["dispatches_FETCH_SIZE"], c["dispatches_WRITE_SIZE"])
-    return tot / frames
+        if walk(k):
+            if _targs(k)[1:2] == ["true"]:
+                continue
+            tot += c["hbm_bytes"] * n_of(c) / (frames - stats_frames)
+        else:
+            tot += c["hbm_bytes"] * n_of(c) / frames
+    return tot
 
 
 def cpu_baseline(scene, rows: int, threads: int):
