@@ -93,6 +93,30 @@ def test_far_glass_beer_distance(gpu, scale, intensity):
     _same(sc)
 
 
+@pytest.mark.parametrize("kind", ["point", "directional", "spot", "area"])
+@pytest.mark.parametrize("blur", [False, True])
+def test_single_light_shadow_records(gpu, kind, blur):
+    """One light of each kind, with and without motion blur: the lit-node shadow records (k_shade
+    stores the lit colour, k_shadow restores the ambient term of a blocked query; the lean origin-only
+    records, and the blurred lean records whose mode travels in L.w) against the oracle, with a mirror
+    (a second level) and shadows cast on the floor by the spheres."""
+    sc = scenegen.simple(40, 30)
+    sc.cameras[0].num_samples = 4
+    sc.max_depth = 2
+    sc.materials[1].type = A.MAT_MIRROR
+    sc.materials[1].mirror = (0.6, 0.6, 0.6)
+    if blur:
+        sc.objects[0].blur = (0.0, 0.25, 0.0)
+    L = {"point": Light(type=A.LIGHT_POINT, position=(0.3, 3.0, -1.0), intensity=(900, 800, 700)),
+         "directional": Light(type=A.LIGHT_DIRECTIONAL, direction=(0.2, -1.0, -0.3), intensity=(0.9, 0.8, 0.7)),
+         "spot": Light(type=A.LIGHT_SPOT, position=(0.0, 3.0, -1.5), direction=(0.0, -1.0, -0.1),
+                       intensity=(900, 800, 700), coverage_deg=35, falloff_deg=20),
+         "area": Light(type=A.LIGHT_AREA, position=(0.0, 3.0, -1.5), direction=(0.0, -1.0, 0.0),
+                       intensity=(900, 800, 700), size=1.5)}[kind]
+    sc.lights = [L]
+    _same(sc)
+
+
 def test_trace_empty_and_nan_batches(gpu):
     sc = scenegen.simple(8, 8)
     with rtg.Renderer(sc, device=0) as r:
