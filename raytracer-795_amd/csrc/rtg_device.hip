@@ -2682,11 +2682,13 @@ __global__ void __launch_bounds__(256) k_resolve(const SceneView sv, const NodeP
 // A block takes PIX pixels: their samples' colours are staged through LDS with coalesced loads
 // (the slots of a pixel are adjacent; one lane per slot), CHUNK samples per pixel at a time, then one
 // lane per pixel sums them in order.  mode 2: the single sample itself; 1: first chunk (start from 0);
-// 0: continue the running sum in `acc`.  64 pixels x 64 samples where level 0 is resolved here (the
-// Whitted passes); 256 x 16 otherwise -- the path tracer's radiance and passes of few samples, which
-// left most of a 64-pixel block idle (round 5, `profiles/r6_ab_accumulate256.jsonl`: bunny 1 spp
-// 0.10 -> 0.04 ms, cornell_pt 2.30 -> 2.11 ms; with the resolve, dragon 1.45 -> 2.0 ms: not used there).
-constexpr int kAccPix = 64, kAccChunk = 64;
+// 0: continue the running sum in `acc`.  32 pixels x 64 samples where level 0 is resolved here (the
+// Whitted passes: 25 KB of LDS instead of 50, twice the blocks per CU for the resolve's dependent
+// gathers -- round 5, `profiles/r6_ab_accumulate_pix32.jsonl`: dragon 1.38 -> 1.09 ms per frame, spheres
+// 1.52 -> 1.08; 16 pixels no better); 256 x 16 otherwise -- the path tracer's radiance and passes of
+// few samples (`r6_ab_accumulate256.jsonl`: bunny 1 spp 0.10 -> 0.04 ms, cornell_pt 2.30 -> 2.11 ms;
+// with the resolve, dragon 1.45 -> 2.0 ms: not used there).
+constexpr int kAccPix = 32, kAccChunk = 64;
 constexpr int kAccPixWide = 256, kAccChunkWide = 16;
 // Colours are read from the level-0 NodePlanes colour plane; `resolve` (Whitted only) evaluates
 // non-final level-0 nodes against level 1 first.
