@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 8
+#define RTG_ABI_VERSION 9
 
 typedef enum rtg_status {
     RTG_OK = 0,
@@ -332,6 +332,18 @@ typedef struct rtg_render_stats {
        (ray, hit record), next-event estimation (light samples + BRDF), continuation sampling,
        compaction + record stores */
     uint64_t pt_shade_cycles[4];
+    /* ABI 9, collect_stats: the flat group (untransformed small meshes tested together):
+       the (lane, triangle) tests its lanes ran -- every member triangle's fast rejection, then each lane's
+       own candidates' exact tests -- and 64 x the tests each wave ran (the most any of its lanes needed).
+       (steps + entry_visits + group_work) / (lane_slots + entry_slots + group_slots) is the SIMD
+       efficiency with the group's per-lane work counted.  group_cycles: the group's wave cycles split
+       into set-up (ray transform, reciprocals, window) and tests (slot 15 of entry_cycles holds both). */
+    uint64_t trace_group_work;
+    uint64_t trace_group_slots;
+    uint64_t shadow_group_work;
+    uint64_t shadow_group_slots;
+    uint64_t trace_group_cycles[2];
+    uint64_t shadow_group_cycles[2];
 } rtg_render_stats;
 
 typedef struct rtg_ray {             /* src/Ray.h:10-12 */
@@ -442,7 +454,10 @@ int32_t rtg_comm_init_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, 
 /* ABI 8: the same with a bound on every wait of the rank (communicator set-up, the failure agreement
    and the gather of rtg_render_ranked): a rank whose peers do not join within timeout_ms aborts the
    communicator (ncclCommAbort) and returns RTG_ERR_HIP instead of blocking; the communicator is then
-   unusable (destroy it).  timeout_ms <= 0: 120000.  rtg_comm_init_rank uses the default. */
+   unusable (destroy it).  The agreement / gather deadline counts from this rank's own shard end, so it
+   must also cover the peers' remaining render time (shard skew).  timeout_ms <= 0: no deadline, which is
+   what rtg_comm_init_rank does (round 6, ADVICE r5: a long, imbalanced render must not abort a healthy
+   rank). */
 int32_t rtg_comm_init_rank_timeout(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
                                    int32_t timeout_ms, rtg_comm** out);
 int32_t rtg_comm_destroy(rtg_comm* comm);

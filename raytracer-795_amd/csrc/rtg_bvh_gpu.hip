@@ -477,12 +477,17 @@ int gpu_build_bvh(const float* centers, const float* bmin, const float* bmax, in
     return 0;
 }
 
-// Process-wide pool of page-locked staging buffers (first fit, kept for the process's lifetime).
+// Process-wide pool of page-locked staging buffers (best fit).  Each buffer keeps its real capacity
+// (a reused larger buffer is returned at that capacity, not at the size last asked of it), and the
+// pool holds at most kPoolBytes: buffers beyond that are freed (a long-lived process
+// creating scenes of varying size must not grow its page-locked memory without bound).
 namespace {
 std::mutex g_pool_mu;
-std::vector<std::pair<void*, size_t>> g_pool;
+std::vector<std::pair<void*, size_t>> g_pool;     // (buffer, capacity)
+size_t g_pool_bytes = 0;
+constexpr size_t kPoolBytes = size_t(1) << 30;
 }
-void* pinned_pool_get(size_t bytes) {
+void* pinned_pool_get(size_t bytes, size_t* cap) {
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
         size_t best = g_pool.size();
@@ -490,18 +495,36 @@ void* pinned_pool_get(size_t bytes) {
             if (g_pool[k].second >= bytes && (best == g_pool.size() || g_pool[k].second < g_pool[best].second)) best = k;
         if (best < g_pool.size()) {
             void* p = g_pool[best].first;
+            *cap = g_pool[best].second;
+            g_pool_bytes -= g_pool[best].second;
             g_pool.erase(g_pool.begin() + best);
             return p;
         }
     }
     void* p = nullptr;
-    if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return nullptr;
+    const size_t want = std::max<size_t>(bytes, 1);
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    *cap = want;
     return p;
 }
-void pinned_pool_put(void* p, size_t bytes) {
+void pinned_pool_put(void* p, size_t cap) {
     if (!p) return;
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.emplace_back(p, bytes);
+    std::vector<void*> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        g_pool.emplace_back(p, cap);
+        g_pool_bytes += cap;
+        // over the cap: free the smallest buffers first (the large ones are the expensive ones to remake)
+        while (g_pool_bytes > kPoolBytes && !g_pool.empty()) {
+            size_t k = 0;
+            for (size_t j = 1; j < g_pool.size(); j++)
+                if (g_pool[j].second < g_pool[k].second) k = j;
+            g_pool_bytes -= g_pool[k].second;
+            drop.push_back(g_pool[k].first);
+            g_pool.erase(g_pool.begin() + k);
+        }
+    }
+    for (void* q : drop) (void)hipHostFree(q);
 }
 
 }  // namespace rtg

@@ -359,7 +359,9 @@ DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d
 // considered: entries the lane's loop went through (the wave runs each for all its lanes)
 // cand_step: node steps taken when the current object's best candidate was accepted; win_step: the
 // same for the query's final winner (the steps after it only prove that it is the nearest)
-struct Stats { unsigned nodes, tris, steps, entries, considered, cand_step, win_step; };
+// gwork: the flat group's triangle tests this lane ran (fast rejections + its own exact tests); gslot:
+// the group triangle tests its wave ran while the lane was in the group (the wave runs the max)
+struct Stats { unsigned nodes, tris, steps, entries, considered, cand_step, win_step, gwork, gslot; };
 
 // ------------------------------------------------------------------ closest hit
 // BVHMethods::FindIntersection (src/Helper.cpp:18-80) with the per-object nearest
@@ -782,12 +784,23 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
 // the winner iff t < nearest, or t == nearest and it comes earlier in the loop order.
 // Returns false (nothing done) for a ray whose object-space direction is not fast: its lane visits the
 // group's entries in the object loop.
-DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float time, float& nearest, HitRec& out) {
+// STATS: lane work / slots in st.gwork / st.gslot; wave cycles of the set-up (transform, reciprocals,
+// window: up to the first triangle) and of the tests charged to ecyc[16] / ecyc[17].
+template <bool STATS = false>
+DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float time, float& nearest, HitRec& out,
+                    Stats& st, unsigned long long* ecyc) {
+    const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
+    auto charge = [&](int slot, unsigned long long t0) {
+        if (STATS && ecyc && (__ballot(1) & __lanemask_lt()) == 0ull)
+            atomicAdd(ecyc + slot, __builtin_amdgcn_s_memtime() - t0);
+    };
     f3 o2, d2;
     transform_ray(sv.tops[sv.gents[0].entry], o, d, time, o2, d2, true);   // the members' common transform
     const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
-    if (!(adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f))
+    if (!(adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f)) {
+        charge(16, c0);
         return false;
+    }
     const float eps = sv.int_eps;
     const f3 inv = mk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y), __builtin_amdgcn_rcpf(d2.z));
     const float da = d2.x != 0.0f ? d2.x : (d2.y != 0.0f ? d2.y : d2.z);
@@ -804,6 +817,8 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
     };
     const float thi1 = window();
     const float tlo = -(fabsf(eps) + 1e-6f);
+    charge(16, c0);
+    const unsigned long long c1 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned cand = 0;
     for (int e = 0; e < sv.num_gents; e++) {
         const GroupEnt& G = sv.gents[e];
@@ -812,6 +827,7 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
         const bool need = !G.win || window_meets(o2, inv, G.win_min[0], G.win_min[1], G.win_min[2], G.win_max[0],
                                                  G.win_max[1], G.win_max[2], tlo, thi1);
         if (__ballot(need) == 0ull) continue;
+        if (STATS) { st.gslot += G.count; st.gwork += need ? G.count : 0; }
         for (int j = G.first; j < G.first + G.count; j++)
             if (need && tri_maybe(sv.gtris[j], o2, d2, eps, thi1)) cand |= 1u << j;
     }
@@ -819,6 +835,12 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
         const GroupEnt& G = sv.gents[e];
         unsigned m = (cand >> G.first) & ((1u << G.count) - 1u);
         if (__ballot(m != 0u) == 0ull) continue;
+        if (STATS) {        // the exact tests: each lane its own candidates, the wave the most any lane has
+            unsigned k = __popc(m), wm = k;
+            for (int off = 32; off > 0; off >>= 1) wm = max(wm, (unsigned)__shfl_xor((int)wm, off));
+            st.gslot += wm;
+            st.gwork += k;
+        }
         if (m == 0u) continue;
         if (G.root_box && !box_hit(o2, d2, inv, true, G.root_min[0], G.root_min[1], G.root_min[2], G.root_max[0],
                                    G.root_max[1], G.root_max[2]))
@@ -855,6 +877,7 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
             }
         }
     }
+    charge(17, c1);
     return true;
 }
 
@@ -885,7 +908,7 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
         bool grouped = false;
         if (!EXHAUSTIVE && sv.num_gents > 0 && __ballot(fin) != 0ull) {
             const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
-            if (fin) grouped = flat_group(sv, o, d, time, nearest, out);
+            if (fin) grouped = flat_group<STATS>(sv, o, d, time, nearest, out, st, ecyc);
             if (STATS && ecyc && (__ballot(1) & __lanemask_lt()) == 0ull)
                 atomicAdd(ecyc + 15, __builtin_amdgcn_s_memtime() - c0);
         }
@@ -1367,22 +1390,22 @@ DEV f3 toward(f3 lpos, f3 p) {
     f3 dv = lpos - p;
     return dv / norm(dv);
 }
-DEV float shadow_tmax(f3 origin, f3 p, f3 lp, float eps) {
+// The query's t bound from dl = |p - L| (light_sample stores dl; k_shadow rebuilds the bound).
+DEV float shadow_tmax_dl(f3 origin, float dl, float eps) {
     // hits with gett() beyond |p-L| + eps can never satisfy the blocking test
-    float dl = norm(p - lp);
     float oabs = fmaxf(fmaxf(fabsf(origin.x), fabsf(origin.y)), fabsf(origin.z));
     float tmax = (dl + eps) * (1.0f + 1e-4f) + 1e-5f * oabs + 1e-30f;
     if (!(tmax == tmax)) tmax = FLT_MAX;
     return tmax;
 }
+DEV float shadow_tmax(f3 origin, f3 p, f3 lp, float eps) { return shadow_tmax_dl(origin, norm(p - lp), eps); }
 // Object-light (NEE) query bound: k_shadow blocks iff |p - hp| < lim = dl - (eps + 1e-4 dl)
 // (Page7.md:143-147 as the oracle states it), hp = o + d t, o = p + w (w = the normal offset).
 // With |d| = 1, |p - hp|^2 = t^2 + 2t (d.w) + |w|^2, so every hit with t >= tcut = -(d.w) +
 // sqrt((d.w)^2 - |w|^2 + lim^2) leaves the query unblocked.  The light's own surface, at
 // t ~ dl - (d.w), lies eps + 1e-4 dl beyond tcut, so the query no longer walks to it.  Margins:
 // 1e-5 relative and 1e-5 |o| absolute, far above the rounding of k_shadow's test.
-DEV float emit_shadow_tmax(f3 origin, f3 p, f3 lp, f3 d, float eps) {
-    const float dl = norm(p - lp);
+DEV float emit_shadow_tmax(f3 origin, f3 p, float dl, f3 d, float eps) {
     const float lim = dl - (eps + 1e-4f * dl);
     const f3 w = origin - p;
     const float dw = dot(d, w);
@@ -1407,7 +1430,7 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     f3 origin = ret.point + ret.normal * sv.shadow_eps;
     f3 c = mk(0, 0, 0);
     f3 dir = mk(0, 0, 0), lp = mk(0, 0, 0);
-    float mode = 0.0f, tmax = FLT_MAX;
+    float mode = 0.0f;
     // every case leaves the light colour and direction of its single BRDF call here; the call
     // follows the switch (one inlined copy of the BRDF code instead of one per light type)
     f3 LCs = mk(0, 0, 0), wis = mk(0, 0, 0);
@@ -1559,12 +1582,29 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
     // both leave the running sum bit-identical.  -0 / NaN channels keep the query.
     if ((mode == 1.0f || mode == 2.0f) && (__float_as_uint(c.x) | __float_as_uint(c.y) | __float_as_uint(c.z)) == 0u)
         mode = 0.0f;
-    if (mode == 1.0f || mode == 3.0f) tmax = shadow_tmax(origin, ret.point, lp, sv.shadow_eps);
-    if (mode == 3.0f) tmax = fminf(tmax, emit_shadow_tmax(origin, ret.point, lp, dir, sv.shadow_eps));
+    // distance tests (modes 1 / 3): only |p - L| is needed, by k_shadow's t bound (shadow_query_tmax)
+    // and its blocking test; directional / environment queries have no light point
+    const float dl = (mode == 1.0f || mode == 3.0f) ? norm(ret.point - lp) : 0.0f;
     sr.o = make_float4(origin.x, origin.y, origin.z, time);
-    sr.d = make_float4(dir.x, dir.y, dir.z, tmax);
+    sr.d = make_float4(dir.x, dir.y, dir.z, dl);
     sr.c = make_float4(c.x, c.y, c.z, mode);
-    sr.L = make_float4(lp.x, lp.y, lp.z, 0.0f);
+}
+
+// The traced mode of a query to light li (a query is listed only when light_sample left a nonzero
+// mode, which depends on the light type alone): 2 = any hit blocks (directional, environment),
+// 3 = object light (hw7), else 1 = distance test against the light point.
+DEV float shadow_mode(const SceneView& sv, int li) {
+    const int t = sv.lights[li].type;
+    return (t == RTG_LIGHT_DIRECTIONAL || t == RTG_LIGHT_ENVIRONMENT) ? 2.0f
+         : (t == kLightEmitMesh || t == kLightEmitSphere) ? 3.0f : 1.0f;
+}
+// k_shadow's t bound of a traced query (what light_sample formed before round 6, bit for bit):
+// p = the node's hit point (mode 3 only), dl from the direction plane's w.
+DEV float shadow_query_tmax(float mode, f3 origin, f3 p, f3 d, float dl, float eps) {
+    if (mode == 2.0f) return FLT_MAX;
+    float tmax = shadow_tmax_dl(origin, dl, eps);
+    if (mode == 3.0f) tmax = fminf(tmax, emit_shadow_tmax(origin, p, dl, d, eps));
+    return tmax;
 }
 
 // ------------------------------------------------------------------ camera / background
@@ -1702,11 +1742,11 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
                                                        bool compact, int nq, int gbase) {
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
-    __shared__ unsigned long long s_ecyc[STATS ? 16 : 1];
-    if (STATS && threadIdx.x < 16) s_ecyc[threadIdx.x] = 0ull;
+    __shared__ unsigned long long s_ecyc[STATS ? 18 : 1];   // entries 0..15, group set-up / tests
+    if (STATS && threadIdx.x < 18) s_ecyc[threadIdx.x] = 0ull;
     if (STATS) __syncthreads();
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Stats st = {0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (i < n) {
         f3 o, d;
         float time, tmax;
@@ -1730,19 +1770,25 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_TRACE_ATTR k_trace(const Scen
         }
     }
     if (STATS) {
-        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries;
-        unsigned mx = st.steps, mc = st.considered;
+        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries, gw = st.gwork;
+        unsigned mx = st.steps, mc = st.considered, mg = st.gslot;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
             ns += __shfl_down(ns, off);
             ne += __shfl_down(ne, off);
+            gw += __shfl_down(gw, off);
             mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
             mc = max(mc, (unsigned)__shfl_xor((int)mc, off));
+            mg = max(mg, (unsigned)__shfl_xor((int)mg, off));
         }
         __syncthreads();
         if (threadIdx.x < 16 && s_ecyc[threadIdx.x]) atomicAdd(&ctr->trace_entry_cycles[threadIdx.x], s_ecyc[threadIdx.x]);
+        if (threadIdx.x >= 16 && threadIdx.x < 18 && s_ecyc[threadIdx.x])
+            atomicAdd(&ctr->trace_group_cycles[threadIdx.x - 16], s_ecyc[threadIdx.x]);
         if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&ctr->trace_group_work, gw);
+            atomicAdd(&ctr->trace_group_slots, 64ull * mg);
             atomicAdd(&ctr->node_visits, nv);
             atomicAdd(&ctr->tri_tests, nt);
             atomicAdd(&ctr->trace_lane_slots, 64ull * mx);
@@ -1912,23 +1958,18 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
                         // one light: a query that is not traced is never read (k_light_sum reads
                         // every record when there are several)
                         if (sr.c.w != 0.0f || sv.num_lights > 1) {
-                            const size_t k = (size_t)i * sv.num_lights + li;
+                            const size_t k = (size_t)li * shadows.nn + i;     // light-major (ShadowPlanes)
                             if (sv.lean_shadow && !sv.has_blur) {
                                 // the 12-byte origin plane only (lit node, below)
-                                reinterpret_cast<float3*>(shadows.o)[k] = make_float3(sr.o.x, sr.o.y, sr.o.z);
+                                reinterpret_cast<float3*>(shadows.o)[i] = make_float3(sr.o.x, sr.o.y, sr.o.z);
                             } else {
                                 // the origin (+ time) is the node's, whatever the light: one record
-                                // per node, at the node's index; direction and light point only
+                                // per node, at the node's index; the direction (+ light distance) only
                                 // for a traced query (k_light_sum reads every contribution; one
-                                // light: no contribution plane, the query's mode in L.w)
+                                // light: no contribution plane, k_shadow knows the mode from the light)
                                 if (li == 0) shadows.o[i] = sr.o;
                                 if (!sv.lit_nodes) shadows.c[k] = sr.c;
-                                if (!sv.lean_shadow && sr.c.w != 0.0f) {
-                                    shadows.d[k] = sr.d;
-                                    shadows.L[k] = sv.lit_nodes ? make_float4(sr.L.x, sr.L.y, sr.L.z, sr.c.w) : sr.L;
-                                } else if (sv.lit_nodes && sr.c.w != 0.0f) {
-                                    reinterpret_cast<float*>(shadows.L + k)[3] = sr.c.w;   // lean, blurred
-                                }
+                                if (!sv.lean_shadow && sr.c.w != 0.0f) shadows.d[k] = sr.d;
                             }
                             // one light (SceneView::lit_nodes): the node stores its lit colour
                             // (ambient + contribution) and its material, and k_shadow puts the
@@ -2002,7 +2043,7 @@ DEV void shade_ray(const SceneView& sv, const CameraDev& cam, int level, const P
     for (int li = 0; li < sv.num_lights; li++) {
         const bool need = (smask >> li) & 1ull;
         const unsigned long long m = __ballot(need);
-        if (need) slist[sb + __popcll(m & lt)] = i * sv.num_lights + li;
+        if (need) slist[sb + __popcll(m & lt)] = li * shadows.nn + i;
         sb += __popcll(m);
     }
 }
@@ -2066,10 +2107,10 @@ __global__ void __launch_bounds__(BLOCK) RTG_SHADE_ATTR k_shade(const SceneView 
 
 // ------------------------------------------------------------------ hw7 path tracer
 // One shading step of oracle/rtg_oracle.c pt_sample() per ray (no reference code exists:
-// pages/Page7.md describes the integrator in prose; DESIGN.md §8 fixes it).  Writes the
-// vertex contribution v into nodes[i] (k_shadow / k_light_sum add the lights, k_pt_gather
-// adds T (x) v to the sample's radiance), the Beer-attenuated throughput and the sample slot into
-// the node's link plane (the only reader is k_pt_gather), and at most one continuation ray.
+// pages/Page7.md describes the integrator in prose; DESIGN.md §8 fixes it).  Adds the vertex's
+// T (x) v to the sample's running radiance (PtRad) when no shadow query is pending, else leaves the
+// node record (colour, point + last light, throughput + radiance target) for k_shadow, and queues
+// at most one continuation ray.
 struct DielSplit {
     bool entering, tir;
     float F;
@@ -2114,7 +2155,7 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                                                   const RayQ next_rays, RayMeta* __restrict__ next_meta,
                                                   PathRec* __restrict__ next_paths, unsigned long long* qcount, int n,
                                                   int nq, int gbase, const unsigned char* __restrict__ lv_in,
-                                                  unsigned char* __restrict__ lv_out, Counters* ctr) {
+                                                  unsigned char* __restrict__ lv_out, const PtRad pr, Counters* ctr) {
     constexpr int BLOCK = kPtBlock;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     // collect_stats (ctr): wave cycles by phase (Counters::pt_shade_cycles), charged by each wave's
@@ -2131,7 +2172,8 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
     RayMeta cm;
     PathRec cp;
     NodeRec nd;
-    f3 Tg = mk(0, 0, 0);            // the vertex's Beer-attenuated throughput (k_pt_gather)
+    f3 Tg = mk(0, 0, 0);            // the vertex's Beer-attenuated throughput
+    f3 Lrun = mk(0, 0, 0);          // the sample's radiance before this vertex (a new sample: 0)
     unsigned long long smask = 0;
     int level = 0;
     if (i < n) {
@@ -2162,10 +2204,12 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
         f3 T = mk(1, 1, 1);
         int spec = 1, medium = 0;
         if (!gen && level > 0) {
-            const PathRec pr = paths[i];
-            T = mk(pr.tr, pr.tg, pr.tb);
-            spec = pr.flags & 1;
-            medium = pr.flags >> 8;
+            const PathRec ph = paths[i];
+            T = mk(ph.tr, ph.tg, ph.tb);
+            spec = ph.flags & 1;
+            medium = ph.flags >> 8;
+            const float4 z = pr.carry_in[i];        // the sample's radiance so far (PtRad)
+            Lrun = mk(z.x, z.y, z.z);
         }
         nd.px = nd.py = nd.pz = 0.0f;
         nd.cr = nd.cg = nd.cb = 0.0f;
@@ -2228,10 +2272,10 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                     for (int li = 0; li < sv.num_lights; li++) {
                         ShadowRec sr;
                         light_sample<FULL, SPOT, BRDF>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
-                        const size_t k = (size_t)i * sv.num_lights + li;
+                        const size_t k = (size_t)li * shadows.nn + i;   // light-major (ShadowPlanes)
                         if (li == 0) shadows.o[i] = sr.o;       // per node (k_shade's layout)
                         shadows.c[k] = sr.c;
-                        if (sr.c.w != 0.0f) { shadows.d[k] = sr.d; shadows.L[k] = sr.L; }
+                        if (sr.c.w != 0.0f) shadows.d[k] = sr.d;
                         if (sr.c.w != 0.0f) smask |= 1ull << li;
                         else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
                     }
@@ -2289,23 +2333,42 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
         Tg = T;
     }
     const unsigned long long t_store = ctr ? __builtin_amdgcn_s_memtime() : 0ull;
-    // compaction: one continuation per lane, shadow list light-major per wave (as k_shade)
-    __shared__ unsigned s_wc[BLOCK / 64], s_ws[BLOCK / 64];
+    // compaction: one continuation per lane (one 64-bit atomic per block: continuations | shadow
+    // queries << 32, the host's counts), and per light one list (slist + li * n, counted in
+    // pr.lcnt[li]: k_shadow runs the lights' lists one launch after the other, in light order).  Wave
+    // counts in LDS, then one thread per light forms its waves' offsets and takes the light's base
+    // (one atomic per light with queries): two barriers for all of it.
+    __shared__ unsigned s_wc[BLOCK / 64];
+    __shared__ unsigned s_lw[kMaxLights][BLOCK / 64];   // per light: the waves' query counts ...
+    __shared__ unsigned s_lo[kMaxLights][BLOCK / 64];   // ... and their offsets in the light's list
+    __shared__ unsigned s_lbase[kMaxLights];
     __shared__ unsigned long long s_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const unsigned long long lt = __lanemask_lt();
     const unsigned long long m1 = __ballot(has);
     const unsigned coff = __popcll(m1 & lt);
-    unsigned stot = 0;
-    for (int li = 0; li < sv.num_lights; li++) stot += __popcll(__ballot((smask >> li) & 1ull));
-    if (lane == 0) { s_wc[wv] = __popcll(m1); s_ws[wv] = stot; }
+    for (int li = 0; li < sv.num_lights; li++) {
+        const unsigned c = __popcll(__ballot((smask >> li) & 1ull));
+        if (lane == 0) s_lw[li][wv] = c;
+    }
+    if (lane == 0) s_wc[wv] = __popcll(m1);
     __syncthreads();
+    if (threadIdx.x < sv.num_lights) {
+        const int li = threadIdx.x;
+        unsigned c = 0;
+        for (int k = 0; k < BLOCK / 64; k++) {
+            s_lo[li][k] = c;
+            c += s_lw[li][k];
+        }
+        s_lbase[li] = c ? atomicAdd(pr.lcnt + li, c) : 0u;
+    }
     if (threadIdx.x == 0) {
         unsigned c = 0, sh = 0;
         for (int k = 0; k < BLOCK / 64; k++) {
-            const unsigned a = s_wc[k], b = s_ws[k];
-            s_wc[k] = c; s_ws[k] = sh;
-            c += a; sh += b;
+            const unsigned a = s_wc[k];
+            s_wc[k] = c;
+            c += a;
+            for (int li = 0; li < sv.num_lights; li++) sh += s_lw[li][k];
         }
         s_base = (c | sh) ? atomicAdd(qcount, ((unsigned long long)sh << 32) | c) : 0ull;
     }
@@ -2318,54 +2381,33 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
             next_paths[idx] = cp;
             if (lv_out) lv_out[idx] = (unsigned char)(level + 1);
         }
-        nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
-        if (smask) nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, nd.F);   // read by k_shadow only
-        nodes.link[i] = make_int4(__float_as_int(Tg.x), __float_as_int(Tg.y), __float_as_int(Tg.z), nd.slot);
+        // the radiance's target: the continuation's queue slot, or the sample's slot of rad
+        float4* tgt = has ? pr.carry_out + idx : pr.rad + nd.slot;
+        if (smask == 0) {
+            // nothing pending: L + T (x) v here (Scene::RecursiveShading's col = ((amb + L0) + L1) + ...
+            // with every light term +0 -- v is never -0, so adding +0 leaves it unchanged)
+            f3 L = Lrun;
+            if (nd.kind & kContrib) L = L + cw(Tg, mk(nd.cr, nd.cg, nd.cb));
+            *tgt = make_float4(L.x, L.y, L.z, 0.0f);
+        } else {
+            // traced queries: k_shadow adds the lit lights to the colour and the last one T (x) v to
+            // the target, which holds L until then.  pnt.w: that last light's index.
+            *tgt = make_float4(Lrun.x, Lrun.y, Lrun.z, 0.0f);
+            nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
+            nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, __int_as_float(63 - __clzll((long long)smask)));
+            nodes.link[i] = make_int4(__float_as_int(Tg.x), __float_as_int(Tg.y), __float_as_int(Tg.z),
+                                      has ? idx : ~nd.slot);
+        }
     }
-    unsigned sb = (unsigned)(s_base >> 32) + s_ws[wv];
     for (int li = 0; li < sv.num_lights; li++) {
         const bool need = (smask >> li) & 1ull;
         const unsigned long long m = __ballot(need);
-        if (need) slist[sb + __popcll(m & lt)] = i * sv.num_lights + li;
-        sb += __popcll(m);
-    }    if (ctr) {
+        if (need) slist[(size_t)li * n + s_lbase[li] + s_lo[li][wv] + __popcll(m & lt)] = li * shadows.nn + i;
+    }
+    if (ctr) {
         charge(3, t_store);
         __syncthreads();
         if (threadIdx.x < 4 && s_cyc[threadIdx.x]) atomicAdd(&ctr->pt_shade_cycles[threadIdx.x], s_cyc[threadIdx.x]);
-    }
-}
-
-// L[slot] += T (x) v of every contributing vertex, one level at a time (stream order keeps
-// the oracle's per-sample summation order).  Level 0 starts the sum: L = (0,0,0) [+ T (x) v].
-// With several lights the in-order light sum of k_light_sum is folded in here.  Vertices
-// i >= nq are level-0 vertices (a pass's level 0: nq = 0; a stream step: its new samples);
-// `rad` is indexed by the vertex's slot (the link plane's w).
-__global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const PathRec* __restrict__ paths,
-                                                   const ShadowPlanes shadows, int nL,
-                                                   const NodePlanes rad, int nq, int n) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float4 nc = nodes.col[i];
-    const int kind = __float_as_int(nc.w);
-    const bool c = (kind & kContrib) != 0;
-    f3 v = mk(nc.x, nc.y, nc.z);
-    if (nL > 1 && (kind & 0x100)) {          // Scene::RecursiveShading's col = ((amb + L0) + L1) + ...
-        for (int li = 0; li < nL; li++) {
-            const float4 sc = shadows.c[(size_t)i * nL + li];
-            v = v + (sc.w != 0.0f ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));   // traced and not blocked
-        }
-    }
-    if (i >= nq) {
-        const int4 lk = nodes.link[i];          // (T.xyz, slot)
-        f3 L = mk(0, 0, 0);
-        if (c) L = L + cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v);
-        rad.col[lk.w] = make_float4(L.x, L.y, L.z, nc.w);
-    } else if (c) {
-        const int4 lk = nodes.link[i];          // (T.xyz, slot)
-        const int slot = lk.w;
-        const float4 z = rad.col[slot];
-        const f3 L = mk(z.x, z.y, z.z) + cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v);
-        rad.col[slot] = make_float4(L.x, L.y, L.z, z.w);
     }
 }
 
@@ -2375,31 +2417,36 @@ __global__ void __launch_bounds__(256) k_pt_gather(const NodePlanes nodes, const
 // does); with several, the visibility is recorded and k_light_sum adds them in light order.
 // Each query is a full closest-hit FindIntersection, as Light::IsShadow does
 // (src/Light.cpp:188-204): the distance test below decides blocking.
-template <bool EXHAUSTIVE, bool STATS, bool TLAS = false>
+// PT: the path tracer's queries of one light (one launch per light, in light order; PtRad): a lit
+// query adds its light's term to the node colour, and the node's last traced light adds T (x) v to
+// the sample's running radiance in its target (the continuation's queue slot or rad[slot]).
+template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool PT = false>
 __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const SceneView sv,
                                                                        const ShadowPlanes shadows, bool lean,
                                                                        const int* __restrict__ slist,
                                                                        const unsigned* scount, const NodePlanes nodes,
                                                                        unsigned* nan_queries, Counters* ctr,
-                                                                       int uni_from) {
+                                                                       int uni_from, const PtRad pr) {
     __shared__ int s_stack[kLdsStack * kTraceBlock];
     __shared__ short s_tstack[TLAS ? kTlasStack * kTraceBlock : 1];
-    __shared__ unsigned long long s_ecyc[STATS ? 16 : 1];
-    if (STATS && threadIdx.x < 16) s_ecyc[threadIdx.x] = 0ull;
+    __shared__ unsigned long long s_ecyc[STATS ? 18 : 1];   // entries 0..15, group set-up / tests
+    if (STATS && threadIdx.x < 18) s_ecyc[threadIdx.x] = 0ull;
     if (STATS) __syncthreads();
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned nanq = 0;
-    Stats st = {0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool was_blocked = false;
     if (j < (int)*scount) {
+        // list entry li * nn + i (ShadowPlanes: light-major); one light: the node index itself
         const int idx = slist[j];
-        const int i = idx / sv.num_lights;      // shading node of the query
+        const int li = sv.num_lights == 1 ? 0 : (int)((unsigned)idx / (unsigned)shadows.nn);
+        const int i = idx - li * shadows.nn;    // shading node of the query
         // lean3: one point / spot / directional light and no motion blur -- 12-byte origin and
         // lit-colour planes (k_shade), time 0, the mode follows from the light type
         const bool lean3 = lean && !sv.has_blur;
         float4 so;
         if (lean3) {
-            const float3 q = reinterpret_cast<const float3*>(shadows.o)[idx];
+            const float3 q = reinterpret_cast<const float3*>(shadows.o)[i];
             so = make_float4(q.x, q.y, q.z, 0.0f);
         } else {
             so = shadows.o[i];                  // one origin record per node
@@ -2419,19 +2466,20 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 tmax = shadow_tmax(o, p, lp, sv.shadow_eps);
             }
         } else {
+            // direction + light distance; the t bound light_sample used to store, rebuilt (the node's
+            // point only for an object light's bound)
             const float4 sd = shadows.d[idx];
             d = mk(sd.x, sd.y, sd.z);
-            tmax = sd.w;
+            const float qm = shadow_mode(sv, li);
+            f3 p = mk(0, 0, 0);
+            if (qm == 3.0f) {
+                const float4 pf = nodes.pnt[i];
+                p = mk(pf.x, pf.y, pf.z);
+            }
+            tmax = shadow_query_tmax(qm, o, p, d, sd.w, sv.shadow_eps);
         }
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
         auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
-        // the query's mode is re-read rather than kept live across the traversal
-        // (register pressure: 128 VGPRs for 4 waves per SIMD)
-        // (lit: the host points `c` at the L plane, whose w holds the mode)
-        auto query_mode = [&]() {
-            return lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f)
-                         : ld(reinterpret_cast<const float*>(shadows.c + idx) + 3);
-        };
         // queries of camera-sample nodes (nodes >= uni_from: level 0 of a pass, a stream step's new
         // samples): a wave whose queries all leave such nodes -- neighbouring points of one or two
         // pixels -- walks wave-uniformly (visit_object)
@@ -2441,7 +2489,8 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                              s_stack + threadIdx.x, kTraceBlock, st,
                                                              s_tstack + (TLAS ? threadIdx.x : 0), uni,
                                                              STATS ? s_ecyc : nullptr);
-        const float mode = query_mode();
+        // the query's mode from its light's type (shadow_mode), not a stored record
+        const float mode = lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f) : shadow_mode(sv, li);
         bool blocked;
         if (mode == 1.0f || mode == 3.0f) {
             blocked = false;
@@ -2449,7 +2498,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 // re-read (not kept live across the traversal: register pressure)
                 f3 o_;
                 if (lean3) {
-                    const float* qo = reinterpret_cast<const float*>(shadows.o) + 3 * (size_t)idx;
+                    const float* qo = reinterpret_cast<const float*>(shadows.o) + 3 * (size_t)i;
                     o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
                 } else {
                     const float* qo = reinterpret_cast<const float*>(shadows.o + i);
@@ -2457,21 +2506,21 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                 }
                 const float* pp = reinterpret_cast<const float*>(nodes.pnt + i);
                 const f3 p_ = mk(ld(pp), ld(pp + 1), ld(pp + 2));
-                f3 d_, l_;
+                f3 d_;
+                float dl;                       // |p - L|
                 if (lean) {     // mode 1 with one light: a point / spot light
-                    l_ = ld3(sv.lights[0].pos);
+                    const f3 l_ = ld3(sv.lights[0].pos);
                     d_ = toward(l_, p_);
+                    dl = norm(p_ - l_);
                 } else {
                     const float* qd = reinterpret_cast<const float*>(shadows.d + idx);
-                    const float* ql = reinterpret_cast<const float*>(shadows.L + idx);
                     d_ = mk(ld(qd), ld(qd + 1), ld(qd + 2));
-                    l_ = mk(ld(ql), ld(ql + 1), ld(ql + 2));
+                    dl = ld(qd + 3);
                 }
                 f3 hp = o_ + d_ * h.t;
                 if (mode == 1.0f) {             // PointLight::IsShadow: |p - L| > |p - hit|
-                    blocked = norm(p_ - l_) > norm(p_ - hp);
+                    blocked = dl > norm(p_ - hp);
                 } else {   // object light (hw7, Page7.md:143-147): an occluder nearer than the sample
-                    const float dl = norm(p_ - l_);
                     blocked = norm(p_ - hp) < dl - (sv.shadow_eps + 1e-4f * dl);
                 }
             }
@@ -2488,7 +2537,26 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             const f3 amb = mk(0, 0, 0) + cw(ld3(sv.ambient), ld3(m.ambient));
             *reinterpret_cast<float3*>(nodes.col + i) = make_float3(amb.x, amb.y, amb.z);
         };
-        if (lean3) {
+        if constexpr (PT) {
+            // lights in order (this launch is light li's): col = ((amb + L0) + L1) + ..., a blocked or
+            // untraced light's term is +0 and leaves the colour unchanged (it is never -0: amb = 0 + La ka)
+            float* cp = reinterpret_cast<float*>(nodes.col + i);
+            f3 v = mk(cp[0], cp[1], cp[2]);
+            if (!blocked) {
+                const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
+                v = v + mk(scp[0], scp[1], scp[2]);
+            }
+            if (li != __float_as_int(nodes.pnt[i].w)) {
+                if (!blocked) { cp[0] = v.x; cp[1] = v.y; cp[2] = v.z; }
+            } else {            // the node's last traced light: L + T (x) v (pt_sample's running sum)
+                const int4 lk = nodes.link[i];
+                float4* tp = lk.w >= 0 ? pr.carry_out + lk.w : pr.rad + ~lk.w;
+                const float4 z = *tp;
+                const f3 L = mk(z.x, z.y, z.z) +
+                             cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v);
+                *tp = make_float4(L.x, L.y, L.z, 0.0f);
+            }
+        } else if (lean3) {
             if (blocked) restore_ambient((int)((unsigned)__float_as_int(nodes.col[i].w) >> kNodeMatShift));
         } else if (sv.num_lights == 1) {
             float* cp = reinterpret_cast<float*>(nodes.col + i);
@@ -2522,11 +2590,13 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         unsigned wmin = was_blocked ? st.win_step : 0xFFFFFFFFu;
         for (int off = 32; off > 0; off >>= 1) wmin = min(wmin, (unsigned)__shfl_xor((int)wmin, off));
         unsigned long long wm = was_blocked ? (unsigned long long)wmin : 0ull;
-        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries;
+        unsigned long long nv = st.nodes, nt = st.tris, ns = st.steps, ne = st.entries, gw = st.gwork;
         unsigned long long bq = was_blocked ? 1ull : 0ull, bs = was_blocked ? st.steps : 0ull,
                            bt = was_blocked ? st.tris : 0ull;
-        unsigned mx = st.steps, mc = st.considered;
+        unsigned mx = st.steps, mc = st.considered, mg = st.gslot;
         for (int off = 32; off > 0; off >>= 1) {
+            gw += __shfl_down(gw, off);
+            mg = max(mg, (unsigned)__shfl_xor((int)mg, off));
             nv += __shfl_down(nv, off);
             nt += __shfl_down(nt, off);
             ns += __shfl_down(ns, off);
@@ -2540,7 +2610,11 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         }
         __syncthreads();
         if (threadIdx.x < 16 && s_ecyc[threadIdx.x]) atomicAdd(&ctr->shadow_entry_cycles[threadIdx.x], s_ecyc[threadIdx.x]);
+        if (threadIdx.x >= 16 && threadIdx.x < 18 && s_ecyc[threadIdx.x])
+            atomicAdd(&ctr->shadow_group_cycles[threadIdx.x - 16], s_ecyc[threadIdx.x]);
         if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&ctr->shadow_group_work, gw);
+            atomicAdd(&ctr->shadow_group_slots, 64ull * mg);
             atomicAdd(&ctr->shadow_node_visits, nv);
             atomicAdd(&ctr->shadow_tri_tests, nt);
             atomicAdd(&ctr->shadow_lane_slots, 64ull * mx);
@@ -2564,8 +2638,7 @@ __global__ void __launch_bounds__(256) k_light_sum(const SceneView sv, const Sha
     if (!(__float_as_int(nc.w) & 0x100)) return;
     f3 col = mk(nc.x, nc.y, nc.z);
     for (int li = 0; li < sv.num_lights; li++) {
-        const size_t k = (size_t)i * sv.num_lights + li;
-        const float4 sc = shadows.c[k];
+        const float4 sc = shadows.c[(size_t)li * shadows.nn + i];
         const bool lit = sc.w != 0.0f;      // a traced query k_shadow found blocked has mode 0
         col = col + (lit ? mk(sc.x, sc.y, sc.z) : mk(0, 0, 0));
     }
@@ -2835,7 +2908,7 @@ void launch_shade(const SceneView& sv, const CameraDev& cam, int level, const Pa
     if (n <= 0) return;
     dim3 g(nblk(n, kShadeBlock)), b(kShadeBlock);
     const NodePlanes np = node_planes(nodes, n);
-    const ShadowPlanes sp = shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1));
+    const ShadowPlanes sp = shadow_planes(shadows, n, sv.num_lights);
     const bool G = gen < 0 ? rays.a == nullptr : gen != 0;   // gen < 0: a pass's level (level 0 has no queue)
 #define RTG_SHADE(F, S, B, T, gr, bl)                                                                             \
     do {                                                                                                          \
@@ -2862,31 +2935,47 @@ void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, co
     const long long cap = (long long)n * sv.num_lights;     // upper bound of the device-side count
     dim3 g(nblk((int)cap, kTraceBlock)), b(kTraceBlock);
     const NodePlanes np = node_planes(nodes, n);
-    ShadowPlanes sp = shadow_planes(shadows, cap);
+    const ShadowPlanes sp = shadow_planes(shadows, n, sv.num_lights);
     const bool lean = whitted && sv.lean_shadow && sv.num_lights == 1;
-    const bool lit = whitted && sv.lit_nodes;     // (lean implies lit)
-    if (lit) sp.c = sp.L;                         // no contribution plane: the mode is L.w
     const bool tl = sv.tlas_root >= 0;
-    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
-    else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
-    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
-    else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from);
+    const PtRad z{};
+    if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from, z);
+    else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from, z);
+    else if (ctr) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from, z);
+    else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from, z);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, st, sv, sp, lean, slist, scount, np, nan_queries, ctr, uni_from, z);
     if (sv.num_lights > 1 && whitted)
         hipLaunchKernelGGL(k_light_sum, dim3(nblk(n, 256)), dim3(256), 0, st, sv, sp, np, n);
+}
+void launch_pt_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, NodeRec* nodes, int n, int exhaustive,
+                      Counters* ctr, unsigned* nan_queries, hipStream_t st, int uni_from, const PtRad& pr) {
+    if (n <= 0 || sv.num_lights == 0) return;
+    dim3 g(nblk(n, kTraceBlock)), b(kTraceBlock);           // a light's list holds at most n queries
+    const NodePlanes np = node_planes(nodes, n);
+    const ShadowPlanes sp = shadow_planes(shadows, n, sv.num_lights);
+    const bool tl = sv.tlas_root >= 0;
+    for (int li = 0; li < sv.num_lights; li++) {
+        const int* sl = slist + (size_t)li * n;
+        const unsigned* sc = pr.lcnt + li;
+        if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
+        else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
+        else if (ctr) hipLaunchKernelGGL((k_shadow<false, true, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
+        else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
+        else hipLaunchKernelGGL((k_shadow<false, false, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
+    }
 }
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st, bool gen, int nq, int gbase,
-                     const unsigned char* lv_in, unsigned char* lv_out, Counters* ctr) {
+                     const unsigned char* lv_in, unsigned char* lv_out, const PtRad& pr, Counters* ctr) {
     if (n <= 0) return;
     dim3 g(nblk(n, kPtBlock)), b(kPtBlock);
 #define RTG_PT_LAUNCH1(F, S, B, G)                                                                                \
     hipLaunchKernelGGL((k_pt_shade<F, S, B, G>), g, b, 0, st, sv, cam, level, ps, seed, rays, meta, hits, paths, \
                        node_planes(nodes, n), \
-                       shadow_planes(shadows, (long long)n * (sv.num_lights > 1 ? sv.num_lights : 1)), slist, next_rays, next_meta, next_paths, qcount, n, \
-                       nq, gbase, lv_in, lv_out, ctr)
+                       shadow_planes(shadows, n, sv.num_lights), slist, next_rays, next_meta, next_paths, qcount, n, \
+                       nq, gbase, lv_in, lv_out, pr, ctr)
 #define RTG_PT_LAUNCH(F, S, B)                                                                                    \
     do {                                                                                                          \
         if (gen) RTG_PT_LAUNCH1(F, S, B, true);                                                                   \
@@ -2904,13 +2993,6 @@ void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const
     else RTG_PT_LAUNCH(false, false, 0);
 #undef RTG_PT_LAUNCH
 #undef RTG_PT_LAUNCH1
-}
-void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* rad,
-                      long long n_rad, int nq, int n, hipStream_t st) {
-    if (n <= 0) return;
-    hipLaunchKernelGGL(k_pt_gather, dim3(nblk(n, 256)), dim3(256), 0, st, node_planes(const_cast<NodeRec*>(nodes), n), paths,
-                       shadow_planes(const_cast<ShadowRec*>(shadows), (long long)n * (nL > 1 ? nL : 1)), nL,
-                       node_planes(rad, n_rad), nq, n);
 }
 void launch_resolve2(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, const NodeRec* grand_nodes, int n,
                      int n_child, int n_grand, hipStream_t st) {

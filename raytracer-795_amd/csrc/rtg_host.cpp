@@ -1093,11 +1093,12 @@ int upload(DBuf& b, const V& v) {
 
 struct Level {
     DBuf rays, meta, hits, nodes, shadows, slist, paths;
+    DBuf carry;                // path tracer: each queued ray's running radiance (16 B, k_pt_gather)
     DBuf lv;                   // stream schedule: the queued rays' levels (1 byte each)
     long long rcap = 0;        // plane stride of `rays` (RayQ) as the previous level wrote them
     void release() {
         rays.release(); meta.release(); hits.release(); nodes.release(); shadows.release(); slist.release();
-        paths.release(); lv.release();
+        paths.release(); carry.release(); lv.release();
     }
 };
 
@@ -1112,6 +1113,8 @@ struct Lane {
                                             // path-tracer gather end
     unsigned long long* h_count = nullptr;  // pinned host slot
     DBuf qcnt;                              // 128 x u64 per pass: [level] next rays | shadow entries << 32
+    DBuf lcnt;                              // path tracer: per-light shadow-list counts per level / step
+    DBuf prad;                              // path tracer, pass schedule: the pass's sample radiance (16 B)
     std::vector<Level> levels;
     // current pass
     std::vector<int> passes;                // indices into the frame's pass list (this lane's, in order)
@@ -1136,7 +1139,7 @@ struct Lane {
         for (Level& l : levels) l.release();
         for (DBuf& b : snodes) b.release();
         snodes.clear();
-        qcnt.release();
+        qcnt.release(); lcnt.release(); prad.release();
         if (h_count) (void)hipHostFree(h_count);
         for (hipEvent_t e : ev_t) if (e) (void)hipEventDestroy(e);
         if (ev_count) (void)hipEventDestroy(ev_count);
@@ -1490,6 +1493,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     bool early_upload = false;               // dnodes / gates / tris / primidx / orig_prim / vnormals uploaded by early_thread
     std::thread early_thread;
     int early_rc = RTG_OK;
+    std::string early_err;                   // early_thread's rtg_last_error() (thread-local there)
     struct EarlyJoin {                       // joined on every return path (the thread reads this frame's arrays)
         std::thread& t;
         ~EarlyJoin() { if (t.joinable()) t.join(); }
@@ -1806,12 +1810,14 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         // nothing below writes these arrays).  Dragon1m: ~7-10 ms of host-to-device copies.
         if (s->device >= 0 && i == d->num_objects - 1 && sah_thread.joinable()) {
             early_thread = std::thread([&, dev = s->device] {
-                if (hipSetDevice(dev) != hipSuccess) { early_rc = RTG_ERR_HIP; return; }
+                if (hipSetDevice(dev) != hipSuccess) { early_rc = RTG_ERR_HIP; early_err = "hipSetDevice"; return; }
                 int rc2;
                 if ((rc2 = upload(s->d_nodes, dnodes)) || (rc2 = upload(s->d_gates, gates)) || (rc2 = upload(s->d_tris, tris)) ||
                     (rc2 = upload(s->d_primidx, primidx)) || (rc2 = upload(s->d_origprim, s->orig_prim)) ||
-                    (rc2 = upload(s->d_vnormals, s->vnormals)))
+                    (rc2 = upload(s->d_vnormals, s->vnormals))) {
                     early_rc = rc2;
+                    early_err = rtg_last_error();
+                }
             });
             early_upload = true;
             sub.lap(" early_upload start");
@@ -2152,7 +2158,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     if (d->num_texcoords > 0) tcflat.assign(d->texcoords, d->texcoords + 2 * (size_t)d->num_texcoords);
     int rc;
     if (early_thread.joinable()) early_thread.join();
-    if (early_rc != RTG_OK) return fail(early_rc, "scene upload (reference-tree records)");
+    if (early_rc != RTG_OK) return fail(early_rc, "scene upload (reference-tree records): " + early_err);
     if (!early_upload &&
         ((rc = upload(s->d_nodes, dnodes)) || (rc = upload(s->d_gates, gates)) || (rc = upload(s->d_tris, tris)) ||
          (rc = upload(s->d_primidx, primidx)) || (rc = upload(s->d_origprim, s->orig_prim)) ||
@@ -2419,7 +2425,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const long long kMax = rtg_pass_rays(nL, pt ? 1 : 0, lanes_req, (uint64_t)total_b);
         const long long kMin = std::min<long long>(2LL << 20, kMax);
         const long long lanes_eff = std::max(1LL, std::min<long long>(lanes_req, (frame_rays + kMin - 1) / kMin));
-        const long long passes = lanes_eff * ((frame_rays + lanes_eff * kMax - 1) / (lanes_eff * kMax));
+        // (an empty shard -- fewer row blocks than ranks -- has no rays: one empty pass, not a division by 0)
+        const long long passes = std::max(1LL, lanes_eff * ((frame_rays + lanes_eff * kMax - 1) / (lanes_eff * kMax)));
         if (total > kMax) {                 // absurd spp: sample chunks of one pixel
             ns_chunk = (int)kMax;
             np_pass = 1;
@@ -2518,9 +2525,13 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         Ln.rcap = (long long)cap;
         const RayQ cur_q = level == 0 ? RayQ{} : ray_planes(Lc.rays.p, Lc.rcap, sv.has_blur);
         const RayQ next_q = ray_planes(Ln.rays.p, Ln.rcap, sv.has_blur);
-        if (pt && ((rc2 = Lc.paths.grow(sizeof(PathRec) * (size_t)n)) || (rc2 = Ln.paths.grow(sizeof(PathRec) * cap))))
+        if (pt && ((rc2 = Lc.paths.grow(sizeof(PathRec) * (size_t)n)) || (rc2 = Ln.paths.grow(sizeof(PathRec) * cap)) ||
+                   (rc2 = Lc.carry.grow(kCarryBytes * (size_t)n)) || (rc2 = Ln.carry.grow(kCarryBytes * cap))))
             return rc2;
         unsigned long long* qc = ln.qcnt.as<unsigned long long>() + level;
+        const PtRad pr = pt ? PtRad{Lc.carry.as<float4>(), Ln.carry.as<float4>(), ln.prad.as<float4>(),
+                                    ln.lcnt.as<unsigned>() + (size_t)level * std::max(nL, 1)}
+                            : PtRad{};
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
         // level 0: k_trace / k_shade / k_pt_shade regenerate the primary rays (no level-0 ray buffer)
         const bool gen = level == 0;
@@ -2532,7 +2543,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                             gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
                             Lc.paths.as<PathRec>(), Lc.nodes.as<NodeRec>(), Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
                             next_q, Ln.meta.as<RayMeta>(), Ln.paths.as<PathRec>(), qc, n, ln.st,
-                            gen, gen ? 0 : n, 0, nullptr, nullptr, sctr);
+                            gen, gen ? 0 : n, 0, nullptr, nullptr, pr, sctr);
         else
             launch_shade(sv, cd, level, ps, o.seed, cur_q,
                          gen ? nullptr : Lc.meta.as<RayMeta>(), Lc.hits.as<HitRec>(),
@@ -2545,16 +2556,17 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
         HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
-        launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
-                      reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
-                      Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/!pt, /*uni_from=*/level < kUniShadowLevels ? 0 : INT_MAX);
+        // (the path tracer: one launch per light, in light order, adding each vertex's T (x) v to its
+        // sample's running radiance -- PtRad; no gather kernel)
+        if (pt)
+            launch_pt_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(), Lc.nodes.as<NodeRec>(), n, exhaustive,
+                             sctr, d_cnt, ln.st, /*uni_from=*/level < kUniShadowLevels ? 0 : INT_MAX, pr);
+        else
+            launch_shadow(sv, Lc.shadows.as<ShadowRec>(), Lc.slist.as<int>(),
+                          reinterpret_cast<const unsigned*>(qc) + 1,   // high word (little endian)
+                          Lc.nodes.as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*light_sum=*/true,
+                          /*uni_from=*/level < kUniShadowLevels ? 0 : INT_MAX);
         if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
-        // path tracer: L[slot] += T (x) vertex contribution, level by level in stream order
-        if (pt) {
-            launch_pt_gather(Lc.nodes.as<NodeRec>(), Lc.paths.as<PathRec>(), Lc.shadows.as<ShadowRec>(), nL,
-                             ln.levels[0].nodes.as<NodeRec>(), ln.counts[0], level == 0 ? 0 : n, n, ln.st);
-            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[5], ln.st));
-        }
         HIP_TRY(hipGetLastError());
         return RTG_OK;
     };
@@ -2565,6 +2577,11 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         int rc2;
         if ((rc2 = ln.qcnt.grow(sizeof(unsigned long long) * 128))) return rc2;
         HIP_TRY(hipMemsetAsync(ln.qcnt.p, 0, sizeof(unsigned long long) * 128, ln.st));
+        if (pt) {
+            const size_t nlc = (size_t)(max_levels + 1) * std::max(nL, 1);
+            if ((rc2 = ln.prad.grow((size_t)16 * std::max(n0, 1))) || (rc2 = ln.lcnt.grow(sizeof(unsigned) * nlc))) return rc2;
+            HIP_TRY(hipMemsetAsync(ln.lcnt.p, 0, sizeof(unsigned) * nlc, ln.st));
+        }
         ln.counts.assign(1, n0);
         ln.level = 0;
         if ((int)ln.levels.size() < 1) ln.levels.resize(1);
@@ -2611,7 +2628,9 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         const NodeRec* level1 = level >= 1 ? N(1) : nullptr;
         const NodeRec* level2 = level >= 2 ? N(2) : nullptr;
         if ((rc2 = timed_launch(ln, [&] {
-                 launch_accumulate(sv, N(0), level1, !pt && level >= 1, s->d_acc.as<float>(), ps, cam->nx, mode, ln.st, !pt,
+                 // (the path tracer: the pass's sample radiance, PtRad)
+                 launch_accumulate(sv, pt ? ln.prad.as<NodeRec>() : N(0), level1, !pt && level >= 1, s->d_acc.as<float>(), ps,
+                                   cam->nx, mode, ln.st, !pt,
                                    ln.counts[0], level >= 1 ? ln.counts[1] : 0, pt ? nullptr : level2,
                                    level >= 2 ? ln.counts[2] : 0);
              }, stt.accumulate_ms, stt.accumulate_launches)))
@@ -2686,11 +2705,13 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                 for (int b2 = 0; b2 < 2; b2++) {
                     Level& Q = ln.levels[b2];
                     if ((rc = Q.rays.grow(kRayBytes * (size_t)R)) || (rc = Q.meta.grow(sizeof(int) * (size_t)R)) ||
-                        (rc = Q.lv.grow((size_t)R)) || (rc = Q.paths.grow(sizeof(PathRec) * (size_t)R)))
+                        (rc = Q.lv.grow((size_t)R)) || (rc = Q.paths.grow(sizeof(PathRec) * (size_t)R)) ||
+                        (rc = Q.carry.grow(kCarryBytes * (size_t)R)))
                         return rc;
                     Q.rcap = R;
                 }
             if ((rc = ln.qcnt.grow(sizeof(unsigned long long) * 128))) return rc;
+            if (pt && (rc = ln.lcnt.grow(sizeof(unsigned) * 2 * (size_t)nLb))) return rc;
             HIP_TRY(hipStreamWaitEvent(ln.st, e0, 0));
         }
         PassDev F;
@@ -2742,6 +2763,14 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             const RayQ next_q = ray_planes(B.rays.p, B.rcap, sv.has_blur);
             unsigned long long* qc = ln.qcnt.as<unsigned long long>() + (step & 1);
             HIP_TRY(hipMemsetAsync(qc, 0, sizeof(unsigned long long), ln.st));
+            // the path tracer's radiance (PtRad): survivors' sums in A, their children's in B, a
+            // sample's last vertex writes the segment's rad; per-light list counts of the step
+            PtRad pr{};
+            if (pt) {
+                pr = PtRad{A.carry.as<float4>(), B.carry.as<float4>(), s->d_rad.as<float4>(),
+                           ln.lcnt.as<unsigned>() + (size_t)(step & 1) * nLb};
+                HIP_TRY(hipMemsetAsync(pr.lcnt, 0, sizeof(unsigned) * nLb, ln.st));
+            }
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[0], ln.st));
             launch_trace(sv, cur_q, W.hits.as<HitRec>(), n, exhaustive, sctr, ln.st, g > 0 ? &cd : nullptr, &F, o.seed,
                          /*compact=*/true, m, gbase);
@@ -2750,7 +2779,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                 launch_pt_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), W.hits.as<HitRec>(), A.paths.as<PathRec>(),
                                 nodes->as<NodeRec>(), W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q,
                                 B.meta.as<RayMeta>(), B.paths.as<PathRec>(), qc, n, ln.st, g > 0, m, gbase,
-                                A.lv.as<unsigned char>(), B.lv.as<unsigned char>(), sctr);
+                                A.lv.as<unsigned char>(), B.lv.as<unsigned char>(), pr, sctr);
             else
                 launch_shade(sv, cd, 0, F, o.seed, cur_q, A.meta.as<RayMeta>(), W.hits.as<HitRec>(), nodes->as<NodeRec>(),
                              W.shadows.as<ShadowRec>(), W.slist.as<int>(), next_q, B.meta.as<RayMeta>(), qc, n, ln.st, g > 0 ? 1 : 0, m, gbase, A.lv.as<unsigned char>(), B.lv.as<unsigned char>());
@@ -2758,14 +2787,16 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             HIP_TRY(hipMemcpyAsync(ln.h_count, qc, sizeof(unsigned long long), hipMemcpyDeviceToHost, ln.st));
             HIP_TRY(hipEventRecord(ln.ev_count, ln.st));
             if (timing) HIP_TRY(hipEventRecord(ln.ev_t[3], ln.st));
-            launch_shadow(sv, W.shadows.as<ShadowRec>(), W.slist.as<int>(), reinterpret_cast<const unsigned*>(qc) + 1,
-                          nodes->as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*whitted=*/!pt,
-                          /*uni_from=*/g > 0 ? m : INT_MAX);   // the step's new camera samples: nodes [m, n)
-            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
+            // the step's new camera samples: nodes [m, n) (uni_from); the path tracer: one launch per
+            // light, in light order, adding each vertex's T (x) v to its sample's radiance (PtRad)
             if (pt)
-                launch_pt_gather(nodes->as<NodeRec>(), A.paths.as<PathRec>(), W.shadows.as<ShadowRec>(), nL,
-                                 s->d_rad.as<NodeRec>(), seg_slots, m, n, ln.st);
-            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[5], ln.st));
+                launch_pt_shadow(sv, W.shadows.as<ShadowRec>(), W.slist.as<int>(), nodes->as<NodeRec>(), n, exhaustive,
+                                 sctr, d_cnt, ln.st, /*uni_from=*/g > 0 ? m : INT_MAX, pr);
+            else
+                launch_shadow(sv, W.shadows.as<ShadowRec>(), W.slist.as<int>(), reinterpret_cast<const unsigned*>(qc) + 1,
+                              nodes->as<NodeRec>(), n, exhaustive, sctr, d_cnt, ln.st, /*whitted=*/true,
+                              /*uni_from=*/g > 0 ? m : INT_MAX);
+            if (timing) HIP_TRY(hipEventRecord(ln.ev_t[4], ln.st));
             HIP_TRY(hipGetLastError());
             ln.level++;
             ln.busy = true;
@@ -2818,16 +2849,14 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                 const unsigned next = (unsigned)q;
                 shadow_listed += q >> 32;
                 if (timing) {
-                    float a = 0.0f, b = 0.0f, c = 0.0f, g2 = 0.0f;
+                    float a = 0.0f, b = 0.0f, c = 0.0f;
                     HIP_TRY(hipEventElapsedTime(&a, ln.ev_t[0], ln.ev_t[1]));
                     HIP_TRY(hipEventElapsedTime(&c, ln.ev_t[1], ln.ev_t[2]));
-                    HIP_TRY(hipEventSynchronize(ln.ev_t[5]));
+                    HIP_TRY(hipEventSynchronize(ln.ev_t[4]));
                     HIP_TRY(hipEventElapsedTime(&b, ln.ev_t[3], ln.ev_t[4]));
-                    HIP_TRY(hipEventElapsedTime(&g2, ln.ev_t[4], ln.ev_t[5]));
                     stt.trace_ms += a; stt.trace_launches++;
                     stt.shade_ms += c; stt.shade_launches++;
                     if (nL > 0) { stt.shadow_ms += b; stt.shadow_launches++; }
-                    if (pt) { stt.resolve_ms += g2; stt.resolve_launches++; }   // the gather, in the resolve slot
                 }
                 if ((long long)next > (pt ? 1LL : 2LL) * ln.sn) return fail(RTG_ERR_HIP, "stream queue overflow");
                 if (!pt && next > 0 && ln.level >= (1 << 20)) return fail(RTG_ERR_UNSUPPORTED, "stream: too many steps");
@@ -2921,13 +2950,6 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
                 stt.shadow_ms += b;
                 stt.shadow_launches++;
             }
-            if (pt) {       // the path tracer's per-level gather, timed in the resolve slot
-                float g = 0.0f;
-                HIP_TRY(hipEventSynchronize(ln.ev_t[5]));
-                HIP_TRY(hipEventElapsedTime(&g, ln.ev_t[4], ln.ev_t[5]));
-                stt.resolve_ms += g;
-                stt.resolve_launches++;
-            }
         }
         const int n = ln.counts[ln.level];
         const bool may_spawn = ln.level + 1 < max_levels;
@@ -2990,6 +3012,14 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     stt.shadow_blocked_steps_before = ctr.shadow_blocked_steps_before;
     stt.shadow_blocked_steps_before_wavemin = ctr.shadow_blocked_steps_before_wavemin;
     for (int b = 0; b < 4; b++) stt.pt_shade_cycles[b] = ctr.pt_shade_cycles[b];
+    stt.trace_group_work = ctr.trace_group_work;
+    stt.trace_group_slots = ctr.trace_group_slots;
+    stt.shadow_group_work = ctr.shadow_group_work;
+    stt.shadow_group_slots = ctr.shadow_group_slots;
+    for (int b = 0; b < 2; b++) {
+        stt.trace_group_cycles[b] = ctr.trace_group_cycles[b];
+        stt.shadow_group_cycles[b] = ctr.shadow_group_cycles[b];
+    }
     for (int b = 0; b < 16; b++) {
         stt.trace_entry_cycles[b] = ctr.trace_entry_cycles[b];
         stt.shadow_entry_cycles[b] = ctr.shadow_entry_cycles[b];

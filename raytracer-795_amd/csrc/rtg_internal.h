@@ -316,8 +316,8 @@ struct NodeRec {        // 48 B, one per traced ray
 // Whitted path: a level's n node records as three planes in the same 48 n bytes (structure of
 // arrays), so the kernels that only need a node's colour (accumulate, light sums, final nodes in
 // resolve) read 16 B of it, and k_shade stores the point only for hits and the links only for
-// non-final nodes.  The path tracer uses the same planes (all three stored; link.w = the slot
-// k_pt_gather adds the vertex's contribution to).
+// non-final nodes.  The path tracer uses the same planes for nodes with traced shadow queries only:
+// colour + kind, point + index of the last traced light, throughput + radiance target (PtRad).
 struct NodePlanes {
     float4* col;    // cr, cg, cb, kind (int bits; kNodeHit set for hits)
     float4* pnt;    // px, py, pz, F               (hit nodes only)
@@ -336,25 +336,30 @@ inline NodePlanes node_planes(NodeRec* base, long long n) {
     return NodePlanes{b, b + n, reinterpret_cast<int4*>(b + 2 * n)};
 }
 
-struct ShadowRec {      // 64 B, nLights per shading node
+struct ShadowRec {      // 48 B per query (the allocation unit of a level's shadow planes)
     float4 o;           // origin.xyz, time
-    float4 d;           // direction.xyz, tmax (world t bound; +inf for directional/env)
-    float4 c;           // contribution rgb, mode (0 none, 1 distance test, 2 any hit)
-    float4 L;           // light point for the distance test, pad
+    float4 d;           // direction.xyz, dl = |p - light point| (modes 1 / 3; k_shadow rebuilds the t bound)
+    float4 c;           // contribution rgb, mode (0 none, 1 distance test, 2 any hit, 3 object light)
 };
 
-// A level's shadow records as four planes over cap = nodes x lights entries (same 64 cap bytes):
-// k_shadow reads the ray planes before its traversal and the contribution after it, and the
-// lean single-light Whitted path (SceneView::lean_shadow) does not store `d` / `L` at all.
+// A level's shadow records as planes (round 6): the origin per shading node (o[i]; the lean
+// single-light path stores it as 12-byte records), direction + light distance and contribution per
+// query, LIGHT-MAJOR: query (node i, light li) at li * nn + i, so the queries of one light that a
+// wave traces (the list is light-major within a wave) read consecutive records -- node-major
+// (i * nLights + li) left every 128-byte line of d / c half used by a wave (C5: 142 B per query).
+// No light-point plane: k_shadow's blocking tests need only dl, and the query's mode follows from
+// the light's type (shadow_mode).
 struct ShadowPlanes {
-    float4* o;      // origin.xyz, time
-    float4* d;      // direction.xyz, tmax
-    float4* c;      // contribution rgb, mode (several lights: k_shadow zeroes it for a blocked query)
-    float4* L;      // light point
+    float4* o;      // origin.xyz, time                      (per node)
+    float4* d;      // direction.xyz, dl                     (per query)
+    float4* c;      // contribution rgb, mode                (per query; several lights: k_shadow zeroes the
+                    // mode of a blocked query)
+    int nn;         // nodes of the level: the light stride of d / c
 };
-inline ShadowPlanes shadow_planes(ShadowRec* base, long long cap) {
+inline ShadowPlanes shadow_planes(ShadowRec* base, int nodes, int lights) {
     float4* b = reinterpret_cast<float4*>(base);
-    return ShadowPlanes{b, b + cap, b + 2 * cap, b + 3 * cap};
+    const long long cap = (long long)nodes * (lights > 1 ? lights : 1);
+    return ShadowPlanes{b, b + nodes, b + nodes + cap, nodes};
 }
 
 struct Counters {
@@ -375,7 +380,26 @@ struct Counters {
     unsigned long long trace_entry_cycles[16], shadow_entry_cycles[16];
     // k_pt_shade wave cycles by phase: hit set-up, next-event estimation, continuation, compaction + stores
     unsigned long long pt_shade_cycles[4];
+    // the flat group (round 6): lane work (triangle tests the lanes ran) and slots (64 x the tests their
+    // waves ran), and its wave cycles split into set-up and tests
+    unsigned long long trace_group_work, trace_group_slots, shadow_group_work, shadow_group_slots;
+    unsigned long long trace_group_cycles[2], shadow_group_cycles[2];
 };
+
+// The path tracer's radiance (round 6): the running sum L of a sample travels with its
+// path.  k_pt_shade reads it from the ray's queue slot (carry_in[i]; a new sample starts from (0,0,0)).
+// A vertex whose contribution is final there (no traced shadow query) adds T (x) v itself and hands L
+// to its continuation (carry_out at the child's queue index) or, the path's last vertex, writes
+// rad[slot]; a vertex with traced queries leaves L in that target and its last light's query in
+// k_shadow (per-light launches, in light order) adds T (x) v.  No per-level gather kernel.
+// lcnt: the level's per-light shadow-list counts (the list of light li at slist + li * n).
+struct PtRad {
+    const float4* carry_in;
+    float4* carry_out;
+    float4* rad;
+    unsigned* lcnt;
+};
+constexpr size_t kCarryBytes = 16;    // float4 per queued ray
 
 // Host-side launchers (rtg_device.hip) ------------------------------------------------
 struct LevelBuffers;
@@ -399,15 +423,14 @@ void launch_accumulate_planes(const SceneView& sv, const NodePlanes& level0, con
                               float* acc, const PassDev& ps, int nx, int mode, hipStream_t st);
 void launch_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, const unsigned* scount, NodeRec* nodes,
                    int n, int exhaustive, Counters* ctr, unsigned* nan_queries, hipStream_t st, bool whitted = true, int uni_from = INT_MAX);  // uni_from: first camera-sample node (wave-uniform walk)
+// the path tracer's queries: one launch per light, in light order (PtRad)
+void launch_pt_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist, NodeRec* nodes, int n, int exhaustive,
+                      Counters* ctr, unsigned* nan_queries, hipStream_t st, int uni_from, const PtRad& pr);
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,
                      const RayQ rays, const RayMeta* meta, const HitRec* hits, PathRec* paths, NodeRec* nodes,
                      ShadowRec* shadows, int* slist, const RayQ next_rays, RayMeta* next_meta, PathRec* next_paths,
                      unsigned long long* qcount, int n, hipStream_t st, bool gen, int nq, int gbase,
-                     const unsigned char* lv_in, unsigned char* lv_out, Counters* ctr = nullptr);
-// rad: NodePlanes over n_rad sample slots (its colour plane is the samples' radiance); vertices
-// i >= nq start their slot's sum (level 0)
-void launch_pt_gather(const NodeRec* nodes, const PathRec* paths, const ShadowRec* shadows, int nL, NodeRec* rad,
-                      long long n_rad, int nq, int n, hipStream_t st);
+                     const unsigned char* lv_in, unsigned char* lv_out, const PtRad& pr, Counters* ctr = nullptr);
 void launch_resolve(const SceneView& sv, NodeRec* nodes, const NodeRec* child_nodes, int n, int n_child,
                     hipStream_t st);
 // levels p (nodes) and p + 1 (child_nodes, resolved inline, not stored) against the resolved level p + 2
@@ -496,16 +519,23 @@ struct PinnedBuf {
 
 // Page-locked staging from a process-wide pool: hipHostMalloc of the ~80 MB a 1 M-triangle build
 // returns costs milliseconds per scene creation, so the buffers are kept and reused.
-void* pinned_pool_get(size_t bytes);
-void pinned_pool_put(void* p, size_t bytes);
+// get returns a buffer of at least `bytes` and its real capacity in *cap; put takes the capacity back.
+void* pinned_pool_get(size_t bytes, size_t* cap);
+void pinned_pool_put(void* p, size_t cap);
 struct PooledPinned {
     void* p = nullptr;
-    size_t bytes = 0;
+    size_t cap = 0;           // the buffer's real capacity (>= the bytes last asked for)
     PooledPinned() = default;
     PooledPinned(const PooledPinned&) = delete;
     PooledPinned& operator=(const PooledPinned&) = delete;
-    ~PooledPinned() { if (p) pinned_pool_put(p, bytes); }
-    bool get(size_t b) { if (p) pinned_pool_put(p, bytes); bytes = b; p = pinned_pool_get(b); return p != nullptr; }
+    ~PooledPinned() { if (p) pinned_pool_put(p, cap); }
+    bool get(size_t b) {
+        if (p && cap >= b) return true;
+        if (p) pinned_pool_put(p, cap);
+        cap = 0;
+        p = pinned_pool_get(b, &cap);
+        return p != nullptr;
+    }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 // The GPU median-split build's result: nodes in breadth-first order (children after their parent) as

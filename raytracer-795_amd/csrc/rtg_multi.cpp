@@ -444,7 +444,7 @@ struct rtg_comm {
     const Rccl* R = nullptr;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1, device = 0;
-    int timeout_ms = 120000;
+    int timeout_ms = 0;            // <= 0: no deadline (rtg_comm_init_rank)
     bool nonblocking = false;
     bool dead = false;
     DevBuf part, recv, flag;
@@ -453,6 +453,12 @@ struct rtg_comm {
 namespace rtg {
 namespace {
 using Clock = std::chrono::steady_clock;
+
+// The deadline of a wait that starts at t0: none (time_point::max) for a communicator set up without a
+// timeout, so a peer's long shard render never aborts a healthy rank.
+Clock::time_point comm_deadline(const rtg_comm* c, Clock::time_point t0) {
+    return c->timeout_ms > 0 ? t0 + std::chrono::milliseconds(c->timeout_ms) : Clock::time_point::max();
+}
 
 // Wait for a non-blocking communicator's pending operation (set-up, an enqueue) to leave
 // ncclInProgress, or for the deadline; on the deadline or an asynchronous error the communicator is
@@ -577,9 +583,9 @@ int32_t rtg_comm_init_rank_timeout(const uint8_t id[RTG_COMM_ID_BYTES], int32_t 
         memcpy(&u, id, sizeof u);
         rtg_comm* k = new rtg_comm();
         k->R = R; k->rank = rank; k->nranks = nranks; k->device = device;
-        k->timeout_ms = timeout_ms > 0 ? timeout_ms : 120000;
+        k->timeout_ms = timeout_ms > 0 ? timeout_ms : 0;
         k->nonblocking = R->CommInitRankConfig && R->CommGetAsyncError && R->CommAbort;
-        const auto deadline = Clock::now() + std::chrono::milliseconds(k->timeout_ms);
+        const auto deadline = comm_deadline(k, Clock::now());
         ncclResult_t e;
         if (k->nonblocking) {
             ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -662,7 +668,7 @@ int32_t rtg_render_ranked(rtg_scene* s, const rtg_camera_desc* cam, const rtg_re
         const std::string local_err = rc == RTG_OK ? std::string() : std::string(rtg_last_error());
         const auto t1 = std::chrono::steady_clock::now();
         // the agreement and the gather share one deadline, counted from the shard's end
-        const auto deadline = t1 + std::chrono::milliseconds(c->timeout_ms);
+        const auto deadline = comm_deadline(c, t1);
         std::string why;
         const int failed = agree_failures(c, rc != RTG_OK, st, deadline, why);
         if (failed < 0) return set_error(RTG_ERR_HIP, "rank status agreement: " + why +

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RTG_ABI_VERSION = 8
+RTG_ABI_VERSION = 9
 
 RTG_OK = 0
 RTG_DEVICE_HOST_ONLY = -1
@@ -133,7 +133,11 @@ class RenderStats(C.Structure):
                 ("shadow_blocked_steps_before", C.c_uint64),
                 ("shadow_blocked_steps_before_wavemin", C.c_uint64),
                 ("trace_entry_cycles", C.c_uint64 * 16), ("shadow_entry_cycles", C.c_uint64 * 16),
-                ("pt_shade_cycles", C.c_uint64 * 4)]
+                ("pt_shade_cycles", C.c_uint64 * 4),
+                # ABI 9: the flat group's lane work / slots and set-up / test cycles
+                ("trace_group_work", C.c_uint64), ("trace_group_slots", C.c_uint64),
+                ("shadow_group_work", C.c_uint64), ("shadow_group_slots", C.c_uint64),
+                ("trace_group_cycles", C.c_uint64 * 2), ("shadow_group_cycles", C.c_uint64 * 2)]
 
 RTG_COMM_ID_BYTES = 128
 
@@ -236,11 +240,23 @@ def load_library(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rtg_abi_version() != RTG_ABI_VERSION:
+    v = lib.rtg_abi_version()
+    # dev A/B variants (RTG_LIBRARY) may be one ABI older: ABI 9 only appended rtg_render_stats fields,
+    # which then read 0 (the structure is zero-initialised and the older library writes its own prefix)
+    if v != RTG_ABI_VERSION and not (os.environ.get("RTG_LIBRARY") and v == RTG_ABI_VERSION - 1 == 8):
         raise RtgError("librtg.so ABI version mismatch")
     if path is None:
         _lib = lib
     return lib
+
+
+def loaded_abi() -> int:
+    """The ABI version of the library in use (RTG_ABI_VERSION, or a dev variant's one older: the scene
+    descriptor's layout is the same in ABI 8 and 9)."""
+    try:
+        return int(load_library().rtg_abi_version())
+    except (RtgError, OSError):
+        return RTG_ABI_VERSION
 
 
 def check(rc: int, lib=None):

@@ -265,8 +265,9 @@ class Comm:
         return bytes(buf)
 
     def __init__(self, uid: bytes, nranks: int, rank: int, device: int, timeout_ms: int = 0):
-        """timeout_ms bounds every wait of this rank (set-up, failure agreement, gather); 0 = the
-        library default (120 s).  A rank whose peers do not join returns an error instead of hanging."""
+        """timeout_ms bounds every wait of this rank (set-up, failure agreement, gather; the latter two
+        count from this rank's shard end, so the bound must cover the peers' remaining render time); 0 = no
+        deadline.  With a bound, a rank whose peers do not join returns an error instead of hanging."""
         self.lib = A.load_library()
         if len(uid) != A.RTG_COMM_ID_BYTES:
             raise ValueError("communicator id must be 128 bytes")

@@ -193,7 +193,7 @@ class Scene:
             return a.ctypes.data_as(C.POINTER(ctype)), a
 
         d = A.SceneDesc()
-        d.abi_version = A.RTG_ABI_VERSION
+        d.abi_version = A.loaded_abi()
         d.max_recursion_depth = int(self.max_depth)
         d.shadow_ray_eps = float(f32(self.shadow_eps))
         d.intersection_test_eps = float(f32(self.int_eps))

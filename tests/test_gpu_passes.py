@@ -45,3 +45,29 @@ def test_tile_order_does_not_change_the_frame(gpu, tile_band):
         shard = r.render(0, num_devices=2, devices=[0, 0], tile_band=tile_band)
     assert np.array_equal(_bits(img), _bits(ref))
     assert np.array_equal(_bits(shard), _bits(ref))
+
+
+def test_wide_row_with_a_tall_band_is_not_mis_tiled(gpu):
+    """tile_pixel forms tile_h * tile_band * nx in 32-bit ints.  A 2^20-pixel row with
+    tile_band = 4096 would be 2^35 pixels per band; the band is clamped so that one band stays below
+    2^31, and the frame equals the one-tile-high order bit for bit (pixels are not mis-placed)."""
+    sc = scenegen.simple(1 << 20, 1)
+    with rtg.Renderer(sc, device=gpu) as r:
+        ref = r.render(0, tile_band=1)
+        img = r.render(0, tile_band=4096)
+        shard = r.render(0, num_devices=2, devices=[0, 0], tile_band=4096)
+    assert np.isfinite(ref).all()
+    assert np.array_equal(_bits(img), _bits(ref))
+    assert np.array_equal(_bits(shard), _bits(ref))
+
+
+@pytest.mark.parametrize("ny", [1, 5])
+def test_more_shards_than_row_blocks(gpu, ny):
+    """Shards that own no rows (an image with fewer 4-row blocks than shards, e.g. 8 GPUs and a short
+    image) render nothing and the gather still yields the single-device frame (round 6: the pass count of
+    an empty shard divided by zero)."""
+    sc = scenegen.simple(64, ny)
+    with rtg.Renderer(sc, device=gpu) as r:
+        ref = r.render(0)
+        shard = r.render(0, num_devices=3, devices=[0, 0, 0])
+    assert np.array_equal(_bits(shard), _bits(ref))

@@ -97,11 +97,13 @@ def _tree(sc, builder):
     return bs, img
 
 
-@pytest.mark.parametrize("n", [2, 5, 300, 2048, 2049, 5000, 70000])
+@pytest.mark.parametrize("n", [2, 5, 300, 512, 513, 1025, 2048, 2049, 5000, 70000])
 def test_gpu_sah_tree_equals_host_tree(gpu, n):
     """The GPU binned-SAH build applies the host's split rule to the same record sets, so both trees
     have the same nodes (box + triangle count; order-independent hash) and every frame is identical.
-    Sizes around the one-wave subtree limit (2048) and the level phase (70000)."""
+    Sizes at the one-wave subtree limit (kSmall = 512 records in rtg_sah_gpu.hip: 512 is built by one
+    wave, 513 takes one level step first, ~1025 splits into halves at about the limit) and in the level
+    phase (70000)."""
     sc = _soup(n, seed=n)
     bh, ih = _tree(sc, HOST_B)
     bg, ig = _tree(sc, GPU_B)
