@@ -488,8 +488,10 @@ def main():
         elif part is not None:     # rehearsal: compact shard, gloo gather in Python
             r.render_device(0, part.data_ptr(), stream, **shard_opts(rank, world), compact_rows=1, **kw)
             st = r.stats()
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
             gather_frame(part, frame, rank, world, dist)
-            return st
+            return dict(st, gather_ms=(time.perf_counter() - tg) * 1e3)
         else:
             r.render_device(0, frame.data_ptr(), stream, **kw)
         return r.stats()
@@ -544,6 +546,14 @@ def main():
             rt = torch.tensor([rays], dtype=torch.float64, device=dev)
             dist.all_reduce(rt, op=dist.ReduceOp.SUM)
             rays = int(rt.item())
+            # every rank's shard time (its render minus its agreement + gather) of the last step
+            shard = float(st["render_ms"] - st.get("gather_ms", 0.0)) if st else 0.0
+            if comm is None and st is not None:
+                shard = float(st["render_ms"])          # rehearsal: render_ms is the shard alone
+            parts = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+            dist.all_gather(parts, torch.tensor([shard], dtype=torch.float64, device=dev))
+            if st is not None:
+                st = dict(st, shard_ms_per_rank=[round(float(x.item()), 3) for x in parts])
         return elapsed, rays, st
 
     elapsed, rays, st = timed(False)
@@ -569,6 +579,7 @@ def main():
                  "single_device_frame_ms": round(single_ms, 2), "row_block": ROW_BLOCK,
                  "gather_ms_rank0": round(st.get("gather_ms", 0.0), 3),
                  "gather_ms_max_over_ranks": round(st.get("gather_ms_max_over_ranks", 0.0), 3),
+                 "shard_ms_per_rank": st.get("shard_ms_per_rank"),
                  "gather_note": "per rank: librtg's failure agreement + RCCL rows gather after the rank's shard "
                                 "finished (rtg_render_stats.gather_ms), last timed step",
                  "timeout_s": args.timeout_s}

@@ -252,8 +252,8 @@ typedef struct rtg_render_opts {
     int32_t schedule;
     /* ABI 8 (these replace the environment knobs of earlier builds; 0 = the library default) */
     int32_t tile_band;       /* pixel order: bands this many 64-pixel tiles high, walked in columns of
-                                tiles (0 = 8 for the reference integrator, 16 for the path tracer
-                                and for row shards).  Results do not depend on it. */
+                                tiles (0 = 64 owned rows: 8 tiles of 8 rows, 16 of a row shard's 4;
+                                DESIGN.md §5).  Results do not depend on it. */
     int32_t segment_pixels;  /* stream schedule, path tracer: pixels whose samples' radiance is buffered
                                 per segment (0 = as many as an eighth of the device memory holds) */
     int32_t segment_nodes;   /* stream schedule, reference integrator: a segment takes no new samples

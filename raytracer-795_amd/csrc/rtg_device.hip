@@ -105,6 +105,14 @@ DEV float f_acos(float x) { return (float)acos((double)x); }
 DEV float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 DEV float f_cos(float x) { return (float)cos((double)x); }
 DEV float f_sin(float x) { return (float)sin((double)x); }
+// (float)cos((double)x) and (float)sin((double)x) with one argument reduction (ocml's sin, cos and
+// sincos share it; the path tracer's two uniform-angle samples per vertex)
+DEV void f_sincos(float x, float& s, float& c) {
+    double sd, cd;
+    sincos((double)x, &sd, &cd);
+    s = (float)sd;
+    c = (float)cd;
+}
 DEV float f_exp(float x) { return (float)exp((double)x); }
 // std::pow(float, int) == (float)pow(double, double).  Integer exponent by binary powering in
 // double: within ~log2(n) double ulps of the exact power, so the float result is the
@@ -399,12 +407,13 @@ DEV void visit_object(const SceneView& sv, const int i, const f3 o, const f3 d, 
     bool found = false;
     int bprim = -1;
     f3 bp = mk(0, 0, 0);
-    if (g.type == RTG_OBJ_SPHERE) {
-        if (g.nprims > 0) {
+    if (T.kind == 0) {            // a sphere: its test data by entry index (SphereEnt)
+        const SphereEnt& S = sv.tsph[i];
+        if (S.prim >= 0) {
             f3 ip;
-            if (sphere_test(o2, d2, ld3(g.center), g.radius, eps, ip)) {
+            if (sphere_test(o2, d2, mk(S.c.x, S.c.y, S.c.z), S.c.w, eps, ip)) {
                 float dist = norm(ip - o2);
-                if (dist < FLT_MAX) { found = true; bprim = g.prim_base; bp = ip; if (STATS) st.cand_step = st.steps; }
+                if (dist < FLT_MAX) { found = true; bprim = S.prim; bp = ip; if (STATS) st.cand_step = st.steps; }
             }
         }
     } else {
@@ -795,7 +804,7 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
             atomicAdd(ecyc + slot, __builtin_amdgcn_s_memtime() - t0);
     };
     f3 o2, d2;
-    transform_ray(sv.tops[sv.gents[0].entry], o, d, time, o2, d2, true);   // the members' common transform
+    transform_ray(*sv.gtop, o, d, time, o2, d2, true);   // the members' common transform
     const float adx = fabsf(d2.x), ady = fabsf(d2.y), adz = fabsf(d2.z);
     if (!(adx >= 1e-30f && adx <= 1e30f && ady >= 1e-30f && ady <= 1e30f && adz >= 1e-30f && adz <= 1e30f)) {
         charge(16, c0);
@@ -1536,7 +1545,9 @@ DEV void light_sample(const SceneView& sv, int li, f3 primeDir, float time, cons
             const float phi = (float)(2 * PI_D) * xi[1];
             const f3 dn = dd > 0.0f ? dv / dd : mk(0, 1, 0);
             const f3 u = ortho_u(dn), w = cross(dn, u);
-            dir = normalized((u * (sinT * f_cos(phi)) + w * (sinT * f_sin(phi))) + dn * cosT);
+            float sp, cp;
+            f_sincos(phi, sp, cp);
+            dir = normalized((u * (sinT * cp) + w * (sinT * sp)) + dn * cosT);
             const f3 oc = p - C;
             const float b = dot(dir, oc);
             const float disc = b * b - (sqn(oc) - Rw * Rw);
@@ -2293,7 +2304,9 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                         const float phi = (float)(2 * PI_D) * xi[0];
                         const float cosT = (flags & RTG_PT_IMPORTANCE) ? sqrtf(1.0f - xi[1]) : xi[1];
                         const float sinT = sqrtf(fmax0(1.0f - cosT * cosT));
-                        const f3 wi = normalized((u * (sinT * f_cos(phi)) + nn * cosT) + bt * (sinT * f_sin(phi)));
+                        float sp, cp;
+                        f_sincos(phi, sp, cp);
+                        const f3 wi = normalized((u * (sinT * cp) + nn * cosT) + bt * (sinT * sp));
                         const f3 fc = phong_or_brdf<BRDF>(mk(1, 1, 1), -d, wi, ret, m);
                         if (flags & RTG_PT_IMPORTANCE) w = cosT > 0.0f ? fc * ((float)PI_D / cosT) : mk(0, 0, 0);
                         else w = fc * (float)(2 * PI_D);

@@ -1162,7 +1162,7 @@ struct rtg_scene {
     SceneView sv{};
     DBuf d_tops, d_geoms, d_nodes, d_nodes4, d_tris, d_primidx, d_vertices, d_vnormals, d_texcoords, d_materials, d_textures,
         d_texels, d_lights, d_origprim, d_topemit, d_etris, d_ecdf, d_tlas, d_tlasidx, d_stris, d_gates, d_gtris,
-        d_gents;
+        d_gents, d_gtop, d_tsph;
     int num_gtris = 0, num_gents = 0;
     int blas_mode = 0;                       // rtg_build_opts.traversal_tree
     int tlas_mode = 0;                       // rtg_build_opts.tlas
@@ -1277,7 +1277,7 @@ static std::vector<DBuf*> scene_buffers(rtg_scene* s) {
     return {&s->d_tops, &s->d_geoms, &s->d_nodes, &s->d_nodes4, &s->d_tris, &s->d_primidx, &s->d_vertices,
             &s->d_vnormals, &s->d_texcoords, &s->d_materials, &s->d_textures, &s->d_texels, &s->d_lights,
             &s->d_origprim, &s->d_topemit, &s->d_etris, &s->d_ecdf, &s->d_tlas, &s->d_tlasidx, &s->d_stris, &s->d_gtris,
-            &s->d_gents,
+            &s->d_gents, &s->d_gtop, &s->d_tsph,
             &s->d_gates};
 }
 
@@ -1306,6 +1306,8 @@ static void bind_view(rtg_scene* s) {
     sv.tlas_idx = s->d_tlasidx.as<int>();
     sv.gtris = s->d_gtris.as<TriGeom>();
     sv.gents = s->d_gents.as<GroupEnt>();
+    sv.gtop = s->d_gtop.as<TopObject>();
+    sv.tsph = s->d_tsph.as<SphereEnt>();
 }
 
 static void scene_free(rtg_scene* s) {
@@ -1943,6 +1945,17 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         T.ident = ident ? 1 : 0;
     }
 
+    std::vector<SphereEnt> tsph(tops.size());
+    for (size_t i = 0; i < tops.size(); i++) {
+        SphereEnt& S = tsph[i];
+        memset(&S, 0, sizeof S);
+        S.prim = -1;
+        if (tops[i].kind == 0) {
+            const Geometry& g = geoms[tops[i].geom];
+            S.c = make_float4(g.center[0], g.center[1], g.center[2], g.radius);
+            S.prim = g.nprims > 0 ? g.prim_base : -1;
+        }
+    }
     // world boxes of the transformed entries: the object loop skips such an entry, before its ray
     // transform, for a lane whose ray line misses the box (closest_hit).  (Round 5 measured every entry
     // with a world box and, for axis-aligned ones, the top-level BVH's distance pruning -- behind the
@@ -2052,6 +2065,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     }
     s->num_gtris = (int)gtris.size();
     s->num_gents = (int)gents.size();
+    std::vector<TopObject> gtop;
+    if (!gents.empty()) gtop.push_back(tops[gents[0].entry]);
     bs.flat_group_entries = s->num_gents;
 
     // materials, textures, lights
@@ -2171,7 +2186,8 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         (rc = upload(s->d_lights, lights)) ||
         (rc = upload(s->d_topemit, top_emit)) || (rc = upload(s->d_etris, etris)) || (rc = upload(s->d_ecdf, ecdf)) ||
         (rc = upload(s->d_tlas, tlas_nodes)) || (rc = upload(s->d_tlasidx, tlas_idx)) ||
-        (rc = upload(s->d_gtris, gtris)) || (rc = upload(s->d_gents, gents)))
+        (rc = upload(s->d_gtris, gtris)) || (rc = upload(s->d_gents, gents)) || (rc = upload(s->d_gtop, gtop)) ||
+        (rc = upload(s->d_tsph, tsph)))
         return rc;
     bs.upload_bytes = 0;
     for (DBuf* b : scene_buffers(s)) bs.upload_bytes += b->used;
@@ -2342,6 +2358,9 @@ int32_t rtg_scene_create_ex(const rtg_scene_desc* desc, int32_t device, const rt
 }
 
 // Camera::Camera (src/Camera.cpp:7-61)
+// Pixel-order band height in owned rows (tile_pixel): the default tile_band is kBandRows / tile height.
+constexpr int kBandRows = 64;
+
 static CameraDev make_camera(const rtg_camera_desc* c) {
     CameraDev k;
     memset(&k, 0, sizeof k);
@@ -2466,11 +2485,13 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     // row strips, so each holds a mix of sky, floor and glass).  4 / 8 / 32 / 64 tiles: in between.
     if (o.tile_band < 0 || o.segment_pixels < 0 || o.segment_nodes < 0)
         return fail(RTG_ERR_INVALID, "tile_band / segment_pixels / segment_nodes");
-    // Round 5 (`profiles/r6_ab_schedule_sweep.jsonl`, `r6_ab_tile_band8.jsonl`, same box, interleaved): bands
-    // of 8 tiles for the reference integrator -- dragon 30.16-30.47 -> 29.91-30.10 ms over four pairs,
-    // cornell_dynamic 14.92-15.18 -> 14.85-15.12 ms; the path tracer (stream schedule) and row shards
-    // keep 16 (`profiles/r6_shard_band.txt`: 1/8 dragon shard 5.39 ms with 8, 4.40 with 16).
-    int tile_s = o.tile_band > 0 ? std::min(o.tile_band, 1 << 12) : (pt || stride > 1 ? 16 : 8);
+    // Band height (round 6): kBandRows owned rows, whatever the tile height -- bands of
+    // 8 tiles for the full frame's 8-row tiles and 16 for a row shard's 4-row tiles, which are the optima
+    // round 5 found by sweeping each case separately (`profiles/history/r6_ab_schedule_sweep.jsonl`,
+    // `r6_shard_band.txt`: 1/8 dragon shard 5.39 ms with 32-row bands, 4.40 with 64); one rule instead of
+    // a special case for shards (its measurements per N: profiles/r7/shard_probe*.txt).
+    const int tile_h = stride > 1 && block < 8 ? (block >= 4 ? 4 : block >= 2 ? 2 : 1) : 8;
+    int tile_s = o.tile_band > 0 ? std::min(o.tile_band, 1 << 12) : std::max(1, kBandRows / tile_h);
     // tile_pixel (device) forms band * (tile_h * tile_s * nx) in 32-bit ints: keep one band of the
     // widest tiles (tile_h <= 8) below 2^31 pixels
     if ((long long)8 * cam->nx >= (1LL << 31)) return fail(RTG_ERR_UNSUPPORTED, "image wider than 2^28 pixels");
@@ -2482,7 +2503,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
             ps.s0 = s0; ps.ns = std::min(ns_chunk, total - s0);
             ps.p0 = p0; ps.npass = std::min(np_pass, npix - p0);
             ps.row_offset = off; ps.row_stride = stride; ps.rows_owned = rows_owned; ps.row_block = block;
-            ps.tile_h = stride > 1 && block < 8 ? (block >= 4 ? 4 : block >= 2 ? 2 : 1) : 8;
+            ps.tile_h = tile_h;
             ps.tile_s = tile_s;
             plist.push_back(ps);
         }
@@ -2717,7 +2738,7 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
         PassDev F;
         F.s0 = 0; F.ns = total; F.p0 = 0; F.npass = npix;
         F.row_offset = off; F.row_stride = stride; F.rows_owned = rows_owned; F.row_block = block;
-        F.tile_h = stride > 1 && block < 8 ? (block >= 4 ? 4 : block >= 2 ? 2 : 1) : 8;
+        F.tile_h = tile_h;
         F.tile_s = tile_s;
         long long cursor = 0, seg_end = 0, seg_slots = 0;
         double seg_node_bytes = 0.0;

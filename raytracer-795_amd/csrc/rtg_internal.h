@@ -44,6 +44,13 @@ struct TopObject {
     float wlo[3], whi[3];   // through the model matrix, blur sweep for times in [0, 1], margins)
     int grouped;            // a member of the flat group (SceneView::gents): fast rays test it there
 };
+// A sphere entry's test data (SceneView::tsph, one per entry, round 6): the object loop tests a sphere
+// from this 32-byte record, whose address depends only on the entry index -- not on a dependent load
+// of its Geometry record through TopObject::geom.  c = centre, radius; prim = its primitive, -1 none.
+struct SphereEnt {
+    float4 c;
+    int prim, pad_[3];
+};
 
 // The flat group (round 5, closest_hit): the identity-transform entries whose mesh is tested without a
 // node -- a root leaf, a reference root over two leaves, or a one-node traversal tree (<= kFlatMaxPrims
@@ -214,6 +221,9 @@ struct SceneView {
     // the flat group (GroupEnt); num_gents 0: none (top-level BVH scenes never group)
     const TriGeom* gtris;
     const GroupEnt* gents;
+    const SphereEnt* tsph;         // per top-level entry: sphere test data (SphereEnt)
+    const TopObject* gtop;         // a copy of the first member's entry: the members' common transform, one
+                                   // load away (not gents[0].entry -> tops[], round 6)
     int num_gtris, num_gents;
 };
 
