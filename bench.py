@@ -580,8 +580,13 @@ def main():
                  "gather_ms_rank0": round(st.get("gather_ms", 0.0), 3),
                  "gather_ms_max_over_ranks": round(st.get("gather_ms_max_over_ranks", 0.0), 3),
                  "shard_ms_per_rank": st.get("shard_ms_per_rank"),
-                 "gather_note": "per rank: librtg's failure agreement + RCCL rows gather after the rank's shard "
-                                "finished (rtg_render_stats.gather_ms), last timed step",
+                 "gather_note": ("per rank: the Python gloo gather of the compact rows after the rank's shard "
+                                 "(host memory), last timed step" if rehearse else
+                                 "per rank: librtg's failure agreement + RCCL rows gather after the rank's shard "
+                                 "finished (rtg_render_stats.gather_ms), last timed step"),
+                 "shard_note": "shard_ms_per_rank: each rank's own shard render of the last timed step"
+                               + (" -- all ranks share one GPU in a rehearsal, so each shard takes about the "
+                                  "whole GPU's frame time" if rehearse else ""),
                  "timeout_s": args.timeout_s}
         if rehearse and not same:
             raise SystemExit("rehearsal: gathered frame differs from the single-device frame")

@@ -832,7 +832,10 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
     for (int e = 0; e < sv.num_gents; e++) {
         const GroupEnt& G = sv.gents[e];
         // the entry's root box widened by the eps overhang against the parameter window (visit_object):
-        // a coherent wave (a pixel's samples) skips the walls it does not face
+        // a coherent wave (a pixel's samples) skips the walls it does not face.  (Round 6 measured a
+        // per-lane loop over each lane's own members here: the triangle records then come as per-lane
+        // gathers instead of scalar loads -- cornell_pt k_shadow 99.5 -> 108 ms,
+        // profiles/r7/ab_group_perlane.jsonl.)
         const bool need = !G.win || window_meets(o2, inv, G.win_min[0], G.win_min[1], G.win_min[2], G.win_max[0],
                                                  G.win_max[1], G.win_max[2], tlo, thi1);
         if (__ballot(need) == 0ull) continue;
@@ -840,20 +843,15 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
         for (int j = G.first; j < G.first + G.count; j++)
             if (need && tri_maybe(sv.gtris[j], o2, d2, eps, thi1)) cand |= 1u << j;
     }
-    for (int e = 0; e < sv.num_gents; e++) {
-        const GroupEnt& G = sv.gents[e];
-        unsigned m = (cand >> G.first) & ((1u << G.count) - 1u);
-        if (__ballot(m != 0u) == 0ull) continue;
-        if (STATS) {        // the exact tests: each lane its own candidates, the wave the most any lane has
-            unsigned k = __popc(m), wm = k;
-            for (int off = 32; off > 0; off >>= 1) wm = max(wm, (unsigned)__shfl_xor((int)wm, off));
-            st.gslot += wm;
-            st.gwork += k;
-        }
-        if (m == 0u) continue;
+    // each member with candidates: its reference root test (box_hit, exact), the lane's own candidates
+    // through the exact test in index order with the window shrinking, the gate, and the top-level
+    // acceptance.  Members are visited in index order per lane, so a lane's sequence of member visits is
+    // the same whether the wave walks the members uniformly (every lane the same members: scalar record
+    // loads) or each lane its own (round 6: a mixed wave issues the most members one lane needs).
+    auto member = [&](const GroupEnt& G, unsigned m) {
         if (G.root_box && !box_hit(o2, d2, inv, true, G.root_min[0], G.root_min[1], G.root_min[2], G.root_max[0],
                                    G.root_max[1], G.root_max[2]))
-            continue;
+            return;
         const float thi0 = window();
         float thi = thi0, best_d = FLT_MAX;
         int best_leaf = -1, bprim = -1;
@@ -884,6 +882,43 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
                 nearest = t;
                 out.obj = i; out.prim = bprim; out.t = t;
             }
+        }
+    };
+    unsigned cm = 0;                                  // members holding candidates of this lane
+    for (int e = 0; e < sv.num_gents; e++) {
+        const GroupEnt& G = sv.gents[e];
+        if ((cand >> G.first) & ((1u << G.count) - 1u)) cm |= 1u << e;
+    }
+    // the wave's union of members (ballots: active lanes only -- the group runs for finite rays) and
+    // whether every lane has fewer: only then does the per-lane walk visit fewer members than the union
+    // (a one-member group, the dragon's floor, never takes it)
+    unsigned un = 0;
+    for (int e = 0; e < sv.num_gents; e++)
+        if (__ballot((cm >> e) & 1u)) un |= 1u << e;
+    const int pu = __popc(un);
+    const bool perlane = pu > 1 && __ballot(__popc(cm) >= pu) == 0ull;
+    if (STATS) {        // the exact tests: each lane its own candidates, the wave the most any lane has
+        unsigned k = __popc(cand), wm = k;
+        for (int off = 32; off > 0; off >>= 1) wm = max(wm, (unsigned)__shfl_xor((int)wm, off));
+        st.gslot += wm;
+        st.gwork += k;
+    }
+    if (!perlane) {
+        unsigned mm = un;                           // every lane skips the members it has no candidate in
+        while (mm) {
+            const int e = __builtin_ctz(mm);
+            mm &= mm - 1u;
+            const GroupEnt& G = sv.gents[e];
+            const unsigned m = (cand >> G.first) & ((1u << G.count) - 1u);
+            if (m) member(G, m);
+        }
+    } else {
+        unsigned mm = cm;
+        while (mm) {
+            const int e = __builtin_ctz(mm);
+            mm &= mm - 1u;
+            const GroupEnt& G = sv.gents[e];
+            member(G, (cand >> G.first) & ((1u << G.count) - 1u));
         }
     }
     charge(17, c1);
@@ -1611,10 +1646,12 @@ DEV float shadow_mode(const SceneView& sv, int li) {
 }
 // k_shadow's t bound of a traced query (what light_sample formed before round 6, bit for bit):
 // p = the node's hit point (mode 3 only), dl from the direction plane's w.
+// EMIT: object-light queries (mode 3) can occur -- the path tracer's instantiations only.
+template <bool EMIT>
 DEV float shadow_query_tmax(float mode, f3 origin, f3 p, f3 d, float dl, float eps) {
     if (mode == 2.0f) return FLT_MAX;
     float tmax = shadow_tmax_dl(origin, dl, eps);
-    if (mode == 3.0f) tmax = fminf(tmax, emit_shadow_tmax(origin, p, dl, d, eps));
+    if (EMIT && mode == 3.0f) tmax = fminf(tmax, emit_shadow_tmax(origin, p, dl, d, eps));
     return tmax;
 }
 
@@ -1624,24 +1661,29 @@ DEV float shadow_query_tmax(float mode, f3 origin, f3 p, f3 d, float dl, float e
 // ts tiles' height over the owned rows, each band in columns of tiles, a column's tiles top to
 // bottom (edge columns / tiles narrower or lower).  A kernel's in-flight rays are a window of
 // consecutive t; ts > 1 makes that window squarer than a one-tile-high strip.
+// n / d for n >= 0, d > 0: a shift when d is a power of two (round 6: the pixel order's divisors --
+// tile width, 64-pixel tiles, full-band columns, the samples per pixel of the bench configs -- are
+// powers of two except at the image's last band / column; a 32-bit division is ~30 VALU instructions,
+// and slot_pixel runs for every ray of every shading kernel)
+DEV int idiv(int n, int d) { return (d & (d - 1)) == 0 ? (n >> __builtin_ctz((unsigned)d)) : n / d; }
 DEV void tile_pixel(int t, int nx, int rows_owned, int th, int ts, int& x, int& k) {
-    const int tw = 64 / th;
+    const int tw = 64 >> __builtin_ctz((unsigned)th);   // th is 1, 2, 4 or 8
     const int sh = th * ts;                          // band height (rows)
-    const int band = t / (sh * nx);
+    const int band = idiv(t, sh * nx);
     const int u = t - band * sh * nx;
     const int hs = min(sh, rows_owned - sh * band);  // rows in this band
-    const int c = u / (tw * hs);                     // tile column
+    const int c = idiv(u, tw * hs);                  // tile column
     const int u2 = u - c * tw * hs;
     const int wb = min(tw, nx - tw * c);
-    const int rt = u2 / (wb * th);                   // tile in the column
+    const int rt = idiv(u2, wb * th);                // tile in the column
     const int u3 = u2 - rt * wb * th;
-    const int r = u3 / wb;
+    const int r = idiv(u3, wb);
     x = tw * c + (u3 - r * wb);
     k = sh * band + th * rt + r;
 }
 DEV void slot_pixel(const CameraDev& cam, const PassDev& ps, int slot, uint32_t& pixel, uint32_t& sample, int& x,
                     int& y) {
-    const int pl = slot / ps.ns, sl = slot - pl * ps.ns;
+    const int pl = idiv(slot, ps.ns), sl = slot - pl * ps.ns;
     int k;
     tile_pixel(ps.p0 + pl, cam.nx, ps.rows_owned, ps.tile_h, ps.tile_s, x, k);
     y = shard_row(k, ps.row_offset, ps.row_stride, ps.row_block);
@@ -2483,13 +2525,15 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             // point only for an object light's bound)
             const float4 sd = shadows.d[idx];
             d = mk(sd.x, sd.y, sd.z);
+            // (object lights, mode 3, exist only for the path tracer: the Whitted instantiations leave
+            // their bound out, which is their register peak's business)
             const float qm = shadow_mode(sv, li);
             f3 p = mk(0, 0, 0);
-            if (qm == 3.0f) {
+            if (PT && qm == 3.0f) {
                 const float4 pf = nodes.pnt[i];
                 p = mk(pf.x, pf.y, pf.z);
             }
-            tmax = shadow_query_tmax(qm, o, p, d, sd.w, sv.shadow_eps);
+            tmax = shadow_query_tmax<PT>(qm, o, p, d, sd.w, sv.shadow_eps);
         }
         if (isnan3(o) || isnan3(d)) nanq++;     // not a traced ray (the host subtracts these)
         auto ld = [&](const float* a) { return __builtin_nontemporal_load(a); };
@@ -2531,7 +2575,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                     dl = ld(qd + 3);
                 }
                 f3 hp = o_ + d_ * h.t;
-                if (mode == 1.0f) {             // PointLight::IsShadow: |p - L| > |p - hit|
+                if (!PT || mode == 1.0f) {      // PointLight::IsShadow: |p - L| > |p - hit|
                     blocked = dl > norm(p_ - hp);
                 } else {   // object light (hw7, Page7.md:143-147): an occluder nearer than the sample
                     blocked = norm(p_ - hp) < dl - (sv.shadow_eps + 1e-4f * dl);
