@@ -1661,11 +1661,7 @@ DEV float shadow_query_tmax(float mode, f3 origin, f3 p, f3 d, float dl, float e
 // ts tiles' height over the owned rows, each band in columns of tiles, a column's tiles top to
 // bottom (edge columns / tiles narrower or lower).  A kernel's in-flight rays are a window of
 // consecutive t; ts > 1 makes that window squarer than a one-tile-high strip.
-// n / d for n >= 0, d > 0: a shift when d is a power of two (round 6: the pixel order's divisors --
-// tile width, 64-pixel tiles, full-band columns, the samples per pixel of the bench configs -- are
-// powers of two except at the image's last band / column; a 32-bit division is ~30 VALU instructions,
-// and slot_pixel runs for every ray of every shading kernel)
-DEV int idiv(int n, int d) { return (d & (d - 1)) == 0 ? (n >> __builtin_ctz((unsigned)d)) : n / d; }
+// (idiv: rtg_internal.h)
 DEV void tile_pixel(int t, int nx, int rows_owned, int th, int ts, int& x, int& k) {
     const int tw = 64 >> __builtin_ctz((unsigned)th);   // th is 1, 2, 4 or 8
     const int sh = th * ts;                          // band height (rows)
@@ -1728,7 +1724,7 @@ DEV void primary_ray(const CameraDev& cam, const PassDev& ps, uint64_t seed, int
         float xi[4];
         rng4(seed, pixel, sample, 1, RNG_CAMERA, 0, 0, xi);
         int si = (int)sample;
-        int ii = si % cam.sample_count, jj = si / cam.sample_count;
+        const int jj = idiv(si, cam.sample_count), ii = si - jj * cam.sample_count;
         m = m + right * (((float)ii + xi[0]) * cam.sw);
         m = m + up * (((float)jj + xi[1]) * cam.sh);
         f3 dv = m - pos;
@@ -2493,8 +2489,9 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
     bool was_blocked = false;
     if (j < (int)*scount) {
         // list entry li * nn + i (ShadowPlanes: light-major); one light: the node index itself
+        // (the path tracer's launches are per light: no division)
         const int idx = slist[j];
-        const int li = sv.num_lights == 1 ? 0 : (int)((unsigned)idx / (unsigned)shadows.nn);
+        const int li = PT ? pr.light : sv.num_lights == 1 ? 0 : (int)((unsigned)idx / (unsigned)shadows.nn);
         const int i = idx - li * shadows.nn;    // shading node of the query
         // lean3: one point / spot / directional light and no motion blur -- 12-byte origin and
         // lit-colour planes (k_shade), time 0, the mode follows from the light type
@@ -2845,7 +2842,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const SceneView sv,
         const int cs = min(kAccChunk, ps.ns - s0);
         __syncthreads();
         for (int e = t; e < np * cs; e += blockDim.x) {
-            const int q = e / cs, s = e - q * cs;
+            const int q = idiv(e, cs), s = e - q * cs;
             const size_t slot = (size_t)(p0 + q) * ps.ns + s0 + s;
             f3 c;
             const float4 nc = level0.col[slot];
@@ -3014,11 +3011,13 @@ void launch_pt_shadow(const SceneView& sv, ShadowRec* shadows, const int* slist,
     for (int li = 0; li < sv.num_lights; li++) {
         const int* sl = slist + (size_t)li * n;
         const unsigned* sc = pr.lcnt + li;
-        if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
-        else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
-        else if (ctr) hipLaunchKernelGGL((k_shadow<false, true, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
-        else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
-        else hipLaunchKernelGGL((k_shadow<false, false, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, pr);
+        PtRad prl = pr;
+        prl.light = li;
+        if (exhaustive) hipLaunchKernelGGL((k_shadow<true, false, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, prl);
+        else if (ctr && tl) hipLaunchKernelGGL((k_shadow<false, true, true, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, prl);
+        else if (ctr) hipLaunchKernelGGL((k_shadow<false, true, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, prl);
+        else if (tl) hipLaunchKernelGGL((k_shadow<false, false, true, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, prl);
+        else hipLaunchKernelGGL((k_shadow<false, false, false, true>), g, b, 0, st, sv, sp, false, sl, sc, np, nan_queries, ctr, uni_from, prl);
     }
 }
 void launch_pt_shade(const SceneView& sv, const CameraDev& cam, int level, const PassDev& ps, uint64_t seed,

@@ -243,16 +243,24 @@ struct PassDev {
     int tile_s;        // tiles per column of a band (the band is tile_s * tile_h rows high)
 };
 
+// n / d for n >= 0, d > 0: a shift when d is a power of two (round 6: the pixel order's and the shards'
+// divisors -- tile widths, 64-pixel tiles, full-band columns, samples per pixel, row blocks of 1 or 4,
+// one shard -- are powers of two except at the image's last band / column; a 32-bit division is ~30
+// VALU instructions, and the slot -> pixel map runs for every ray of every shading kernel)
+__host__ __device__ inline int idiv(int n, int d) {
+    return (d & (d - 1)) == 0 ? (n >> __builtin_ctz((unsigned)d)) : n / d;
+}
 // Shard row ownership (rtg_render_opts.row_block): owned row k <-> image row y.
 __host__ __device__ inline int shard_row(int k, int off, int stride, int block) {
-    const int b = k / block;
+    const int b = idiv(k, block);
     return (b * stride + off) * block + (k - b * block);
 }
 // owned index of image row y, or -1 when another shard owns it
 __host__ __device__ inline int shard_owned_index(int y, int off, int stride, int block) {
-    const int b = y / block;
-    if (b % stride != off) return -1;
-    return (b / stride) * block + (y - b * block);
+    const int b = idiv(y, block);
+    const int q = idiv(b, stride);
+    if (b - q * stride != off) return -1;
+    return q * block + (y - b * block);
 }
 
 struct CameraDev {
@@ -408,6 +416,7 @@ struct PtRad {
     float4* carry_out;
     float4* rad;
     unsigned* lcnt;
+    int light;          // k_shadow: the light of this launch's list (its entries are light * n + node)
 };
 constexpr size_t kCarryBytes = 16;    // float4 per queued ray
 
