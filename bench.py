@@ -15,7 +15,7 @@ Prints ONE JSON line (rank 0).  Extra objects:
                issue (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, one wave64 VALU instruction per 2
                cycles at 2.4 GHz = 1228.8 G wave-instructions/s), from the committed PMC counters
                (profiles/counters_<workload>.json: SQ_INSTS_VALU per launch) divided by the live
-               HIP-event launch time; `kernels` holds the same for k_shadow, k_shade, k_resolve (k_pt_gather) and
+               HIP-event launch time; `kernels` holds the same for k_shadow, k_shade (k_pt_shade), k_resolve2 (Whitted) and
                k_accumulate plus each kernel's measured HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE)
                against 8 TB/s, and the traversal kernels' SIMD lane efficiency (node steps / lane
                slots of a collect_stats frame) with the lane-adjusted VALU fraction; `model` holds
@@ -248,10 +248,11 @@ def kernel_table(counters, st_roof, st_stats, pt: bool) -> dict:
     rows = [("k_trace", "rtg::k_trace<false, false, *>", "trace"),
             ("k_shadow", first("rtg::k_shadow<false, false"), "shadow"),
             ("k_pt_shade" if pt else "k_shade", shade, "shade"),
-            ("k_accumulate", "rtg::k_accumulate", "accumulate")]
-    # the bottom-up pass: k_resolve (Whitted), or the path tracer's per-level k_pt_gather (timed in the
-    # library's resolve slot)
-    rows.append(("k_pt_gather", "rtg::k_pt_gather", "resolve") if pt else ("k_resolve", "rtg::k_resolve", "resolve"))
+            ("k_accumulate", first("rtg::k_accumulate<"), "accumulate")]
+    # the bottom-up pass (Whitted only): k_resolve2 resolves two levels per launch (round 5); the path
+    # tracer has no bottom-up pass since round 6 (radiance rides with the path, k_pt_gather is gone)
+    if not pt:
+        rows.append(("k_resolve2", first("rtg::k_resolve2"), "resolve"))
     out = {}
     for key, name, slot in rows:
         n = st_roof.get(f"{slot}_launches", 0)

@@ -898,8 +898,11 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
     const int pu = __popc(un);
     const bool perlane = pu > 1 && __ballot(__popc(cm) >= pu) == 0ull;
     if (STATS) {        // the exact tests: each lane its own candidates, the wave the most any lane has
-        unsigned k = __popc(cand), wm = k;
-        for (int off = 32; off > 0; off >>= 1) wm = max(wm, (unsigned)__shfl_xor((int)wm, off));
+        // (a max over the active lanes only -- lanes of non-finite rays are not in here -- by ballots)
+        const unsigned k = __popc(cand);
+        unsigned wm = 0;
+        for (int bit = 5; bit >= 0; bit--)
+            if (__ballot(k >= (wm | (1u << bit)))) wm |= 1u << bit;
         st.gslot += wm;
         st.gwork += k;
     }

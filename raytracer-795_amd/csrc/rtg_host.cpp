@@ -1093,7 +1093,7 @@ int upload(DBuf& b, const V& v) {
 
 struct Level {
     DBuf rays, meta, hits, nodes, shadows, slist, paths;
-    DBuf carry;                // path tracer: each queued ray's running radiance (16 B, k_pt_gather)
+    DBuf carry;                // path tracer: each queued ray's running radiance (16 B; k_pt_shade reads it)
     DBuf lv;                   // stream schedule: the queued rays' levels (1 byte each)
     long long rcap = 0;        // plane stride of `rays` (RayQ) as the previous level wrote them
     void release() {
@@ -2683,7 +2683,8 @@ static int render_impl(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rende
     // path record too) -- followed by new camera samples from the frame's slot cursor.  A lane runs
     // a sample's ray tree in consecutive steps of one stream, so every per-sample sum keeps its
     // order and the frame is bit-identical to the pass schedule (and to the oracle):
-    //  * path tracer: k_pt_gather adds each vertex to the sample's radiance in level order; the
+    //  * path tracer: each queued ray carries its sample's running radiance (PtRad); k_pt_shade
+    //    and the per-light k_shadow launches add each vertex's terms in level order, and the
     //    radiance of a segment of pixels lives in one buffer (16 B per slot, segments sized to an
     //    eighth of the device memory) and is summed per pixel in sample order (MultiSample,
     //    src/Scene.cpp:386-411) once the segment's paths have ended;

@@ -1,7 +1,7 @@
 """GPU parity of the hw7 path tracer (pages/Page7.md; no reference code exists, so the CPU
 restatement in oracle/rtg_oracle.c pt_sample() is the specification).
 
-The GPU wavefront (k_pt_shade / k_shadow / k_pt_gather) must reproduce the oracle's paths on
+The GPU wavefront (k_pt_shade / k_shadow, radiance carried with each path) must reproduce the oracle's paths on
 the same Philox stream: same image within the north_star bar (L-inf < 1e-3 on the float
 framebuffer) and the same number of traced rays, for every combination of the hw7 renderer
 parameters (uniform / importance sampling, next event estimation, Russian roulette).
