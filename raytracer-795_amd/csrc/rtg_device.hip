@@ -2444,9 +2444,10 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
             if (nd.kind & kContrib) L = L + cw(Tg, mk(nd.cr, nd.cg, nd.cb));
             *tgt = make_float4(L.x, L.y, L.z, 0.0f);
         } else {
-            // traced queries: k_shadow adds the lit lights to the colour and the last one T (x) v to
-            // the target, which holds L until then.  pnt.w: that last light's index.
-            *tgt = make_float4(Lrun.x, Lrun.y, Lrun.z, 0.0f);
+            // traced queries: k_shadow adds the lit lights to the colour and the last one writes
+            // L + T (x) v to the target; L waits in this ray's own queue slot (its carry was read
+            // above).  pnt.w: that last light's index.
+            pr.carry_in[i] = make_float4(Lrun.x, Lrun.y, Lrun.z, 0.0f);
             nodes.col[i] = make_float4(nd.cr, nd.cg, nd.cb, __int_as_float(nd.kind));
             nodes.pnt[i] = make_float4(nd.px, nd.py, nd.pz, __int_as_float(63 - __clzll((long long)smask)));
             nodes.link[i] = make_int4(__float_as_int(Tg.x), __float_as_int(Tg.y), __float_as_int(Tg.z),
@@ -2546,6 +2547,23 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                                                              s_stack + threadIdx.x, kTraceBlock, st,
                                                              s_tstack + (TLAS ? threadIdx.x : 0), uni,
                                                              STATS ? s_ecyc : nullptr);
+        // PT: the tail's records in one round of loads after the traversal (the node's point + last
+        // light, colour, the query's origin / direction / lit colour; in the last light's launch the
+        // throughput + target and L too): one memory latency instead of three dependent ones
+        const bool pt_last = PT && pr.light == sv.num_lights - 1;
+        float4 t_o, t_d, t_pnt, t_col, t_c, t_lr;
+        int4 t_lk;
+        if constexpr (PT) {
+            t_o = shadows.o[i];
+            t_d = shadows.d[idx];
+            t_pnt = nodes.pnt[i];
+            t_col = nodes.col[i];
+            t_c = shadows.c[idx];
+            if (pt_last) {
+                t_lk = nodes.link[i];
+                t_lr = pr.carry_in[i];
+            }
+        }
         // the query's mode from its light's type (shadow_mode), not a stored record
         const float mode = lean3 ? (sv.lights[0].type == RTG_LIGHT_DIRECTIONAL ? 2.0f : 1.0f) : shadow_mode(sv, li);
         bool blocked;
@@ -2554,7 +2572,9 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
             if (h.obj >= 0) {
                 // re-read (not kept live across the traversal: register pressure)
                 f3 o_;
-                if (lean3) {
+                if (PT) {
+                    o_ = mk(t_o.x, t_o.y, t_o.z);
+                } else if (lean3) {
                     const float* qo = reinterpret_cast<const float*>(shadows.o) + 3 * (size_t)i;
                     o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
                 } else {
@@ -2562,10 +2582,13 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
                     o_ = mk(ld(qo), ld(qo + 1), ld(qo + 2));
                 }
                 const float* pp = reinterpret_cast<const float*>(nodes.pnt + i);
-                const f3 p_ = mk(ld(pp), ld(pp + 1), ld(pp + 2));
+                const f3 p_ = PT ? mk(t_pnt.x, t_pnt.y, t_pnt.z) : mk(ld(pp), ld(pp + 1), ld(pp + 2));
                 f3 d_;
                 float dl;                       // |p - L|
-                if (lean) {     // mode 1 with one light: a point / spot light
+                if (PT) {
+                    d_ = mk(t_d.x, t_d.y, t_d.z);
+                    dl = t_d.w;
+                } else if (lean) {     // mode 1 with one light: a point / spot light
                     const f3 l_ = ld3(sv.lights[0].pos);
                     d_ = toward(l_, p_);
                     dl = norm(p_ - l_);
@@ -2597,20 +2620,21 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         if constexpr (PT) {
             // lights in order (this launch is light li's): col = ((amb + L0) + L1) + ..., a blocked or
             // untraced light's term is +0 and leaves the colour unchanged (it is never -0: amb = 0 + La ka)
-            float* cp = reinterpret_cast<float*>(nodes.col + i);
-            f3 v = mk(cp[0], cp[1], cp[2]);
-            if (!blocked) {
-                const float* scp = reinterpret_cast<const float*>(shadows.c + idx);
-                v = v + mk(scp[0], scp[1], scp[2]);
-            }
-            if (li != __float_as_int(nodes.pnt[i].w)) {
-                if (!blocked) { cp[0] = v.x; cp[1] = v.y; cp[2] = v.z; }
+            f3 v = mk(t_col.x, t_col.y, t_col.z);
+            if (!blocked) v = v + mk(t_c.x, t_c.y, t_c.z);
+            if (!pt_last && li != __float_as_int(t_pnt.w)) {
+                if (!blocked) {
+                    float* cp = reinterpret_cast<float*>(nodes.col + i);
+                    cp[0] = v.x; cp[1] = v.y; cp[2] = v.z;
+                }
             } else {            // the node's last traced light: L + T (x) v (pt_sample's running sum)
-                const int4 lk = nodes.link[i];
-                float4* tp = lk.w >= 0 ? pr.carry_out + lk.w : pr.rad + ~lk.w;
-                const float4 z = *tp;
-                const f3 L = mk(z.x, z.y, z.z) +
-                             cw(mk(__int_as_float(lk.x), __int_as_float(lk.y), __int_as_float(lk.z)), v);
+                if (!pt_last) {
+                    t_lk = nodes.link[i];
+                    t_lr = pr.carry_in[i];
+                }
+                float4* tp = t_lk.w >= 0 ? pr.carry_out + t_lk.w : pr.rad + ~t_lk.w;
+                const f3 L = mk(t_lr.x, t_lr.y, t_lr.z) +
+                             cw(mk(__int_as_float(t_lk.x), __int_as_float(t_lk.y), __int_as_float(t_lk.z)), v);
                 *tp = make_float4(L.x, L.y, L.z, 0.0f);
             }
         } else if (lean3) {

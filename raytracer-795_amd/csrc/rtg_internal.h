@@ -408,11 +408,14 @@ struct Counters {
 // path.  k_pt_shade reads it from the ray's queue slot (carry_in[i]; a new sample starts from (0,0,0)).
 // A vertex whose contribution is final there (no traced shadow query) adds T (x) v itself and hands L
 // to its continuation (carry_out at the child's queue index) or, the path's last vertex, writes
-// rad[slot]; a vertex with traced queries leaves L in that target and its last light's query in
-// k_shadow (per-light launches, in light order) adds T (x) v.  No per-level gather kernel.
-// lcnt: the level's per-light shadow-list counts (the list of light li at slist + li * n).
+// rad[slot]; a vertex with traced queries leaves L in its own queue slot (carry_in[i], read by then)
+// and its last light's query in k_shadow (per-light launches, in light order) writes L + T (x) v to the
+// target -- node-indexed, so k_shadow loads it with the node's other records in one round, and the
+// last light's launch (every query in it is its node's last) loads all of them unconditionally.  No
+// per-level gather kernel.  lcnt: the level's per-light shadow-list counts (light li's list at
+// slist + li * n).
 struct PtRad {
-    const float4* carry_in;
+    float4* carry_in;
     float4* carry_out;
     float4* rad;
     unsigned* lcnt;
