@@ -2325,11 +2325,20 @@ __global__ void __launch_bounds__(kPtBlock) RTG_PT_SHADE_ATTR k_pt_shade(const S
                         ShadowRec sr;
                         light_sample<FULL, SPOT, BRDF>(sv, li, d, time, ret, m, seed, pixel, sample, path, sr);
                         const size_t k = (size_t)li * shadows.nn + i;   // light-major (ShadowPlanes)
-                        if (li == 0) shadows.o[i] = sr.o;       // per node (k_shade's layout)
-                        shadows.c[k] = sr.c;
-                        if (sr.c.w != 0.0f) shadows.d[k] = sr.d;
-                        if (sr.c.w != 0.0f) smask |= 1ull << li;
-                        else if (sv.num_lights == 1) { nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f; }
+                        // only traced queries' records: k_shadow reads nothing else (no light sum)
+                        if (sr.c.w != 0.0f) {
+                            shadows.c[k] = sr.c;
+                            shadows.d[k] = sr.d;
+                            smask |= 1ull << li;
+                        } else if (sv.num_lights == 1) {
+                            nd.cr = nd.cr + 0.0f; nd.cg = nd.cg + 0.0f; nd.cb = nd.cb + 0.0f;
+                        }
+                    }
+                    // the query origin, per node (k_shade's layout; light_sample's origin is the same
+                    // for every light), only when a query is traced
+                    if (smask) {
+                        const f3 og = ret.point + ret.normal * sv.shadow_eps;
+                        shadows.o[i] = make_float4(og.x, og.y, og.z, time);
                     }
                 }
                 charge(1, t_nee);

@@ -1942,6 +1942,18 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             float z = 0.0f;
             ident = ident && memcmp(&T.blur[k], &z, 4) == 0;
         }
+        // A sphere whose inverse is the identity up to the signs of its zeros (compared by value) and
+        // whose blur is zero -- an untransformed sphere: glm's inverse leaves -0 entries -- takes the
+        // same fast path: for a finite ray the transformed ray equals o + 0, d + 0 in value, and the
+        // sphere test, its point and gett() give the same values (signed zeros aside, on which no
+        // outcome depends: the test compares, t > 0 is required), so the hit record is the same.
+        if (!ident && T.kind == 0) {
+            bool unit = true;
+            for (int c = 0; c < 4; c++)
+                for (int r = 0; r < 3; r++) unit = unit && T.inv[c * 4 + r] == (c == r ? 1.0f : 0.0f);
+            for (int k = 0; k < 3; k++) unit = unit && T.blur[k] == 0.0f;
+            ident = unit;
+        }
         T.ident = ident ? 1 : 0;
     }
 
@@ -1965,7 +1977,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         TopObject& T = tops[i];
         T.wbox = 0;
         const ObjBVH& ob = s->bvh[T.geom];
-        if (T.ident || ob.root < 0) continue;
+        if ((T.ident && T.kind != 0) || ob.root < 0) continue;   // (a sphere has no root-box test)
         TBox b;
         const HNode& r = ob.nodes[ob.root];
         if (!entry_world_box(top_model[i], r.mn, r.mx, geoms[T.geom].prune_pad, T.blur, b)) continue;

@@ -10,6 +10,7 @@ import pytest
 import pyoracle
 import rtg
 from rtg import scenegen
+from rtg import _abi as A
 
 pytestmark = pytest.mark.gpu
 
@@ -212,6 +213,45 @@ def test_trace_transformed_entries_any_time_matches_oracle(gpu):
             assert np.array_equal(h["t"][m].view(np.int32), ref["t"][m].view(np.int32))
             assert np.array_equal(h["point"][m].view(np.int32), ref["point"][m].view(np.int32))
             assert np.array_equal(h["normal"][m].view(np.int32), ref["normal"][m].view(np.int32))
+
+
+@pytest.mark.parametrize("name", ["cornell_pt", "spheres_small"])
+def test_trace_untransformed_spheres_signed_zeros_matches_oracle(gpu, name):
+    """Untransformed spheres (inverse = identity up to the signs of its zeros, zero blur) skip the
+    ray transform (TopObject::ident, rtg_host.cpp): the world ray equals the object-space ray in value,
+    not always in the signs of its zeros.  Origins and directions with components of exactly +0 and
+    -0, aimed at the sphere centres or at random, against the literal oracle (hit records and the
+    shading point / normal bitwise), pruned and exhaustive."""
+    sc = scenegen.cornell_pt(32, 24, spp=1) if name == "cornell_pt" else scenegen.spheres(32, 24, spp=1, n=64)
+    rng = np.random.default_rng(47)
+    n = 8000
+    cen = np.asarray([np.asarray(sc.vertices)[ob.center - 1] for ob in sc.objects
+                      if ob.type == A.OBJ_SPHERE], np.float64)
+    lo = np.asarray(sc.vertices).min(0) - 2
+    hi = np.asarray(sc.vertices).max(0) + 2
+    o = rng.uniform(lo, hi, (n, 3))
+    tgt = cen[rng.integers(0, len(cen), n)]
+    d = np.where(rng.random((n, 1)) < 0.7, tgt - o, rng.standard_normal((n, 3)))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    sgn = np.where(rng.random((n, 3)) < 0.5, -0.0, 0.0)
+    zd = rng.random((n, 3)) < 0.15
+    d[zd] = sgn[zd]
+    d[np.all(d == 0, axis=1), 1] = -1.0
+    zo = rng.random((n, 3)) < 0.15
+    o[zo] = np.where(rng.random((n, 3)) < 0.5, -0.0, 0.0)[zo]
+    o, d = o.astype(np.float32), d.astype(np.float32)
+    t = np.zeros(n, np.float32)
+    ref = pyoracle.Oracle(sc).trace(o, d, t)
+    assert (ref["object"] >= 0).mean() > 0.3
+    with rtg.Renderer(sc, device=gpu) as r:
+        for trav in (0, 1):
+            h = r.trace(o, d, t, traversal=trav)
+            assert np.array_equal(h["full"], ref["full"])
+            assert np.array_equal(h["object"], ref["object"])
+            assert np.array_equal(h["prim"], ref["prim"])
+            m = ref["full"] == 1
+            for k in ("t", "point", "normal"):
+                assert np.array_equal(h[k][m].view(np.int32), ref[k][m].view(np.int32)), k
 
 
 @pytest.mark.parametrize("block", [1, 2, 4, 5, 8])
