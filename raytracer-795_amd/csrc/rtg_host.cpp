@@ -2078,7 +2078,21 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
     s->num_gtris = (int)gtris.size();
     s->num_gents = (int)gents.size();
     std::vector<TopObject> gtop;
-    if (!gents.empty()) gtop.push_back(tops[gents[0].entry]);
+    if (!gents.empty()) {
+        gtop.push_back(tops[gents[0].entry]);
+        // The group's transform the identity up to the signs of its zeros, zero blur (untransformed
+        // meshes): flat_group takes transform_ray's identity path (o + 0, d + 0).  The group runs only
+        // for finite rays whose direction components are all nonzero (fast), so d2 is d bit for bit
+        // and o2 equals o in value; every division the group's tests do is by a direction component or
+        // by a determinant of edges and direction, neither of which involves o2, and the rest compares
+        // values -- the hit record is the same (t > 0 is required, so its bits are too).
+        TopObject& G0 = gtop[0];
+        bool unit = true;
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 3; r++) unit = unit && G0.inv[c * 4 + r] == (c == r ? 1.0f : 0.0f);
+        for (int k = 0; k < 3; k++) unit = unit && G0.blur[k] == 0.0f;
+        if (unit) G0.ident = 1;
+    }
     bs.flat_group_entries = s->num_gents;
 
     // materials, textures, lights
