@@ -347,8 +347,11 @@ DEV bool ray_finite(f3 o, f3 d, float time) {
     const float s = (((o.x * 0.0f + o.y * 0.0f) + (o.z * 0.0f + d.x * 0.0f)) + (d.y * 0.0f + d.z * 0.0f)) + time * 0.0f;
     return s == 0.0f;       // x * 0 is NaN exactly for x = +-inf or NaN
 }
-DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d2, bool fin) {
-    if (T.ident && fin) {
+// strict: only the +0 identity (ident == 1) returns the ray -- hit_record, whose sphere texture
+// coordinates (atan2) and normals see the signs of zeros; the traversal also takes ident == 2 (the
+// identity up to zero signs, rtg_host.cpp), whose outcomes depend on values only.
+DEV void transform_ray(const TopObject& T, f3 o, f3 d, float time, f3& o2, f3& d2, bool fin, bool strict = false) {
+    if ((strict ? T.ident == 1 : T.ident != 0) && fin) {
         // identity inverse, +0 blur: (x*1 + y*0) + (z*0 + w*0) == x + 0 for finite inputs
         // (the only effect is -0 -> +0)
         o2 = mk(o.x + 0.0f, o.y + 0.0f, o.z + 0.0f);
@@ -1271,7 +1274,7 @@ DEV Ret hit_record(const SceneView& sv, f3 o, f3 d, float time, const HitRec& h)
     const TopObject& T = sv.tops[h.obj];
     const Geometry& g = sv.geoms[T.geom];
     f3 o2, d2;
-    transform_ray(T, o, d, time, o2, d2, ray_finite(o, d, time));
+    transform_ray(T, o, d, time, o2, d2, ray_finite(o, d, time), /*strict=*/true);
     Ret ret;
     ret.matIndex = T.material;
     ret.dm = RTG_DECAL_NONE;

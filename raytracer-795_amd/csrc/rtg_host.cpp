@@ -1952,9 +1952,10 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             for (int c = 0; c < 4; c++)
                 for (int r = 0; r < 3; r++) unit = unit && T.inv[c * 4 + r] == (c == r ? 1.0f : 0.0f);
             for (int k = 0; k < 3; k++) unit = unit && T.blur[k] == 0.0f;
-            ident = unit;
+            T.ident = unit ? 2 : 0;    // (hit_record keeps the product: transform_ray's strict)
+        } else {
+            T.ident = ident ? 1 : 0;
         }
-        T.ident = ident ? 1 : 0;
     }
 
     std::vector<SphereEnt> tsph(tops.size());
@@ -2091,7 +2092,7 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
         for (int c = 0; c < 4; c++)
             for (int r = 0; r < 3; r++) unit = unit && G0.inv[c * 4 + r] == (c == r ? 1.0f : 0.0f);
         for (int k = 0; k < 3; k++) unit = unit && G0.blur[k] == 0.0f;
-        if (unit) G0.ident = 1;
+        if (unit && !G0.ident) G0.ident = 2;
     }
     bs.flat_group_entries = s->num_gents;
 

@@ -39,8 +39,9 @@ struct TopObject {
     int material;           // 1-based (instance override applied)
     int geom;               // index of the geometry (base mesh for instances)
     int is_instance;
-    int ident;              // inv is exactly the identity (+0 off-diagonal) and blur is +0, or a sphere's
-                            // inv is the identity up to zero signs and its blur zero (rtg_host.cpp)
+    int ident;              // 1: inv is exactly the identity (+0 off-diagonal) and blur is +0; 2: a sphere's
+                            // inv is the identity up to zero signs and its blur zero (rtg_host.cpp;
+                            // traversal only, transform_ray's strict)
     int wbox;               // wlo / whi valid: a transformed entry's world box (root box + eps overhang
     float wlo[3], whi[3];   // through the model matrix, blur sweep for times in [0, 1], margins)
     int grouped;            // a member of the flat group (SceneView::gents): fast rays test it there
