@@ -931,6 +931,9 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
     return true;
 }
 
+#ifndef RTG_BSPH
+#define RTG_BSPH 1            // the transformed meshes' bounding-sphere skip (A/B: 0)
+#endif
 // ecyc (STATS): per-entry wave-cycle accumulators in LDS (the kernel flushes them to Counters); the
 // flat group's cycles are charged to slot 15
 template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool UNI = false>
@@ -976,6 +979,15 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                 const float le = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
                 const float e = (fabsf(sl) + fabsf(le)) * 3.814697265625e-6f + 1e-30f;   // 2^-18
                 skip = sl + e < le - e;
+                // the bounding sphere (TopObject::bsph): the line's squared distance from its centre,
+                // |oc x d|^2 / |d|^2, against r^2 plus 3e-5 |oc|^2 (the rounding here and the object-space
+                // line's offset for far origins); NaN / inf compare false (entry kept)
+                if (!skip && RTG_BSPH && T.bsph) {
+                    const f3 oc = o - mk(T.bs[0], T.bs[1], T.bs[2]);
+                    const f3 cr = cross(oc, d);
+                    const float dd = dot(d, d);
+                    skip = dot(cr, cr) > T.bs[3] * dd + 3e-5f * (dot(oc, oc) * dd);
+                }
             }
             if (!skip) {
                 if (STATS) st.entries++;

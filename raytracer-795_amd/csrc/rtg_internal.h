@@ -45,6 +45,11 @@ struct TopObject {
     int wbox;               // wlo / whi valid: a transformed entry's world box (root box + eps overhang
     float wlo[3], whi[3];   // through the model matrix, blur sweep for times in [0, 1], margins)
     int grouped;            // a member of the flat group (SceneView::gents): fast rays test it there
+    // round 6: a transformed mesh entry (wbox) whose world-space bounding sphere is much tighter than its
+    // world box: centre + squared radius (vertices through the model matrix, blur sweep, the eps
+    // overhang and margins); the object loop skips the entry for a lane whose ray line misses it
+    int bsph;
+    float bs[4];
 };
 // A sphere entry's test data (SceneView::tsph, one per entry, round 6): the object loop tests a sphere
 // from this 32-byte record, whose address depends only on the entry index -- not on a dependent load

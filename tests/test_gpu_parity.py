@@ -254,6 +254,40 @@ def test_trace_untransformed_spheres_signed_zeros_matches_oracle(gpu, name):
                 assert np.array_equal(h[k][m].view(np.int32), ref[k][m].view(np.int32)), k
 
 
+def test_trace_bounding_sphere_silhouette_matches_oracle(gpu):
+    """Transformed meshes whose world bounding sphere is tight (TopObject::bsph: cornell_pt's scaled,
+    translated icosphere) are skipped by lanes whose ray line misses the sphere.  Rays grazing the
+    sphere's silhouette (0.97-1.03 of its radius) from near and far origins (up to 400 units), against
+    the literal oracle, pruned and exhaustive."""
+    sc = scenegen.cornell_pt(32, 24, spp=1)
+    rng = np.random.default_rng(59)
+    n = 8000
+    c = np.array([-1.2, 1.4, -2.0])
+    u = rng.standard_normal((n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    dist = np.where(rng.random(n) < 0.5, rng.uniform(1.5, 12.0, n), rng.uniform(12.0, 400.0, n))
+    o = c + u * dist[:, None]
+    # a target on a random tangent offset: the line passes at 0.97-1.03 x 1.4 from the centre
+    w = rng.standard_normal((n, 3))
+    w -= (w * u).sum(1, keepdims=True) * u
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    tgt = c + w * (1.4 * rng.uniform(0.97, 1.03, n))[:, None]
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o, d = o.astype(np.float32), d.astype(np.float32)
+    t = np.zeros(n, np.float32)
+    ref = pyoracle.Oracle(sc).trace(o, d, t)
+    ico = next(k for k, ob in enumerate(sc.objects) if ob.type == A.OBJ_MESH and ob.xforms)
+    assert (ref["object"] == ico).mean() > 0.05
+    with rtg.Renderer(sc, device=gpu) as r:
+        for trav in (0, 1):
+            h = r.trace(o, d, t, traversal=trav)
+            assert np.array_equal(h["object"], ref["object"])
+            assert np.array_equal(h["prim"], ref["prim"])
+            m = ref["full"] == 1
+            assert np.array_equal(h["t"][m].view(np.int32), ref["t"][m].view(np.int32))
+
+
 @pytest.mark.parametrize("block", [1, 2, 4, 5, 8])
 def test_row_shards_sum_to_full_frame(gpu, block):
     """Multi-GPU partition (rows (y // block) % G == rank, incl. a partial last block) +
