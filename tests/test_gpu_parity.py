@@ -254,30 +254,41 @@ def test_trace_untransformed_spheres_signed_zeros_matches_oracle(gpu, name):
                 assert np.array_equal(h[k][m].view(np.int32), ref[k][m].view(np.int32)), k
 
 
-def test_trace_bounding_sphere_silhouette_matches_oracle(gpu):
-    """Transformed meshes whose world bounding sphere is tight (TopObject::bsph: cornell_pt's scaled,
-    translated icosphere) are skipped by lanes whose ray line misses the sphere.  Rays grazing the
-    sphere's silhouette (0.97-1.03 of its radius) from near and far origins (up to 400 units), against
-    the literal oracle, pruned and exhaustive."""
-    sc = scenegen.cornell_pt(32, 24, spp=1)
+@pytest.mark.parametrize("name", ["cornell_pt", "dragon_small"])
+def test_trace_bounding_sphere_silhouette_matches_oracle(gpu, name):
+    """Mesh entries with a world box whose world bounding sphere is tight (TopObject::bsph: cornell_pt's
+    scaled, translated icosphere; the dragon's displaced sphere, untransformed but with glm's signed-zero
+    inverse) are skipped by lanes whose ray line misses the sphere.  Rays grazing the sphere's
+    silhouette (0.97-1.03 of its radius) from near and far origins (up to 400 units), a quarter of them
+    turned away (the sphere behind the origin: its parameter test), against the literal oracle, pruned
+    and exhaustive."""
     rng = np.random.default_rng(59)
     n = 8000
-    c = np.array([-1.2, 1.4, -2.0])
+    if name == "cornell_pt":
+        sc = scenegen.cornell_pt(32, 24, spp=1)
+        c, rad = np.array([-1.2, 1.4, -2.0]), 1.4
+        ico = next(k for k, ob in enumerate(sc.objects) if ob.type == A.OBJ_MESH and ob.xforms)
+    else:
+        sc = scenegen.dragon1m(32, 24, spp=1, nu=80, nv=40)
+        ico = next(k for k, ob in enumerate(sc.objects) if ob.type == A.OBJ_MESH and len(ob.faces) > 100)
+        v = np.asarray(sc.vertices, np.float64)[np.unique(np.asarray(sc.objects[ico].faces)) - 1]
+        c = 0.5 * (v.min(0) + v.max(0))
+        rad = np.sqrt(((v - c) ** 2).sum(1)).max()
     u = rng.standard_normal((n, 3))
     u /= np.linalg.norm(u, axis=1, keepdims=True)
     dist = np.where(rng.random(n) < 0.5, rng.uniform(1.5, 12.0, n), rng.uniform(12.0, 400.0, n))
     o = c + u * dist[:, None]
-    # a target on a random tangent offset: the line passes at 0.97-1.03 x 1.4 from the centre
+    # a target on a random tangent offset: the line passes at 0.97-1.03 x the radius from the centre
     w = rng.standard_normal((n, 3))
     w -= (w * u).sum(1, keepdims=True) * u
     w /= np.linalg.norm(w, axis=1, keepdims=True)
-    tgt = c + w * (1.4 * rng.uniform(0.97, 1.03, n))[:, None]
+    tgt = c + w * (rad * rng.uniform(0.97, 1.03, n))[:, None]
     d = tgt - o
     d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d[rng.random(n) < 0.25] *= -1.0       # the sphere behind the origin (the parameter test)
     o, d = o.astype(np.float32), d.astype(np.float32)
     t = np.zeros(n, np.float32)
     ref = pyoracle.Oracle(sc).trace(o, d, t)
-    ico = next(k for k, ob in enumerate(sc.objects) if ob.type == A.OBJ_MESH and ob.xforms)
     assert (ref["object"] == ico).mean() > 0.05
     with rtg.Renderer(sc, device=gpu) as r:
         for trav in (0, 1):
