@@ -1989,9 +1989,10 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
             fin = fin && std::isfinite(T.wlo[z]) && std::isfinite(T.whi[z]);
         }
         T.wbox = fin ? 1 : 0;
-        // the bounding sphere (TopObject::bsph): a mesh's vertices through the model matrix (double),
-        // centred on their box's middle and half the blur sweep, radius + |blur| / 2 + the eps overhang
-        // through the matrix (Frobenius norm) + the world box's margin.  The device test adds 3e-5 |oc|^2
+        // the bounding sphere (TopObject::bsph): centre c0 = M (root box middle), radius the largest
+        // distance of a triangle corner through the model matrix (double; one parallel pass, no storage),
+        // then the blur sweep (centre + blur / 2, radius + |blur| / 2), the eps overhang through the
+        // matrix (Frobenius norm) and the world box's margin.  The device test adds 3e-5 |oc|^2
         // (squared) for its own rounding and the object-space line's (far origins: a skipped line has
         // |oc| > r, so that slack is >= 1e-5 |oc|, above the transform's ~2e-7 cond |o|); taken only for a
         // well-conditioned matrix and a sphere of at most 60 % of the box's volume.
@@ -2006,45 +2007,48 @@ static int build_scene(rtg_scene* s, const rtg_scene_desc* d) {
                     fri += (double)T.inv[c * 4 + r] * T.inv[c * 4 + r];
                 }
             fro = std::sqrt(fro); fri = std::sqrt(fri);
-            double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, scale = 0.0;
-            std::vector<double> wv;
-            wv.reserve((size_t)gg.nprims * 9);
-            bool okv = std::isfinite(fro) && std::isfinite(fri) && fro * fri <= 6.0;   // 3 for a similarity
-            for (int k = gg.prim_base; okv && k < gg.prim_base + gg.nprims; k++) {
-                const TriGeom& tg = tris[k];
-                const double a[3] = {tg.p0.x, tg.p0.y, tg.p0.z};
-                const double amb[3] = {tg.p0.w, tg.p1.x, tg.p1.y}, amc[3] = {tg.p1.z, tg.p1.w, tg.p2.x};
-                for (int q = 0; q < 3; q++) {
-                    double v[3];
-                    for (int z = 0; z < 3; z++) v[z] = a[z] - (q == 1 ? amb[z] : q == 2 ? amc[z] : 0.0);
-                    for (int r = 0; r < 3; r++) {
-                        const double w = (double)M.c[0][r] * v[0] + (double)M.c[1][r] * v[1] + (double)M.c[2][r] * v[2] + (double)M.c[3][r];
-                        okv = okv && std::isfinite(w);
-                        lo[r] = std::min(lo[r], w); hi[r] = std::max(hi[r], w);
-                        scale = std::max(scale, std::fabs(w));
-                        wv.push_back(w);
+            if (std::isfinite(fro) && std::isfinite(fri) && fro * fri <= 6.0) {     // 3 for a similarity
+                double c0[3];
+                const HNode& rt = ob.nodes[ob.root];
+                const double m[3] = {0.5 * ((double)rt.mn[0] + rt.mx[0]), 0.5 * ((double)rt.mn[1] + rt.mx[1]),
+                                     0.5 * ((double)rt.mn[2] + rt.mx[2])};
+                for (int r = 0; r < 3; r++) {
+                    c0[r] = (double)M.c[0][r] * m[0] + (double)M.c[1][r] * m[1] + (double)M.c[2][r] * m[2] + (double)M.c[3][r];
+                }
+                std::vector<double> part(build_threads(), 0.0);
+                parallel_chunks((size_t)gg.nprims, 65536, [&](int ch, size_t b0, size_t b1) {
+                    double mx2 = 0.0;
+                    for (size_t k = (size_t)gg.prim_base + b0; k < (size_t)gg.prim_base + b1; k++) {
+                        const TriGeom& tg = tris[k];
+                        const double a[3] = {tg.p0.x, tg.p0.y, tg.p0.z};
+                        const double e[2][3] = {{tg.p0.w, tg.p1.x, tg.p1.y}, {tg.p1.z, tg.p1.w, tg.p2.x}};
+                        for (int q = 0; q < 3; q++) {
+                            double v[3], d2 = 0.0;
+                            for (int z = 0; z < 3; z++) v[z] = q == 0 ? a[z] : a[z] - e[q - 1][z];
+                            for (int r = 0; r < 3; r++) {
+                                const double w = (double)M.c[0][r] * v[0] + (double)M.c[1][r] * v[1] +
+                                                 (double)M.c[2][r] * v[2] + (double)M.c[3][r] - c0[r];
+                                d2 += w * w;
+                            }
+                            mx2 = d2 > mx2 || d2 != d2 ? d2 : mx2;    // NaN propagates (no sphere)
+                        }
                     }
-                }
-            }
-            if (okv) {
-                double c[3], r2 = 0.0, bl = 0.0, ext = 0.0, vol = 1.0;
+                    part[ch] = mx2;
+                });
+                double r2 = 0.0, bl = 0.0, scale = 0.0, ext = 0.0, vol = 1.0;
+                for (double v : part) r2 = v > r2 || v != v ? v : r2;
                 for (int z = 0; z < 3; z++) {
-                    c[z] = 0.5 * (lo[z] + hi[z]);
                     bl += (double)T.blur[z] * T.blur[z];
-                    ext = std::max(ext, hi[z] - lo[z]);
-                    scale = std::max(scale, std::fabs((double)T.blur[z]));
-                }
-                for (size_t q = 0; q < wv.size(); q += 3) {
-                    const double dx = wv[q] - c[0], dy = wv[q + 1] - c[1], dz = wv[q + 2] - c[2];
-                    r2 = std::max(r2, dx * dx + dy * dy + dz * dz);
+                    scale = std::max(scale, std::max(std::fabs((double)T.wlo[z]), std::fabs((double)T.whi[z])));
+                    ext = std::max(ext, (double)T.whi[z] - (double)T.wlo[z]);
+                    vol *= (double)T.whi[z] - (double)T.wlo[z];
                 }
                 const double rad = std::sqrt(r2) + 0.5 * std::sqrt(bl) + (double)gg.prune_pad * fro +
                                    1e-4 * (scale + ext) + 1e-6;
-                for (int z = 0; z < 3; z++) vol *= (double)T.whi[z] - (double)T.wlo[z];
                 const double svol = 4.18879020478639 * rad * rad * rad;
                 if (std::isfinite(rad) && svol <= 0.6 * vol) {
                     T.bsph = 1;
-                    for (int z = 0; z < 3; z++) T.bs[z] = (float)(c[z] + 0.5 * (double)T.blur[z]);
+                    for (int z = 0; z < 3; z++) T.bs[z] = (float)(c0[z] + 0.5 * (double)T.blur[z]);
                     T.bs[3] = std::nextafter((float)(rad * rad * (1.0 + 1e-6)), FLT_MAX);
                 }
             }
