@@ -936,7 +936,8 @@ DEV bool flat_group(const SceneView& sv, const f3 o, const f3 d, const float tim
 #endif
 // ecyc (STATS): per-entry wave-cycle accumulators in LDS (the kernel flushes them to Counters); the
 // flat group's cycles are charged to slot 15
-template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool UNI = false>
+// BDIST (the path tracer's shadow queries): the bounding sphere's parameter test too (below)
+template <bool EXHAUSTIVE, bool STATS, bool TLAS = false, bool UNI = false, bool BDIST = false>
 DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, int* stack, int sstride, Stats& st,
                        short* tstack = nullptr, bool uni = false, unsigned long long* ecyc = nullptr) {
     HitRec out;
@@ -987,6 +988,23 @@ DEV HitRec closest_hit(const SceneView& sv, f3 o, f3 d, float time, float tmax, 
                     const f3 cr = cross(oc, d);
                     const float dd = dot(d, d);
                     skip = dot(cr, cr) > T.bs[3] * dd + 3e-5f * (dot(oc, oc) * dd);
+                    if (BDIST && !skip) {
+                        // the sphere's parameter interval t* -+ r/|d| (t* = -oc.d/|d|^2, scaled by |d|^2):
+                        // wholly behind the origin (every candidate's gett() <= 0 fails t > 0) or wholly
+                        // beyond tmax / the winner so far (t > nearest fails t < nearest; ties need
+                        // equality, which the slack excludes).  Slack 1e-5 (|o| + |c| + r) |d| + 1e-5
+                        // nearest |d|^2: the object-space t of a matrix with Frobenius product <= 6 (host)
+                        // is the world t up to ~1e-6 of those terms.  Measured: the path tracer's shadow
+                        // queries gain (C5 k_shadow -1.7 ms), the Whitted ones and camera / bounce rays
+                        // lose (profiles/r7/ab_bsph_param_test_dropped.jsonl), so only k_shadow<PT> asks.
+                        const float q = dot(oc, d);
+                        const float dn = __builtin_amdgcn_sqrtf(dd);
+                        const float r = __builtin_amdgcn_sqrtf(T.bs[3]);
+                        const float S = 1e-5f * ((((fabsf(o.x) + fabsf(o.y)) + fabsf(o.z)) +
+                                                  ((fabsf(T.bs[0]) + fabsf(T.bs[1])) + fabsf(T.bs[2])) + r) * dn);
+                        const float rd = r * dn * 1.00001f;
+                        skip = q > rd + S || -q - rd > nearest * dd * 1.00001f + S;
+                    }
                 }
             }
             if (!skip) {
@@ -2567,7 +2585,7 @@ __global__ void __launch_bounds__(kTraceBlock) RTG_SHADOW_ATTR k_shadow(const Sc
         // pixels -- walks wave-uniformly (visit_object)
         constexpr bool KUNI = !EXHAUSTIVE && !TLAS;
         const bool uni = KUNI && sv.uni_walk && __ballot(i < uni_from) == 0ull;
-        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KUNI>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax,
+        HitRec h = closest_hit<EXHAUSTIVE, STATS, TLAS, KUNI, PT>(sv, o, d, so.w, EXHAUSTIVE ? FLT_MAX : tmax,
                                                              s_stack + threadIdx.x, kTraceBlock, st,
                                                              s_tstack + (TLAS ? threadIdx.x : 0), uni,
                                                              STATS ? s_ecyc : nullptr);
